@@ -1,0 +1,237 @@
+/* tt2_capi.h -- C ABI of libtt2.so, the MI355X (gfx950) kernel library behind the
+ * Transformer-TTS mel path (encoder -> decoder -> post-net).
+ *
+ * The reference (keonlee9420/Transformer-tacotron2, /root/reference/README.md:1-3)
+ * ships no code, so it has no FFI to mirror; this ABI is the boundary SURVEY.md
+ * section 8(b) defines: one entry point per fused block of the path, plain
+ * pointers and sizes, no torch types.  INTEGRATION.md shows the ctypes binding.
+ *
+ * Conventions
+ *  - Every device buffer (inputs, outputs, workspace) is allocated by the caller;
+ *    nothing allocates on the hot path, so every call is hipGraph-capturable.
+ *  - Calls are stream-ordered on the caller's stream and reentrant.
+ *  - Return 0 (TT2_OK) or a negative TT2_E_* code; tt2_last_error() returns a
+ *    thread-local message for the last failure on this thread.
+ *  - dtype fields: TT2_DT_F32 = 0, TT2_DT_BF16 = 1.  Activations are
+ *    channels-last row-major [rows, channels]; rows = batch * time.
+ *  - Dropout: keep(idx) = hash(seed, site, idx) >= thr; thr = 0
+ *    disables it.  seed points to a device uint32.
+ */
+#ifndef TT2_CAPI_H
+#define TT2_CAPI_H
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TT2_OK 0
+#define TT2_E_INVALID -1
+#define TT2_E_LAUNCH -2
+#define TT2_E_HIP -3
+
+#define TT2_DT_F32 0
+#define TT2_DT_BF16 1
+
+/* ------------------------------------------------------------------ runtime */
+const char* tt2_last_error(void);
+int tt2_version(void);
+int tt2_init(int device);
+int tt2_set_error(int code, const char* msg);
+int tt2_check_launch(hipError_t err, const char* what);
+
+/* --------------------------------------------------------------------- GEMM
+ * C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)), epi = (+bias[n]) (+res[m,n]) (act)
+ *          (*gate: res==0 ? 0 : gate_scale) (dropout) (+beta*C[m,n]).
+ * trans_a = 0: A(m,k) = a[m*lda + k]; 1: a[k*lda + m].  trans_b likewise for B(n,k).
+ * a_conv_t > 0: A is the implicit im2col of a channels-last sequence batch
+ *   (time = m % a_conv_t, tap = k / a_conv_c, zero outside [0, T)); b_conv_* the
+ *   same for an N-contiguous B (wgrad of a conv).
+ * splits > 1: split-K with an f32 workspace of tt2_gemm_workspace_size() bytes.
+ * Replaces the nn.Linear / nn.Conv1d products of SURVEY 8(a) rows a1, a3-a9, a11. */
+typedef struct tt2_gemm_args {
+  const void* a; const void* b; void* c;
+  const float* bias;
+  const void* res; const void* gate;
+  const uint32_t* drop_seed;
+  void* workspace; size_t ws_bytes;
+  int64_t lda, ldb, ldc, ldr, ldg;
+  int32_t m, n, k;
+  int32_t dtype_in, dtype_out, res_dtype, gate_dtype;
+  int32_t trans_a, trans_b;
+  int32_t act;          /* 0 none, 1 relu, 2 tanh */
+  int32_t splits;
+  float alpha, beta, gate_scale;
+  uint32_t drop_site, drop_thr;
+  float drop_scale;
+  int32_t a_conv_t, a_conv_c, a_conv_pad;
+  int32_t b_conv_t, b_conv_c, b_conv_pad;
+} tt2_gemm_args;
+
+size_t tt2_gemm_workspace_size(const tt2_gemm_args* a);
+int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream);
+
+/* ---------------------------------------------------------------- attention
+ * Scaled dot-product attention over heads of width 64, read in place from
+ * projection outputs: head h of row (b, t) of Q is q[(b*tq + t)*q_ld + 64h].
+ * Key j of batch b is visible iff j < key_len[b] (key_len may be NULL) and,
+ * if causal, j <= t.  A row with no visible key outputs 0.
+ * lse: [batch*heads, tq] f32, log2-domain log-sum-exp of scale*log2(e)*QK^T
+ * (+inf for empty rows); written by fwd, read by bwd.
+ * bwd: delta [batch*heads, tq] f32 scratch; dq/dk/dv may alias column slices
+ * of one fused gradient buffer.  Replaces SURVEY 8(a) a3, a6, a7 (+ a11). */
+typedef struct tt2_attn_args {
+  const void* q; const void* k; const void* v;
+  const void* o;      /* bwd: forward output */
+  const void* dout;   /* bwd: gradient of the output */
+  void* o_out;        /* fwd: output */
+  void* dq; void* dk; void* dv;
+  float* lse; float* delta;
+  int64_t q_ld, k_ld, v_ld, o_ld, do_ld, dq_ld, dk_ld, dv_ld;
+  const int32_t* key_len;
+  int32_t batch, heads, head_dim, tq, tk, causal, dtype;
+  float scale;
+} tt2_attn_args;
+
+int tt2_attn_fwd(const tt2_attn_args* a, hipStream_t stream);
+int tt2_attn_bwd(const tt2_attn_args* a, hipStream_t stream);
+
+/* ------------------------------------------------------------- reductions */
+#define TT2_COLSUM_ROWS 128
+#define TT2_LN_BWD_BLOCKS 256
+#define TT2_BN_ROWS_PER_CHUNK 64
+#define TT2_PE_BWD_BLOCKS 256
+#define TT2_LOSS_BLOCKS 256
+#define TT2_ADAM_NORM_BLOCKS 256
+
+/* dst[c] = beta*dst[c] + sum_r src[r*ld + c] (fixed summation order) */
+typedef struct tt2_reduce_args {
+  const float* src; float* dst;
+  int64_t ld; int32_t rows, cols;
+  float beta;
+} tt2_reduce_args;
+int tt2_reduce_rows(const tt2_reduce_args* a, hipStream_t stream);
+
+/* Bias gradient: dst[n] = beta*dst[n] + sum_m x[m*ld + n]. */
+size_t tt2_colsum_workspace_size(int m, int n);
+int tt2_colsum(const void* x, int dtype, int64_t ld, int m, int n, float* dst, float beta, void* ws,
+               size_t ws_bytes, hipStream_t stream);
+
+/* ------------------------------------------------------------- LayerNorm
+ * fwd: y = LN(x + drop(branch)) (branch may be NULL), mean/rstd [m] f32 saved.
+ * bwd: dx = dL/ds (residual stream), dbranch = drop'(dx); dgamma/dbeta (f32)
+ *      = grad_beta*old + sum over rows.  C must be 512 (d_model).
+ * Replaces the post-LN residual blocks of SURVEY 8(a) a3, a4, a6, a7. */
+typedef struct tt2_ln_args {
+  const void* x; const void* branch; const void* dy;
+  void* y; void* dx; void* dbranch;
+  const float* gamma; const float* beta;
+  float* mean; float* rstd;
+  float* dgamma; float* dbeta;
+  void* workspace; size_t ws_bytes;
+  const uint32_t* drop_seed;
+  int32_t m, c, dtype;
+  float eps, grad_beta;
+  uint32_t drop_site, drop_thr;
+  float drop_scale;
+} tt2_ln_args;
+int tt2_layernorm_fwd(const tt2_ln_args* a, hipStream_t stream);
+size_t tt2_layernorm_bwd_workspace_size(const tt2_ln_args* a);
+int tt2_layernorm_bwd(const tt2_ln_args* a, hipStream_t stream);
+
+/* ------------------------------------------------------------- BatchNorm
+ * fwd: out = drop(act((y - mean)*rstd*gamma + beta)) (+ res), statistics over
+ *      all m rows (training: batch stats + running update; eval: running stats).
+ * bwd: dy from dout (dtype dout_dtype), dgamma/dbeta written (f32).
+ * Replaces the Conv1d+BatchNorm blocks of SURVEY 8(a) a1 (relu) and a9 (tanh). */
+typedef struct tt2_bn_args {
+  const void* y; const void* dout; const void* res;
+  void* out; void* dy;
+  const float* gamma; const float* beta;
+  float* mean; float* rstd;
+  float* run_mean; float* run_var;
+  float* dgamma; float* dbeta;
+  void* workspace; size_t ws_bytes;
+  const uint32_t* drop_seed;
+  int64_t res_ld;  /* row stride of res (elements) */
+  int32_t m, c, act, dtype, out_dtype, res_dtype, dout_dtype, training;
+  float eps, momentum;
+  uint32_t drop_site, drop_thr;
+  float drop_scale;
+} tt2_bn_args;
+size_t tt2_batchnorm_workspace_size(const tt2_bn_args* a);
+int tt2_batchnorm_fwd(const tt2_bn_args* a, hipStream_t stream);
+int tt2_batchnorm_bwd(const tt2_bn_args* a, hipStream_t stream);
+
+/* -------------------------------------------------- embedding / pos. enc. */
+int tt2_embedding_fwd(const int64_t* ids, const void* table, void* out, int m, int c, int vocab, int dtype,
+                      hipStream_t stream);
+/* dtable (f32) is zeroed then scatter-added; rows == pad_idx get no gradient */
+int tt2_embedding_bwd(const int64_t* ids, const void* dout, float* dtable, int m, int c, int vocab, int pad_idx,
+                      int dtype, hipStream_t stream);
+
+/* out = drop(x + alpha*pe[row % t + t_offset]); bwd: dx = drop'(dout), *dalpha = sum dx*pe */
+typedef struct tt2_pe_args {
+  const void* x; const void* dout; void* out; void* dx;
+  const float* alpha; const float* pe; float* dalpha;
+  void* workspace; size_t ws_bytes;
+  const uint32_t* drop_seed;
+  int32_t m, c, t, t_offset, dtype;
+  uint32_t drop_site, drop_thr;
+  float drop_scale;
+} tt2_pe_args;
+int tt2_posenc_fwd(const tt2_pe_args* a, hipStream_t stream);
+size_t tt2_posenc_bwd_workspace_size(void);
+int tt2_posenc_bwd(const tt2_pe_args* a, hipStream_t stream);
+
+/* teacher forcing: out[b*t + j] = j == 0 ? 0 : mel[b, j-1] (mel f32 [batch, t, c]) */
+int tt2_shift_right(const float* mel, void* out, int batch, int t, int c, int dtype, hipStream_t stream);
+int tt2_cast2d(const void* src, int src_dtype, int64_t src_ld, void* dst, int dst_dtype, int64_t dst_ld, int m,
+               int n, hipStream_t stream);
+
+/* ------------------------------------------------------------------- loss
+ * heads [batch*t, heads_ld] f32 (cols 0..n_mels-1 mel_before, col n_mels stop logit),
+ * mel_after [batch*t, n_mels] f32, target f32 [batch, t, n_mels].
+ * loss_out[4] = (total, mse_before, mse_after, bce_stop); gradients: g_heads
+ * (f32, heads_ld; mel cols carry before + after terms), g_after (grad_dtype).
+ * Replaces SURVEY 8(a) a10. */
+typedef struct tt2_loss_args {
+  const float* heads; const float* mel_after; const float* target;
+  const int32_t* mel_len;
+  float* loss_out; float* g_heads; void* g_after;
+  void* workspace; size_t ws_bytes;
+  int64_t heads_ld;
+  int32_t batch, t, n_mels, grad_dtype;
+  float pos_weight;
+  float grad_scale;  /* multiplies every gradient (1/world_size under data parallelism) */
+} tt2_loss_args;
+size_t tt2_loss_workspace_size(void);
+int tt2_tts_loss(const tt2_loss_args* a, hipStream_t stream);
+
+/* conv dgrad weight: wd[ci][tap][co] = w[co][k-1-tap][ci] */
+int tt2_conv_weight_flip(const void* w, void* wd, int cout, int cin, int k, int dtype, hipStream_t stream);
+
+/* -------------------------------------------------------------- optimizer
+ * Fused Adam(W) over the flat f32 parameter buffer with optional global-norm
+ * clipping and Noam warmup (lr * d^-0.5 * min(s^-0.5, s*warmup^-1.5)); writes the
+ * bf16 shadow used by the bf16 kernels.  step is a device counter (step+1 is used). */
+typedef struct tt2_adam_args {
+  float* params; const float* grads; float* exp_avg; float* exp_avg_sq;
+  void* shadow_bf16;
+  int32_t* step;
+  void* workspace; size_t ws_bytes;
+  int64_t n;
+  float lr, beta1, beta2, eps, weight_decay, clip_norm, warmup;
+  int32_t noam, d_model;
+} tt2_adam_args;
+size_t tt2_adam_workspace_size(void);
+int tt2_adam_step(const tt2_adam_args* a, hipStream_t stream);
+/* step += 1; seed += 1 (seed may be NULL) */
+int tt2_step_bump(int32_t* step, uint32_t* seed, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,430 @@
+// misc.hip -- the HBM-bound pieces of the path (gfx950): row reductions,
+// bias gradients, embedding, scaled positional encoding, teacher-forcing input,
+// casts, the fused TTS loss (+ its input gradients), weight repacks and the
+// fused Adam/clip optimizer step.  All grid-stride, 16-B vectorised where the
+// row width allows, deterministic (fixed-order partial sums, no float atomics
+// except the embedding scatter).
+#include <math.h>
+
+#include "tt2_capi.h"
+#include "tt2_common.h"
+
+namespace {
+constexpr int NT = 256;
+
+int grid_for(int64_t total, int per = NT) {
+  int64_t b = (total + per - 1) / per;
+  return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+TT2_DEV float ldf(const void* p, int64_t i, int dt) {
+  return dt == TT2_BF16 ? (float)reinterpret_cast<const bf16*>(p)[i] : reinterpret_cast<const float*>(p)[i];
+}
+TT2_DEV void stf(void* p, int64_t i, int dt, float v) {
+  if (dt == TT2_BF16) reinterpret_cast<bf16*>(p)[i] = (bf16)v;
+  else reinterpret_cast<float*>(p)[i] = v;
+}
+
+// dst[c] = beta * dst[c] + sum_r src[r * ld + c]   (fixed order)
+__global__ void reduce_rows_kernel(const float* src, int rows, int cols, int64_t ld, float* dst, float beta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) s += src[(int64_t)r * ld + c];
+  dst[c] = beta != 0.f ? beta * dst[c] + s : s;
+}
+
+// partial column sums of a [M, N] matrix: part[blockIdx.y][n]
+__global__ void colsum_partial_kernel(const void* x, int dt, int64_t ld, int M, int N, int rows_per, float* part) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += ldf(x, (int64_t)r * ld + n, dt);
+  part[(int64_t)blockIdx.y * N + n] = s;
+}
+
+// ------------------------------------------------------------ embedding
+template <typename T>
+__global__ void embed_fwd_kernel(const int64_t* ids, const T* table, T* out, int M, int C, int V) {
+  const int64_t total = (int64_t)M * C;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int m = (int)(i / C), c = (int)(i % C);
+    const int64_t id = ids[m];
+    out[i] = (id >= 0 && id < V) ? table[id * C + c] : from_f32<T>(0.f);
+  }
+}
+template <typename T>
+__global__ void embed_bwd_kernel(const int64_t* ids, const T* dout, float* dtable, int M, int C, int V, int pad_idx) {
+  const int64_t total = (int64_t)M * C;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int m = (int)(i / C), c = (int)(i % C);
+    const int64_t id = ids[m];
+    if (id >= 0 && id < V && id != pad_idx) atomicAdd(&dtable[id * C + c], to_f32(dout[i]));
+  }
+}
+
+// ------------------------------------------------------ positional encoding
+// out = drop(x + alpha * pe[t]),  t = row % T
+template <typename T>
+__global__ void pe_fwd_kernel(const T* x, const float* alpha, const float* pe, T* out, int M, int C, int Tlen,
+                              int t_off, DropDesc drop) {
+  const int64_t total = (int64_t)M * C;
+  const float al = *alpha;
+  const uint32_t seed = drop.thr ? *drop.seed : 0u;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int m = (int)(i / C), c = (int)(i % C);
+    const int t = m % Tlen + t_off;
+    float v = to_f32(x[i]) + al * pe[(int64_t)t * C + c];
+    if (drop.thr) v = drop_apply(drop, seed, (uint32_t)i, v);
+    out[i] = from_f32<T>(v);
+  }
+}
+// dx = drop'(dout); part[block] = sum dx * pe
+template <typename T>
+__global__ __launch_bounds__(NT) void pe_bwd_kernel(const T* dout, const float* pe, T* dx, float* part, int M, int C,
+                                                    int Tlen, DropDesc drop) {
+  __shared__ float red[NT / 64];
+  const int64_t total = (int64_t)M * C;
+  const uint32_t seed = drop.thr ? *drop.seed : 0u;
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int m = (int)(i / C), c = (int)(i % C);
+    const int t = m % Tlen;
+    float g = to_f32(dout[i]);
+    if (drop.thr) g = drop_apply(drop, seed, (uint32_t)i, g);
+    dx[i] = from_f32<T>(g);
+    s += g * pe[(int64_t)t * C + c];
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < NT / 64; ++w) t += red[w];
+    part[blockIdx.x] = t;
+  }
+}
+
+// ------------------------------------------------------ teacher forcing input
+// out[b*T + t, c] = t == 0 ? 0 : mel[b, t-1, c]
+template <typename T>
+__global__ void shift_right_kernel(const float* mel, T* out, int B, int Tlen, int C) {
+  const int64_t total = (int64_t)B * Tlen * C;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int64_t m = i / C;
+    const int t = (int)(m % Tlen);
+    out[i] = from_f32<T>(t == 0 ? 0.f : mel[i - C]);
+  }
+}
+
+__global__ void cast2d_kernel(const void* src, int sdt, int64_t sld, void* dst, int ddt, int64_t dld, int M, int N) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int m = (int)(i / N), n = (int)(i % N);
+    stf(dst, (int64_t)m * dld + n, ddt, ldf(src, (int64_t)m * sld + n, sdt));
+  }
+}
+
+// ------------------------------------------------------------------- loss
+// heads [M, hld] f32: cols 0..79 mel_before, col 80 stop logit.  after [M, 80] f32.
+// Writes: part[block][4] = (sum sq before, sum sq after, sum bce, 0);
+//         g_heads[m, 0..79] = d/dbefore (direct + residual from after), g_heads[m, 80] = d/dstop,
+//         g_heads[m, 81..hld) = 0; g_after[m, c] (T) = d/dafter.
+template <typename T>
+__global__ __launch_bounds__(NT) void loss_kernel(const float* heads, int64_t hld, const float* after,
+                                                  const float* target, const int32_t* mel_len, int B, int Tlen,
+                                                  int NM, float pos_weight, float gscale, float* g_heads, T* g_after, float* part) {
+  __shared__ float red[3][NT / 64];
+  int nvalid = 0;
+  for (int b = 0; b < B; ++b) nvalid += min(max(mel_len[b], 0), Tlen);
+  const float inv_n = nvalid > 0 ? gscale / nvalid : 0.f;
+  const float inv_nm = inv_n / NM;
+  const int M = B * Tlen;
+  const int64_t total = (int64_t)M * hld;
+  float sb = 0.f, sa = 0.f, ss = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int m = (int)(i / hld), c = (int)(i % hld);
+    const int b = m / Tlen, t = m % Tlen;
+    const int len = mel_len[b];
+    const bool valid = t < len;
+    float g = 0.f;
+    if (c < NM) {
+      const int64_t j = (int64_t)m * NM + c;
+      const float db = heads[i] - target[j];
+      const float da = after[j] - target[j];
+      float ga = 0.f;
+      if (valid) {
+        sb += db * db;
+        sa += da * da;
+        g = 2.f * db * inv_nm;
+        ga = 2.f * da * inv_nm;
+      }
+      g_after[j] = from_f32<T>(ga);
+      g += ga;  // mel_after = mel_before + postnet(mel_before): residual path
+    } else if (c == NM) {
+      const float x = heads[i];
+      const float y = (t == len - 1) ? 1.f : 0.f;
+      if (valid) {
+        // BCEWithLogits(pos_weight): l = -[pw*y*log s(x) + (1-y)*log(1-s(x))]
+        const float lsp = fminf(x, 0.f) - log1pf(expf(-fabsf(x)));   // log sigmoid(x)
+        const float lsn = fminf(-x, 0.f) - log1pf(expf(-fabsf(x)));  // log sigmoid(-x)
+        ss += -(pos_weight * y * lsp + (1.f - y) * lsn);
+        const float sg = 1.f / (1.f + expf(-x));
+        g = (pos_weight * y * (sg - 1.f) + (1.f - y) * sg) * inv_n;
+      }
+    }
+    g_heads[i] = g;
+  }
+  sb = wave_sum(sb); sa = wave_sum(sa); ss = wave_sum(ss);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = sb; red[1][w] = sa; red[2][w] = ss; }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    float t = 0.f;
+    for (int k = 0; k < NT / 64; ++k) t += red[threadIdx.x][k];
+    part[blockIdx.x * 4 + threadIdx.x] = t;
+  }
+}
+
+__global__ void loss_finalize_kernel(const float* part, int nblocks, const int32_t* mel_len, int B, int Tlen, int NM,
+                                     float* out) {
+  if (threadIdx.x != 0) return;
+  int nvalid = 0;
+  for (int b = 0; b < B; ++b) nvalid += min(max(mel_len[b], 0), Tlen);
+  float s[3] = {0.f, 0.f, 0.f};
+  for (int k = 0; k < 3; ++k)
+    for (int i = 0; i < nblocks; ++i) s[k] += part[i * 4 + k];
+  const float n = nvalid > 0 ? (float)nvalid : 1.f;
+  out[1] = s[0] / (n * NM);
+  out[2] = s[1] / (n * NM);
+  out[3] = s[2] / n;
+  out[0] = out[1] + out[2] + out[3];
+}
+
+// ------------------------------------------------------------ weight repack
+// conv dgrad weight: wd[ci][tap'][co] = w[co][K-1-tap'][ci]
+template <typename T>
+__global__ void conv_wflip_kernel(const T* w, T* wd, int Cout, int Cin, int K) {
+  const int64_t total = (int64_t)Cout * Cin * K;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int ci = (int)(i / ((int64_t)K * Cout));
+    const int rem = (int)(i % ((int64_t)K * Cout));
+    const int tp = rem / Cout, co = rem % Cout;
+    wd[i] = w[((int64_t)co * K + (K - 1 - tp)) * Cin + ci];
+  }
+}
+
+// ------------------------------------------------------------------ Adam
+__global__ __launch_bounds__(NT) void sumsq_kernel(const float* g, int64_t n, float* part) {
+  __shared__ float red[NT / 64];
+  float s = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) s += g[i] * g[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < NT / 64; ++w) t += red[w];
+    part[blockIdx.x] = t;
+  }
+}
+
+struct AdamArgs {
+  float* p; const float* g; float* m; float* v; bf16* shadow;
+  int64_t n;
+  const float* norm_part; int n_part;   // clip: sum of partial squared norms
+  int32_t* step;                        // device step counter (read; bumped by tt2_step_bump)
+  float lr, beta1, beta2, eps, wd, clip, warmup, d_model_rsqrt;
+  int noam;
+};
+
+__global__ __launch_bounds__(NT) void adam_kernel(AdamArgs a) {
+  const int step = *a.step + 1;
+  float scale = 1.f;
+  if (a.clip > 0.f && a.norm_part) {
+    float s = 0.f;
+    for (int i = 0; i < a.n_part; ++i) s += a.norm_part[i];
+    const float nrm = sqrtf(s);
+    if (nrm > a.clip) scale = a.clip / (nrm + 1e-6f);
+  }
+  float lr = a.lr;
+  if (a.noam) lr = a.lr * a.d_model_rsqrt * fminf(rsqrtf((float)step), step * powf(a.warmup, -1.5f));
+  const float bc1 = 1.f - powf(a.beta1, (float)step);
+  const float bc2 = 1.f - powf(a.beta2, (float)step);
+  const float step_size = lr / bc1;
+  const float bc2_sqrt = sqrtf(bc2);
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * NT) {
+    const float g = a.g[i] * scale;
+    float p = a.p[i];
+    if (a.wd != 0.f) p -= lr * a.wd * p;  // decoupled (AdamW) weight decay
+    const float m = a.beta1 * a.m[i] + (1.f - a.beta1) * g;
+    const float v = a.beta2 * a.v[i] + (1.f - a.beta2) * g * g;
+    a.m[i] = m;
+    a.v[i] = v;
+    p -= step_size * m / (sqrtf(v) / bc2_sqrt + a.eps);
+    a.p[i] = p;
+    if (a.shadow) a.shadow[i] = (bf16)p;
+  }
+}
+
+__global__ void step_bump_kernel(int32_t* step, uint32_t* seed) {
+  if (threadIdx.x == 0) {
+    step[0] += 1;
+    if (seed) seed[0] += 1u;
+  }
+}
+
+}  // namespace
+
+// =============================================================== C ABI
+extern "C" int tt2_reduce_rows(const tt2_reduce_args* p, hipStream_t s) {
+  if (p->cols <= 0) return TT2_OK;
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((p->cols + 255) / 256), dim3(256), 0, s, p->src, p->rows, p->cols,
+                     p->ld, p->dst, p->beta);
+  return tt2_check_launch(hipGetLastError(), "tt2_reduce_rows");
+}
+
+extern "C" size_t tt2_colsum_workspace_size(int m, int n) {
+  const int R = (m + TT2_COLSUM_ROWS - 1) / TT2_COLSUM_ROWS;
+  return (size_t)R * n * sizeof(float);
+}
+
+extern "C" int tt2_colsum(const void* x, int dtype, int64_t ld, int m, int n, float* dst, float beta, void* ws,
+                          size_t ws_bytes, hipStream_t s) {
+  if (n <= 0) return TT2_OK;
+  if (ws_bytes < tt2_colsum_workspace_size(m, n)) return tt2_set_error(TT2_E_INVALID, "tt2_colsum: workspace");
+  const int R = (m + TT2_COLSUM_ROWS - 1) / TT2_COLSUM_ROWS;
+  float* part = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3((n + 255) / 256, R), dim3(256), 0, s, x, dtype, ld, m, n,
+                     TT2_COLSUM_ROWS, part);
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, R, n, (int64_t)n, dst, beta);
+  return tt2_check_launch(hipGetLastError(), "tt2_colsum");
+}
+
+extern "C" int tt2_embedding_fwd(const int64_t* ids, const void* table, void* out, int m, int c, int vocab,
+                                 int dtype, hipStream_t s) {
+  const int g = grid_for((int64_t)m * c);
+  if (dtype == TT2_DT_BF16)
+    hipLaunchKernelGGL(embed_fwd_kernel<bf16>, dim3(g), dim3(NT), 0, s, ids, (const bf16*)table, (bf16*)out, m, c, vocab);
+  else
+    hipLaunchKernelGGL(embed_fwd_kernel<float>, dim3(g), dim3(NT), 0, s, ids, (const float*)table, (float*)out, m, c,
+                       vocab);
+  return tt2_check_launch(hipGetLastError(), "tt2_embedding_fwd");
+}
+
+extern "C" int tt2_embedding_bwd(const int64_t* ids, const void* dout, float* dtable, int m, int c, int vocab,
+                                 int pad_idx, int dtype, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(dtable, 0, (size_t)vocab * c * sizeof(float), s);
+  if (e != hipSuccess) return tt2_check_launch(e, "tt2_embedding_bwd memset");
+  const int g = grid_for((int64_t)m * c);
+  if (dtype == TT2_DT_BF16)
+    hipLaunchKernelGGL(embed_bwd_kernel<bf16>, dim3(g), dim3(NT), 0, s, ids, (const bf16*)dout, dtable, m, c, vocab,
+                       pad_idx);
+  else
+    hipLaunchKernelGGL(embed_bwd_kernel<float>, dim3(g), dim3(NT), 0, s, ids, (const float*)dout, dtable, m, c,
+                       vocab, pad_idx);
+  return tt2_check_launch(hipGetLastError(), "tt2_embedding_bwd");
+}
+
+extern "C" int tt2_posenc_fwd(const tt2_pe_args* p, hipStream_t s) {
+  DropDesc d{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
+  const int g = grid_for((int64_t)p->m * p->c);
+  if (p->dtype == TT2_DT_BF16)
+    hipLaunchKernelGGL(pe_fwd_kernel<bf16>, dim3(g), dim3(NT), 0, s, (const bf16*)p->x, p->alpha, p->pe,
+                       (bf16*)p->out, p->m, p->c, p->t, p->t_offset, d);
+  else
+    hipLaunchKernelGGL(pe_fwd_kernel<float>, dim3(g), dim3(NT), 0, s, (const float*)p->x, p->alpha, p->pe,
+                       (float*)p->out, p->m, p->c, p->t, p->t_offset, d);
+  return tt2_check_launch(hipGetLastError(), "tt2_posenc_fwd");
+}
+
+extern "C" size_t tt2_posenc_bwd_workspace_size(void) { return TT2_PE_BWD_BLOCKS * sizeof(float); }
+
+extern "C" int tt2_posenc_bwd(const tt2_pe_args* p, hipStream_t s) {
+  if (!p->workspace || p->ws_bytes < tt2_posenc_bwd_workspace_size())
+    return tt2_set_error(TT2_E_INVALID, "tt2_posenc_bwd: workspace");
+  DropDesc d{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
+  float* part = reinterpret_cast<float*>(p->workspace);
+  if (p->dtype == TT2_DT_BF16)
+    hipLaunchKernelGGL(pe_bwd_kernel<bf16>, dim3(TT2_PE_BWD_BLOCKS), dim3(NT), 0, s, (const bf16*)p->dout, p->pe,
+                       (bf16*)p->dx, part, p->m, p->c, p->t, d);
+  else
+    hipLaunchKernelGGL(pe_bwd_kernel<float>, dim3(TT2_PE_BWD_BLOCKS), dim3(NT), 0, s, (const float*)p->dout, p->pe,
+                       (float*)p->dx, part, p->m, p->c, p->t, d);
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(1), dim3(64), 0, s, part, TT2_PE_BWD_BLOCKS, 1, (int64_t)1,
+                     p->dalpha, 0.f);
+  return tt2_check_launch(hipGetLastError(), "tt2_posenc_bwd");
+}
+
+extern "C" int tt2_shift_right(const float* mel, void* out, int batch, int t, int c, int dtype, hipStream_t s) {
+  const int g = grid_for((int64_t)batch * t * c);
+  if (dtype == TT2_DT_BF16)
+    hipLaunchKernelGGL(shift_right_kernel<bf16>, dim3(g), dim3(NT), 0, s, mel, (bf16*)out, batch, t, c);
+  else
+    hipLaunchKernelGGL(shift_right_kernel<float>, dim3(g), dim3(NT), 0, s, mel, (float*)out, batch, t, c);
+  return tt2_check_launch(hipGetLastError(), "tt2_shift_right");
+}
+
+extern "C" int tt2_cast2d(const void* src, int src_dtype, int64_t src_ld, void* dst, int dst_dtype, int64_t dst_ld,
+                          int m, int n, hipStream_t s) {
+  if ((int64_t)m * n == 0) return TT2_OK;
+  hipLaunchKernelGGL(cast2d_kernel, dim3(grid_for((int64_t)m * n)), dim3(NT), 0, s, src, src_dtype, src_ld, dst,
+                     dst_dtype, dst_ld, m, n);
+  return tt2_check_launch(hipGetLastError(), "tt2_cast2d");
+}
+
+extern "C" size_t tt2_loss_workspace_size(void) { return TT2_LOSS_BLOCKS * 4 * sizeof(float); }
+
+extern "C" int tt2_tts_loss(const tt2_loss_args* p, hipStream_t s) {
+  if (p->n_mels + 1 > p->heads_ld) return tt2_set_error(TT2_E_INVALID, "tt2_tts_loss: heads_ld too small");
+  if (!p->workspace || p->ws_bytes < tt2_loss_workspace_size())
+    return tt2_set_error(TT2_E_INVALID, "tt2_tts_loss: workspace");
+  float* part = reinterpret_cast<float*>(p->workspace);
+  if (p->grad_dtype == TT2_DT_BF16)
+    hipLaunchKernelGGL(loss_kernel<bf16>, dim3(TT2_LOSS_BLOCKS), dim3(NT), 0, s, p->heads, p->heads_ld,
+                       p->mel_after, p->target, p->mel_len, p->batch, p->t, p->n_mels, p->pos_weight, p->grad_scale, p->g_heads,
+                       (bf16*)p->g_after, part);
+  else
+    hipLaunchKernelGGL(loss_kernel<float>, dim3(TT2_LOSS_BLOCKS), dim3(NT), 0, s, p->heads, p->heads_ld,
+                       p->mel_after, p->target, p->mel_len, p->batch, p->t, p->n_mels, p->pos_weight, p->grad_scale, p->g_heads,
+                       (float*)p->g_after, part);
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), 0, s, part, TT2_LOSS_BLOCKS, p->mel_len, p->batch,
+                     p->t, p->n_mels, p->loss_out);
+  return tt2_check_launch(hipGetLastError(), "tt2_tts_loss");
+}
+
+extern "C" int tt2_conv_weight_flip(const void* w, void* wd, int cout, int cin, int k, int dtype, hipStream_t s) {
+  const int g = grid_for((int64_t)cout * cin * k);
+  if (dtype == TT2_DT_BF16)
+    hipLaunchKernelGGL(conv_wflip_kernel<bf16>, dim3(g), dim3(NT), 0, s, (const bf16*)w, (bf16*)wd, cout, cin, k);
+  else
+    hipLaunchKernelGGL(conv_wflip_kernel<float>, dim3(g), dim3(NT), 0, s, (const float*)w, (float*)wd, cout, cin, k);
+  return tt2_check_launch(hipGetLastError(), "tt2_conv_weight_flip");
+}
+
+extern "C" size_t tt2_adam_workspace_size(void) { return TT2_ADAM_NORM_BLOCKS * sizeof(float); }
+
+extern "C" int tt2_adam_step(const tt2_adam_args* p, hipStream_t s) {
+  AdamArgs a{};
+  a.p = p->params; a.g = p->grads; a.m = p->exp_avg; a.v = p->exp_avg_sq; a.shadow = (bf16*)p->shadow_bf16;
+  a.n = p->n; a.step = p->step;
+  a.lr = p->lr; a.beta1 = p->beta1; a.beta2 = p->beta2; a.eps = p->eps; a.wd = p->weight_decay;
+  a.clip = p->clip_norm; a.warmup = p->warmup; a.noam = p->noam;
+  a.d_model_rsqrt = p->d_model > 0 ? 1.f / sqrtf((float)p->d_model) : 1.f;
+  if (p->clip_norm > 0.f) {
+    if (!p->workspace || p->ws_bytes < tt2_adam_workspace_size())
+      return tt2_set_error(TT2_E_INVALID, "tt2_adam_step: workspace");
+    float* part = reinterpret_cast<float*>(p->workspace);
+    hipLaunchKernelGGL(sumsq_kernel, dim3(TT2_ADAM_NORM_BLOCKS), dim3(NT), 0, s, p->grads, p->n, part);
+    a.norm_part = part;
+    a.n_part = TT2_ADAM_NORM_BLOCKS;
+  }
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(p->n, NT * 4)), dim3(NT), 0, s, a);
+  return tt2_check_launch(hipGetLastError(), "tt2_adam_step");
+}
+
+extern "C" int tt2_step_bump(int32_t* step, uint32_t* seed, hipStream_t s) {
+  hipLaunchKernelGGL(step_bump_kernel, dim3(1), dim3(64), 0, s, step, seed);
+  return tt2_check_launch(hipGetLastError(), "tt2_step_bump");
+}

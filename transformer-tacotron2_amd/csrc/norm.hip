@@ -1,0 +1,395 @@
+// norm.hip -- fused residual + dropout + LayerNorm, and training/eval BatchNorm
+// with fused activation + dropout (+ residual), forward and backward (gfx950).
+//
+// LayerNorm (post-LN sublayer end):
+//   s = x + drop(branch);  y = (s - mean(s)) * rstd * gamma + beta
+// one wave per 512-wide row (8 values per lane, 16-B vector loads).  The
+// backward recomputes s from the saved x and branch (no s buffer) and emits
+// ds (the residual-stream gradient) and drop-masked ds (the branch gradient),
+// plus per-workgroup gamma/beta partial sums reduced by tt2_reduce_rows.
+//
+// BatchNorm1d over rows (SURVEY 8(a) a1 encoder convs, a9 post-net):
+//   train: per-chunk (mean, M2) partials -> Chan combine -> mean, rstd, running
+//   stats update (unbiased var, momentum); eval: running stats.
+//   z = act((y - mean) * rstd * gamma + beta); out = drop(z) (+ res)
+// The backward recomputes z from y (saved) and the statistics.
+#include <math.h>
+
+#include "tt2_capi.h"
+#include "tt2_common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+template <typename T> TT2_DEV void ld8(const T* p, float (&v)[8]);
+template <> TT2_DEV void ld8(const bf16* p, float (&v)[8]) {
+  bf16x8 x = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+}
+template <> TT2_DEV void ld8(const float* p, float (&v)[8]) {
+  f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+}
+template <typename T> TT2_DEV void st8(T* p, const float (&v)[8]);
+template <> TT2_DEV void st8(bf16* p, const float (&v)[8]) {
+  bf16x8 x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = (bf16)v[j];
+  *reinterpret_cast<bf16x8*>(p) = x;
+}
+template <> TT2_DEV void st8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+
+// --------------------------------------------------------------- LayerNorm
+struct LnArgs {
+  const void* x; const void* branch; const void* dy;
+  void* y; void* dx; void* dbranch;
+  const float* gamma; const float* beta;
+  float* mean; float* rstd;
+  float* part;  // bwd: [gridDim.x][2][C] (dgamma, dbeta)
+  int M, C;
+  float eps;
+  DropDesc drop;
+};
+
+template <typename T>
+__global__ __launch_bounds__(NT) void ln_fwd_kernel(LnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.M) return;
+  const int c0 = lane * 8;
+  const int64_t off = (int64_t)row * a.C + c0;
+  float s[8], br[8];
+  ld8(reinterpret_cast<const T*>(a.x) + off, s);
+  if (a.branch) {
+    ld8(reinterpret_cast<const T*>(a.branch) + off, br);
+    const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)(off + j), br[j]) : br[j];
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sum += s[j];
+  const float mean = wave_sum(sum) / a.C;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { const float d = s[j] - mean; sq += d * d; }
+  const float rstd = rsqrtf(wave_sum(sq) / a.C + a.eps);
+  float y[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) y[j] = (s[j] - mean) * rstd * a.gamma[c0 + j] + a.beta[c0 + j];
+  st8(reinterpret_cast<T*>(a.y) + off, y);
+  if (lane == 0 && a.mean) { a.mean[row] = mean; a.rstd[row] = rstd; }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void ln_bwd_kernel(LnArgs a) {
+  __shared__ float red[4][2][512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c0 = lane * 8;
+  float g[8], bt[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { g[j] = a.gamma[c0 + j]; bt[j] = 0.f; }
+  float pg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
+  for (int row = blockIdx.x * 4 + w; row < a.M; row += gridDim.x * 4) {
+    const int64_t off = (int64_t)row * a.C + c0;
+    float s[8], br[8], dy[8];
+    ld8(reinterpret_cast<const T*>(a.x) + off, s);
+    ld8(reinterpret_cast<const T*>(a.dy) + off, dy);
+    if (a.branch) {
+      ld8(reinterpret_cast<const T*>(a.branch) + off, br);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)(off + j), br[j]) : br[j];
+    }
+    const float mean = a.mean[row], rstd = a.rstd[row];
+    float c1 = 0.f, c2 = 0.f, xh[8], gd[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xh[j] = (s[j] - mean) * rstd;
+      gd[j] = g[j] * dy[j];
+      c1 += gd[j];
+      c2 += gd[j] * xh[j];
+      pg[j] += dy[j] * xh[j];
+      pb[j] += dy[j];
+    }
+    c1 = wave_sum(c1) / a.C;
+    c2 = wave_sum(c2) / a.C;
+    float ds[8], db[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ds[j] = rstd * (gd[j] - c1 - xh[j] * c2);
+      db[j] = a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)(off + j), ds[j]) : ds[j];
+    }
+    st8(reinterpret_cast<T*>(a.dx) + off, ds);
+    if (a.dbranch) st8(reinterpret_cast<T*>(a.dbranch) + off, db);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[w][0][c0 + j] = pg[j]; red[w][1][c0 + j] = pb[j]; }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * a.C; i += NT) {
+    const int which = i / a.C, c = i % a.C;
+    a.part[((int64_t)blockIdx.x * 2 + which) * a.C + c] =
+        red[0][which][c] + red[1][which][c] + red[2][which][c] + red[3][which][c];
+  }
+  (void)bt;
+}
+
+// --------------------------------------------------------------- BatchNorm
+struct BnArgs {
+  const void* y; const void* dout; const void* res;
+  void* out; void* dy;
+  const float* gamma; const float* beta;
+  float* mean; float* rstd;
+  float* run_mean; float* run_var;
+  float* part;  // train stats: [R][2][C] (chunk mean, chunk M2); bwd: [R][2][C] sums
+  float* dgamma; float* dbeta;
+  int64_t res_ld;
+  int M, C, R, rows_per, act, out_dt, res_dt, training;
+  float eps, momentum;
+  DropDesc drop;
+};
+
+TT2_DEV float act_f(int act, float v) {
+  return act == ACT_RELU ? fmaxf(v, 0.f) : (act == ACT_TANH ? tanhf(v) : v);
+}
+TT2_DEV float act_grad_from_out(int act, float z) {
+  return act == ACT_RELU ? (z > 0.f ? 1.f : 0.f) : (act == ACT_TANH ? 1.f - z * z : 1.f);
+}
+
+// grid (ceil(C/256), R): thread = column, chunk = rows [r*rows_per, ...)
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= a.C) return;
+  const int r0 = blockIdx.y * a.rows_per, r1 = min(a.M, r0 + a.rows_per);
+  const T* y = reinterpret_cast<const T*>(a.y);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += to_f32(y[(int64_t)r * a.C + c]);
+  const int n = r1 - r0;
+  const float mu = n > 0 ? s / n : 0.f;
+  float m2 = 0.f;
+  for (int r = r0; r < r1; ++r) { const float d = to_f32(y[(int64_t)r * a.C + c]) - mu; m2 += d * d; }
+  a.part[((int64_t)blockIdx.y * 2 + 0) * a.C + c] = mu;
+  a.part[((int64_t)blockIdx.y * 2 + 1) * a.C + c] = m2;
+}
+
+__global__ void bn_finalize_kernel(BnArgs a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  if (!a.training) {
+    a.mean[c] = a.run_mean[c];
+    a.rstd[c] = rsqrtf(a.run_var[c] + a.eps);
+    return;
+  }
+  double n = 0.0, mu = 0.0, m2 = 0.0;
+  for (int r = 0; r < a.R; ++r) {
+    const int nb = min(a.rows_per, a.M - r * a.rows_per);
+    if (nb <= 0) break;
+    const double mb = a.part[((int64_t)r * 2 + 0) * a.C + c];
+    const double m2b = a.part[((int64_t)r * 2 + 1) * a.C + c];
+    const double nn = n + nb;
+    const double d = mb - mu;
+    mu += d * nb / nn;
+    m2 += m2b + d * d * n * nb / nn;
+    n = nn;
+  }
+  const double var = n > 0 ? m2 / n : 0.0;
+  a.mean[c] = (float)mu;
+  a.rstd[c] = (float)(1.0 / sqrt(var + a.eps));
+  if (a.run_mean) {
+    const double unb = n > 1 ? m2 / (n - 1) : var;
+    a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mu);
+    a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
+  const int64_t total = (int64_t)a.M * a.C;
+  const T* y = reinterpret_cast<const T*>(a.y);
+  const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int c = (int)(i % a.C);
+    float z = act_f(a.act, (to_f32(y[i]) - a.mean[c]) * a.rstd[c] * a.gamma[c] + a.beta[c]);
+    if (a.drop.thr) z = drop_apply(a.drop, seed, (uint32_t)i, z);
+    if (a.res) {
+      const int64_t ri = (i / a.C) * a.res_ld + c;
+      z += a.res_dt == TT2_BF16 ? (float)reinterpret_cast<const bf16*>(a.res)[ri]
+                                : reinterpret_cast<const float*>(a.res)[ri];
+    }
+    if (a.out_dt == TT2_BF16) reinterpret_cast<bf16*>(a.out)[i] = (bf16)z;
+    else reinterpret_cast<float*>(a.out)[i] = z;
+  }
+}
+
+// dpre = d(pre-activation BN output): recompute z from y.
+TT2_DEV float bn_dpre(const BnArgs& a, uint32_t seed, int64_t i, int c, float yv, float doutv, float& xh) {
+  xh = (yv - a.mean[c]) * a.rstd[c];
+  const float z = act_f(a.act, xh * a.gamma[c] + a.beta[c]);
+  float g = a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)i, doutv) : doutv;
+  return g * act_grad_from_out(a.act, z);
+}
+
+template <typename T, typename TD>
+__global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= a.C) return;
+  const int r0 = blockIdx.y * a.rows_per, r1 = min(a.M, r0 + a.rows_per);
+  const T* y = reinterpret_cast<const T*>(a.y);
+  const TD* dout = reinterpret_cast<const TD*>(a.dout);
+  const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
+  float s1 = 0.f, s2 = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const int64_t i = (int64_t)r * a.C + c;
+    float xh;
+    const float dp = bn_dpre(a, seed, i, c, to_f32(y[i]), to_f32(dout[i]), xh);
+    s1 += dp;
+    s2 += dp * xh;
+  }
+  a.part[((int64_t)blockIdx.y * 2 + 0) * a.C + c] = s1;
+  a.part[((int64_t)blockIdx.y * 2 + 1) * a.C + c] = s2;
+}
+
+__global__ void bn_bwd_finalize_kernel(BnArgs a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int r = 0; r < a.R; ++r) {
+    s1 += a.part[((int64_t)r * 2 + 0) * a.C + c];
+    s2 += a.part[((int64_t)r * 2 + 1) * a.C + c];
+  }
+  a.dbeta[c] = s1;
+  a.dgamma[c] = s2;
+}
+
+template <typename T, typename TD>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
+  const int64_t total = (int64_t)a.M * a.C;
+  const T* y = reinterpret_cast<const T*>(a.y);
+  const TD* dout = reinterpret_cast<const TD*>(a.dout);
+  const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
+  const float invM = 1.f / a.M;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int c = (int)(i % a.C);
+    float xh;
+    const float dp = bn_dpre(a, seed, i, c, to_f32(y[i]), to_f32(dout[i]), xh);
+    float g;
+    if (a.training) g = a.gamma[c] * a.rstd[c] * (dp - a.dbeta[c] * invM - xh * a.dgamma[c] * invM);
+    else g = a.gamma[c] * a.rstd[c] * dp;
+    reinterpret_cast<T*>(a.dy)[i] = from_f32<T>(g);
+  }
+}
+
+int grid_for(int64_t total) {
+  int64_t b = (total + NT - 1) / NT;
+  return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+}  // namespace
+
+extern "C" int tt2_layernorm_fwd(const tt2_ln_args* p, hipStream_t s) {
+  if (p->c != 512) return tt2_set_error(TT2_E_INVALID, "tt2_layernorm: C must be 512");
+  LnArgs a{};
+  a.x = p->x; a.branch = p->branch; a.y = p->y;
+  a.gamma = p->gamma; a.beta = p->beta; a.mean = p->mean; a.rstd = p->rstd;
+  a.M = p->m; a.C = p->c; a.eps = p->eps;
+  a.drop = DropDesc{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
+  if (p->m == 0) return TT2_OK;
+  dim3 g((p->m + 3) / 4);
+  if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(ln_fwd_kernel<bf16>, g, dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(ln_fwd_kernel<float>, g, dim3(NT), 0, s, a);
+  return tt2_check_launch(hipGetLastError(), "tt2_layernorm_fwd");
+}
+
+extern "C" size_t tt2_layernorm_bwd_workspace_size(const tt2_ln_args* p) {
+  return (size_t)TT2_LN_BWD_BLOCKS * 2 * p->c * sizeof(float);
+}
+
+extern "C" int tt2_layernorm_bwd(const tt2_ln_args* p, hipStream_t s) {
+  if (p->c != 512) return tt2_set_error(TT2_E_INVALID, "tt2_layernorm: C must be 512");
+  if (!p->workspace || p->ws_bytes < tt2_layernorm_bwd_workspace_size(p))
+    return tt2_set_error(TT2_E_INVALID, "tt2_layernorm_bwd: workspace too small");
+  LnArgs a{};
+  a.x = p->x; a.branch = p->branch; a.dy = p->dy; a.dx = p->dx; a.dbranch = p->dbranch;
+  a.gamma = p->gamma; a.beta = p->beta; a.mean = p->mean; a.rstd = p->rstd;
+  a.part = reinterpret_cast<float*>(p->workspace);
+  a.M = p->m; a.C = p->c; a.eps = p->eps;
+  a.drop = DropDesc{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
+  const int nb = TT2_LN_BWD_BLOCKS;
+  if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nb), dim3(NT), 0, s, a);
+  if (int rc = tt2_check_launch(hipGetLastError(), "tt2_layernorm_bwd")) return rc;
+  // gamma / beta gradients: sum the per-block partials
+  tt2_reduce_args r{};
+  r.src = a.part; r.rows = nb; r.cols = p->c; r.ld = 2 * p->c; r.dst = p->dgamma; r.beta = p->grad_beta;
+  if (int rc = tt2_reduce_rows(&r, s)) return rc;
+  r.src = a.part + p->c; r.dst = p->dbeta;
+  return tt2_reduce_rows(&r, s);
+}
+
+static BnArgs bn_args(const tt2_bn_args* p) {
+  BnArgs a{};
+  a.y = p->y; a.dout = p->dout; a.res = p->res; a.out = p->out; a.dy = p->dy;
+  a.gamma = p->gamma; a.beta = p->beta; a.mean = p->mean; a.rstd = p->rstd;
+  a.run_mean = p->run_mean; a.run_var = p->run_var;
+  a.part = reinterpret_cast<float*>(p->workspace);
+  a.dgamma = p->dgamma; a.dbeta = p->dbeta;
+  a.M = p->m; a.C = p->c; a.act = p->act; a.out_dt = p->out_dtype; a.res_dt = p->res_dtype;
+  a.res_ld = p->res_ld > 0 ? p->res_ld : p->c;
+  a.training = p->training;
+  a.eps = p->eps; a.momentum = p->momentum;
+  a.rows_per = TT2_BN_ROWS_PER_CHUNK;
+  a.R = (p->m + a.rows_per - 1) / a.rows_per;
+  a.drop = DropDesc{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
+  return a;
+}
+
+extern "C" size_t tt2_batchnorm_workspace_size(const tt2_bn_args* p) {
+  const size_t R = (p->m + TT2_BN_ROWS_PER_CHUNK - 1) / TT2_BN_ROWS_PER_CHUNK;
+  return R * 2 * p->c * sizeof(float);
+}
+
+extern "C" int tt2_batchnorm_fwd(const tt2_bn_args* p, hipStream_t s) {
+  if (p->m <= 0) return TT2_OK;
+  if (p->training && (!p->workspace || p->ws_bytes < tt2_batchnorm_workspace_size(p)))
+    return tt2_set_error(TT2_E_INVALID, "tt2_batchnorm_fwd: workspace too small");
+  BnArgs a = bn_args(p);
+  const bool bf = p->dtype == TT2_DT_BF16;
+  if (p->training) {
+    dim3 g((p->c + NT - 1) / NT, a.R);
+    if (bf) hipLaunchKernelGGL(bn_stats_kernel<bf16>, g, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL(bn_stats_kernel<float>, g, dim3(NT), 0, s, a);
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + 255) / 256), dim3(256), 0, s, a);
+  const int g = grid_for((int64_t)p->m * p->c);
+  if (bf) hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(g), dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(g), dim3(NT), 0, s, a);
+  return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_fwd");
+}
+
+extern "C" int tt2_batchnorm_bwd(const tt2_bn_args* p, hipStream_t s) {
+  if (p->m <= 0) return TT2_OK;
+  if (!p->workspace || p->ws_bytes < tt2_batchnorm_workspace_size(p))
+    return tt2_set_error(TT2_E_INVALID, "tt2_batchnorm_bwd: workspace too small");
+  BnArgs a = bn_args(p);
+  const bool bf = p->dtype == TT2_DT_BF16;
+  const bool dbf = p->dout_dtype == TT2_DT_BF16;
+  dim3 g((p->c + NT - 1) / NT, a.R);
+#define TT2_BN_DISPATCH(KER, grid)                                                              \
+  if (bf && dbf) hipLaunchKernelGGL((KER<bf16, bf16>), grid, dim3(NT), 0, s, a);                \
+  else if (bf) hipLaunchKernelGGL((KER<bf16, float>), grid, dim3(NT), 0, s, a);                 \
+  else if (dbf) hipLaunchKernelGGL((KER<float, bf16>), grid, dim3(NT), 0, s, a);                \
+  else hipLaunchKernelGGL((KER<float, float>), grid, dim3(NT), 0, s, a);
+  TT2_BN_DISPATCH(bn_bwd_stats_kernel, g)
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + 255) / 256), dim3(256), 0, s, a);
+  const int ga = grid_for((int64_t)p->m * p->c);
+  TT2_BN_DISPATCH(bn_bwd_apply_kernel, dim3(ga))
+#undef TT2_BN_DISPATCH
+  return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_bwd");
+}

@@ -1,0 +1,207 @@
+"""ctypes binding of libtt2.so (include/tt2_capi.h).
+
+``import torch`` happens first so libtt2 binds to the HIP runtime torch already
+loaded (one runtime per process).  There is no fallback: if the library or a
+GPU is missing, ``lib()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede CDLL: one HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtt2.so")
+
+DT_F32 = 0
+DT_BF16 = 1
+ACT_NONE, ACT_RELU, ACT_TANH = 0, 1, 2
+
+vp = C.c_void_p
+i32, i64, u32, f32, sz = C.c_int32, C.c_int64, C.c_uint32, C.c_float, C.c_size_t
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [
+        ("a", vp), ("b", vp), ("c", vp),
+        ("bias", vp), ("res", vp), ("gate", vp),
+        ("drop_seed", vp),
+        ("workspace", vp), ("ws_bytes", sz),
+        ("lda", i64), ("ldb", i64), ("ldc", i64), ("ldr", i64), ("ldg", i64),
+        ("m", i32), ("n", i32), ("k", i32),
+        ("dtype_in", i32), ("dtype_out", i32), ("res_dtype", i32), ("gate_dtype", i32),
+        ("trans_a", i32), ("trans_b", i32),
+        ("act", i32), ("splits", i32),
+        ("alpha", f32), ("beta", f32), ("gate_scale", f32),
+        ("drop_site", u32), ("drop_thr", u32), ("drop_scale", f32),
+        ("a_conv_t", i32), ("a_conv_c", i32), ("a_conv_pad", i32),
+        ("b_conv_t", i32), ("b_conv_c", i32), ("b_conv_pad", i32),
+    ]
+
+
+# (name, argtypes) for every exported entry point; tests check these exist.
+SIGNATURES: dict[str, tuple[list, object]] = {
+    "tt2_last_error": ([], C.c_char_p),
+    "tt2_version": ([], C.c_int),
+    "tt2_init": ([C.c_int], C.c_int),
+    "tt2_gemm_workspace_size": ([C.POINTER(GemmArgs)], sz),
+    "tt2_gemm": ([C.POINTER(GemmArgs), vp], C.c_int),
+}
+
+_lib = None
+
+
+class TT2Error(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libtt2.so and bind signatures (no device calls)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise TT2Error(f"libtt2.so not built ({path}); run transformer-tacotron2_amd/build_lib.py")
+        L = C.CDLL(path)
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+_inited = set()
+
+
+def lib():
+    """The library, initialised on the current device (raises without a GPU)."""
+    L = load()
+    if not torch.cuda.is_available():
+        raise TT2Error("tt2: no HIP device available (libtt2 has no CPU fallback)")
+    dev = torch.cuda.current_device()
+    if dev not in _inited:
+        check(L.tt2_init(dev), "tt2_init")
+        _inited.add(dev)
+    return L
+
+
+def check(rc: int, what: str = "tt2"):
+    if rc != 0:
+        msg = load().tt2_last_error()
+        raise TT2Error(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return DT_BF16
+    if t.dtype == torch.float32:
+        return DT_F32
+    raise TT2Error(f"unsupported dtype {t.dtype}")
+
+
+class AttnArgs(C.Structure):
+    _fields_ = [
+        ("q", vp), ("k", vp), ("v", vp), ("o", vp), ("dout", vp),
+        ("o_out", vp), ("dq", vp), ("dk", vp), ("dv", vp),
+        ("lse", vp), ("delta", vp),
+        ("q_ld", i64), ("k_ld", i64), ("v_ld", i64), ("o_ld", i64), ("do_ld", i64),
+        ("dq_ld", i64), ("dk_ld", i64), ("dv_ld", i64),
+        ("key_len", vp),
+        ("batch", i32), ("heads", i32), ("head_dim", i32), ("tq", i32), ("tk", i32), ("causal", i32),
+        ("dtype", i32),
+        ("scale", f32),
+    ]
+
+
+SIGNATURES.update({
+    "tt2_attn_fwd": ([C.POINTER(AttnArgs), vp], C.c_int),
+    "tt2_attn_bwd": ([C.POINTER(AttnArgs), vp], C.c_int),
+})
+
+
+class ReduceArgs(C.Structure):
+    _fields_ = [("src", vp), ("dst", vp), ("ld", i64), ("rows", i32), ("cols", i32), ("beta", f32)]
+
+
+class LnArgs(C.Structure):
+    _fields_ = [
+        ("x", vp), ("branch", vp), ("dy", vp), ("y", vp), ("dx", vp), ("dbranch", vp),
+        ("gamma", vp), ("beta", vp), ("mean", vp), ("rstd", vp), ("dgamma", vp), ("dbeta", vp),
+        ("workspace", vp), ("ws_bytes", sz), ("drop_seed", vp),
+        ("m", i32), ("c", i32), ("dtype", i32), ("eps", f32), ("grad_beta", f32),
+        ("drop_site", u32), ("drop_thr", u32), ("drop_scale", f32),
+    ]
+
+
+class BnArgs(C.Structure):
+    _fields_ = [
+        ("y", vp), ("dout", vp), ("res", vp), ("out", vp), ("dy", vp),
+        ("gamma", vp), ("beta", vp), ("mean", vp), ("rstd", vp), ("run_mean", vp), ("run_var", vp),
+        ("dgamma", vp), ("dbeta", vp), ("workspace", vp), ("ws_bytes", sz), ("drop_seed", vp),
+        ("res_ld", i64),
+        ("m", i32), ("c", i32), ("act", i32), ("dtype", i32), ("out_dtype", i32), ("res_dtype", i32),
+        ("dout_dtype", i32), ("training", i32), ("eps", f32), ("momentum", f32),
+        ("drop_site", u32), ("drop_thr", u32), ("drop_scale", f32),
+    ]
+
+
+class PeArgs(C.Structure):
+    _fields_ = [
+        ("x", vp), ("dout", vp), ("out", vp), ("dx", vp), ("alpha", vp), ("pe", vp), ("dalpha", vp),
+        ("workspace", vp), ("ws_bytes", sz), ("drop_seed", vp),
+        ("m", i32), ("c", i32), ("t", i32), ("t_offset", i32), ("dtype", i32),
+        ("drop_site", u32), ("drop_thr", u32), ("drop_scale", f32),
+    ]
+
+
+class LossArgs(C.Structure):
+    _fields_ = [
+        ("heads", vp), ("mel_after", vp), ("target", vp), ("mel_len", vp), ("loss_out", vp), ("g_heads", vp),
+        ("g_after", vp), ("workspace", vp), ("ws_bytes", sz), ("heads_ld", i64),
+        ("batch", i32), ("t", i32), ("n_mels", i32), ("grad_dtype", i32), ("pos_weight", f32), ("grad_scale", f32),
+    ]
+
+
+class AdamArgs(C.Structure):
+    _fields_ = [
+        ("params", vp), ("grads", vp), ("exp_avg", vp), ("exp_avg_sq", vp), ("shadow_bf16", vp), ("step", vp),
+        ("workspace", vp), ("ws_bytes", sz), ("n", i64),
+        ("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32), ("weight_decay", f32), ("clip_norm", f32),
+        ("warmup", f32), ("noam", i32), ("d_model", i32),
+    ]
+
+
+P_ = C.POINTER
+SIGNATURES.update({
+    "tt2_reduce_rows": ([P_(ReduceArgs), vp], C.c_int),
+    "tt2_colsum_workspace_size": ([C.c_int, C.c_int], sz),
+    "tt2_colsum": ([vp, C.c_int, i64, C.c_int, C.c_int, vp, f32, vp, sz, vp], C.c_int),
+    "tt2_layernorm_fwd": ([P_(LnArgs), vp], C.c_int),
+    "tt2_layernorm_bwd_workspace_size": ([P_(LnArgs)], sz),
+    "tt2_layernorm_bwd": ([P_(LnArgs), vp], C.c_int),
+    "tt2_batchnorm_workspace_size": ([P_(BnArgs)], sz),
+    "tt2_batchnorm_fwd": ([P_(BnArgs), vp], C.c_int),
+    "tt2_batchnorm_bwd": ([P_(BnArgs), vp], C.c_int),
+    "tt2_embedding_fwd": ([vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp], C.c_int),
+    "tt2_embedding_bwd": ([vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp], C.c_int),
+    "tt2_posenc_fwd": ([P_(PeArgs), vp], C.c_int),
+    "tt2_posenc_bwd_workspace_size": ([], sz),
+    "tt2_posenc_bwd": ([P_(PeArgs), vp], C.c_int),
+    "tt2_shift_right": ([vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp], C.c_int),
+    "tt2_cast2d": ([vp, C.c_int, i64, vp, C.c_int, i64, C.c_int, C.c_int, vp], C.c_int),
+    "tt2_loss_workspace_size": ([], sz),
+    "tt2_tts_loss": ([P_(LossArgs), vp], C.c_int),
+    "tt2_conv_weight_flip": ([vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp], C.c_int),
+    "tt2_adam_workspace_size": ([], sz),
+    "tt2_adam_step": ([P_(AdamArgs), vp], C.c_int),
+    "tt2_step_bump": ([vp, vp, vp], C.c_int),
+})

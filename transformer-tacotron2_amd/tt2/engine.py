@@ -1,0 +1,568 @@
+"""TTSEngine -- the training/inference step as an explicit kernel schedule.
+
+No autograd: the forward writes every activation the backward needs into a
+preallocated per-shape arena; the backward walks the network in reverse with
+hand-written gradient kernels (libtt2), writing parameter gradients straight
+into one flat f32 buffer.  Everything runs on the current torch stream with
+no host synchronisation and no allocation after warm-up, so a whole step
+(forward + loss + backward + Adam) is capturable in one hipGraph.
+
+Layout: activations are channels-last [batch*time, channels];
+Me = B*Tx encoder rows, Md = B*Ty decoder rows.  Compute dtype ``cd`` is bf16
+(f32 accumulation, f32 master weights/grads/statistics) or f32 (parity mode,
+exact-f32 MFMA).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import ops
+from ._lib import ACT_NONE, ACT_RELU, ACT_TANH
+from .config import (SITE_DEC_FC1, SITE_DEC_FC2, SITE_DEC_LAYER, SITE_DEC_PE, SITE_ENC_CONV, SITE_ENC_LAYER,
+                     SITE_ENC_PE, SITE_POSTNET, TTSConfig)
+from .ops import NO_DROP, Drop
+from .params import Layout, bn_layers, build_slots, postnet_channels, stats_layout
+
+
+def sinusoid_table(max_len: int, dim: int) -> torch.Tensor:
+    """Scaled-PE table (same formula as transformers modeling_speecht5.py:404-409)."""
+    pe = torch.zeros(max_len, dim)
+    position = torch.arange(0, max_len).unsqueeze(1)
+    div_term = torch.exp(torch.arange(0, dim, 2, dtype=torch.int64).float() * -(math.log(10000.0) / dim))
+    pe[:, 0::2] = torch.sin(position.float() * div_term)
+    pe[:, 1::2] = torch.cos(position.float() * div_term)
+    return pe
+
+
+def auto_splits(n_out: int, n_in: int, k: int) -> int:
+    tiles = ((n_out + 127) // 128) * ((n_in + 127) // 128)
+    if tiles >= 256:
+        return 1
+    s = max(1, min(32, 512 // tiles, k // 256))
+    return s
+
+
+class Arena:
+    """All activations / gradient scratch for one (B, Tx, Ty) shape."""
+
+    def __init__(self, c: TTSConfig, B: int, Tx: int, Ty: int, cd: torch.dtype, dev):
+        self.B, self.Tx, self.Ty = B, Tx, Ty
+        d, F, H = c.d_model, c.d_ffn, c.n_heads
+        Me, Md = B * Tx, B * Ty
+        self.Me, self.Md = Me, Md
+        self.t = {}
+        f32 = torch.float32
+
+        def mk(name, shape, dtype=cd):
+            self.t[name] = torch.empty(shape, dtype=dtype, device=dev)
+
+        mk("text", (Me,), torch.int64)
+        mk("text_len", (B,), torch.int32)
+        mk("mel_len", (B,), torch.int32)
+        mk("mel", (B, Ty, c.n_mels), f32)
+        mk("emb", (Me, d))
+        for i in range(c.enc_conv_layers):
+            mk(f"ecv_y{i}", (Me, d))
+            mk(f"ecv_o{i}", (Me, d))
+            mk(f"ecv_mean{i}", (d,), f32)
+            mk(f"ecv_rstd{i}", (d,), f32)
+        mk("eproj", (Me, d))
+        mk("ex0", (Me, d))
+        for l in range(c.n_enc):
+            mk(f"eqkv{l}", (Me, 3 * d))
+            mk(f"eatt{l}", (Me, d))
+            mk(f"else{l}", (B * H, Tx), f32)
+            mk(f"eo{l}", (Me, d))
+            mk(f"eh1{l}", (Me, d))
+            mk(f"eln1m{l}", (Me,), f32)
+            mk(f"eln1r{l}", (Me,), f32)
+            mk(f"ef1{l}", (Me, F))
+            mk(f"ef2{l}", (Me, d))
+            mk(f"ex{l + 1}", (Me, d))
+            mk(f"eln2m{l}", (Me,), f32)
+            mk(f"eln2r{l}", (Me,), f32)
+        mk("mkv", (Me, c.n_dec * 2 * d))
+        mk("din", (Md, c.n_mels))
+        mk("dp1", (Md, c.dec_prenet))
+        mk("dp2", (Md, c.dec_prenet))
+        mk("dproj", (Md, d))
+        mk("dx0", (Md, d))
+        for l in range(c.n_dec):
+            mk(f"dqkv{l}", (Md, 3 * d))
+            mk(f"datt{l}", (Md, d))
+            mk(f"dlse{l}", (B * H, Ty), f32)
+            mk(f"do{l}", (Md, d))
+            mk(f"dh1{l}", (Md, d))
+            mk(f"dcq{l}", (Md, d))
+            mk(f"dcatt{l}", (Md, d))
+            mk(f"dclse{l}", (B * H, Ty), f32)
+            mk(f"dco{l}", (Md, d))
+            mk(f"dh2{l}", (Md, d))
+            mk(f"df1{l}", (Md, F))
+            mk(f"df2{l}", (Md, d))
+            mk(f"dx{l + 1}", (Md, d))
+            for k in (1, 2, 3):
+                mk(f"dln{k}m{l}", (Md,), f32)
+                mk(f"dln{k}r{l}", (Md,), f32)
+        self.heads_ld = 96
+        self.t["heads"] = torch.zeros(Md, self.heads_ld, dtype=f32, device=dev)
+        mk("pin", (Md, c.n_mels))
+        chans = postnet_channels(c)
+        for i in range(c.postnet_layers):
+            mk(f"pcv_y{i}", (Md, chans[i + 1]))
+            if i < c.postnet_layers - 1:
+                mk(f"pcv_o{i}", (Md, chans[i + 1]))
+            mk(f"pcv_mean{i}", (chans[i + 1],), f32)
+            mk(f"pcv_rstd{i}", (chans[i + 1],), f32)
+        mk("mel_after", (Md, c.n_mels), f32)
+        mk("loss", (4,), f32)
+        # ---- gradient scratch
+        mk("g_heads", (Md, self.heads_ld), f32)
+        self.t["gh_cd"] = torch.zeros(Md, self.heads_ld, dtype=cd, device=dev)
+        mk("g_after", (Md, c.n_mels))
+        mk("g_pa", (Md, c.postnet_channels))
+        mk("g_pb", (Md, c.postnet_channels))
+        mk("g_xa", (Md, d))
+        mk("g_xb", (Md, d))
+        mk("g_res", (Md, d))
+        mk("g_br", (Md, d))
+        mk("g_f1", (Md, F))
+        mk("g_qkv", (Md, 3 * d))
+        mk("g_att", (Md, d))
+        mk("g_p1", (Md, c.dec_prenet))
+        mk("g_p2", (Md, c.dec_prenet))
+        mk("g_mkv", (Me, c.n_dec * 2 * d))
+        mk("delta", (B * H, max(Tx, Ty)), f32)
+
+    def __getitem__(self, k):
+        return self.t[k]
+
+
+class TTSEngine:
+    def __init__(self, cfg: TTSConfig | None = None, dtype: torch.dtype = torch.bfloat16, device="cuda",
+                 seed: int = 0):
+        self.cfg = c = cfg or TTSConfig()
+        assert c.d_model == 512 and c.head_dim == 64, "kernels are built for d_model 512, head_dim 64"
+        self.cd = dtype
+        self.dev = torch.device(device)
+        self.lay = Layout(build_slots(c))
+        self.slay = stats_layout(c)
+        n = self.lay.numel
+        self.params = torch.zeros(n, dtype=torch.float32, device=self.dev)
+        self.grads = torch.zeros(n, dtype=torch.float32, device=self.dev)
+        self.shadow = torch.zeros(n, dtype=torch.bfloat16, device=self.dev) if dtype == torch.bfloat16 else None
+        self.stats = torch.zeros(self.slay.numel, dtype=torch.float32, device=self.dev)
+        self.nbt = {name: 0 for name, _ in bn_layers(c)}
+        self.exp_avg = None
+        self.exp_avg_sq = None
+        self.pe = sinusoid_table(c.max_len, c.d_model).to(self.dev)
+        self.seed = torch.tensor([seed], dtype=torch.int32, device=self.dev)   # per-step dropout seed (uint32)
+        self.step_t = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.ws = ops.Workspace()
+        self.arenas: dict[tuple, Arena] = {}
+        self.training = True
+        self.dropout_enabled = True
+        self.grad_scale = 1.0
+        self.grad_ready_hook = None   # called as hook(flat_offset) during backward (DP bucketing)
+        self.opt = dict(lr=1.0, beta1=0.9, beta2=0.98, eps=1e-9, weight_decay=0.0, clip_norm=1.0, warmup=4000.0,
+                        noam=True)
+        self._init_defaults()
+
+    # ------------------------------------------------------------ parameters
+    def _init_defaults(self):
+        for name, _ in bn_layers(self.cfg):
+            self.slay.view(self.stats, name + ".rv").fill_(1.0)
+        for name, (off, shape, n) in self.lay.slots.items():
+            if name.endswith(".g") or name.endswith("alpha"):
+                self.P(name).fill_(1.0)
+        self.sync_shadow()
+
+    def P(self, name):
+        return self.lay.view(self.params, name)
+
+    def G(self, name):
+        return self.lay.view(self.grads, name)
+
+    def W(self, name):
+        return self.lay.view(self.shadow if self.shadow is not None else self.params, name)
+
+    def S(self, name):
+        return self.slay.view(self.stats, name)
+
+    def sync_shadow(self):
+        if self.shadow is not None:
+            self.shadow.copy_(self.params)
+
+    def load_slots(self, P: dict, S: dict | None = None, nbt: dict | None = None):
+        with torch.no_grad():
+            for k, v in P.items():
+                self.P(k).copy_(v.reshape(self.P(k).shape))
+            for k, v in (S or {}).items():
+                self.S(k).copy_(v)
+        if nbt:
+            self.nbt.update(nbt)
+        self.sync_shadow()
+
+    def drop(self, site: int, p: float) -> Drop:
+        if self.training and self.dropout_enabled and p > 0:
+            return Drop(self.seed, site, p)
+        return NO_DROP
+
+    def arena(self, B, Tx, Ty) -> Arena:
+        key = (B, Tx, Ty)
+        if key not in self.arenas:
+            self.arenas[key] = Arena(self.cfg, B, Tx, Ty, self.cd, self.dev)
+        return self.arenas[key]
+
+    # ------------------------------------------------------------ GEMM helpers
+    def _lin(self, x, w, out, m, n, k, bias=None, act=ACT_NONE, drop=NO_DROP, res=None, ldx=None, ldo=None,
+             a_conv=None, beta=0.0):
+        ops.gemm(x, w, out, m, n, k, ldx or k, k, ldo or n, bias=bias, res=res, ldr=ldo or n, act=act, drop=drop,
+                 a_conv=a_conv, beta=beta, ws=self.ws)
+
+    def _dgrad(self, dy, w, out, m, n_in, n_out, res=None, gate=None, gate_scale=1.0, ldy=None, ldo=None,
+               a_conv=None, beta=0.0):
+        """out[m, n_in] = dy[m, n_out] @ W[n_out, n_in] (+res) (*gate)"""
+        ops.gemm(dy, w, out, m, n_in, n_out, ldy or n_out, n_in, ldo or n_in, trans_b=True, res=res,
+                 ldr=ldo or n_in, gate=gate, ldg=ldo or n_in, gate_scale=gate_scale, a_conv=a_conv, beta=beta,
+                 ws=self.ws)
+
+    def _conv_dgrad(self, dy, wflip, out, m, cin, cout, K, T, ldo=None, beta=0.0):
+        """out[m, cin] = conv1d(dy, flipped W): implicit im2col of dy x wflip[cin][tap][cout]"""
+        ops.gemm(dy, wflip, out, m, cin, K * cout, cout, K * cout, ldo or cin, a_conv=(T, cout, (K - 1) // 2),
+                 beta=beta, ws=self.ws)
+
+    def _wgrad(self, dy, x, gw, n_out, n_in, m, ldy=None, ldx=None, b_conv=None):
+        """gw[n_out, n_in] (f32) = dy[m, n_out]^T @ x[m, n_in]"""
+        ops.gemm(dy, x, gw, n_out, n_in, m, ldy or n_out, ldx or n_in, n_in, trans_a=True, trans_b=True,
+                 splits=auto_splits(n_out, n_in, m), b_conv=b_conv, ws=self.ws)
+
+    def _bias(self, dy, ld, m, n, gb):
+        ops.colsum(dy, ld, m, n, gb, ws=self.ws)
+
+    # ------------------------------------------------------------ forward
+    def stage_inputs(self, A: Arena, text, text_len, mel, mel_len):
+        A["text"].copy_(text.reshape(-1), non_blocking=True)
+        A["text_len"].copy_(text_len, non_blocking=True)
+        A["mel_len"].copy_(mel_len, non_blocking=True)
+        A["mel"].copy_(mel, non_blocking=True)
+
+    def forward(self, A: Arena):
+        c, cd = self.cfg, self.cd
+        B, Tx, Ty, Me, Md = A.B, A.Tx, A.Ty, A.Me, A.Md
+        d, F, H, K = c.d_model, c.d_ffn, c.n_heads, c.enc_conv_kernel
+        pad = (K - 1) // 2
+        tr = self.training
+        scale = 1.0 / math.sqrt(c.head_dim)
+        # ---------------- encoder pre-net
+        ops.embedding_fwd(A["text"], self.W("enc.embed"), A["emb"], Me, c.vocab)
+        x = A["emb"]
+        for i in range(c.enc_conv_layers):
+            y = A[f"ecv_y{i}"]
+            self._lin(x, self.W(f"enc.conv{i}.w"), y, Me, d, K * d, bias=self.P(f"enc.conv{i}.b"), ldx=d,
+                      a_conv=(Tx, d, pad))
+            ops.batchnorm_fwd(y, self.P(f"enc.bn{i}.g"), self.P(f"enc.bn{i}.b"), A[f"ecv_mean{i}"],
+                              A[f"ecv_rstd{i}"], self.S(f"enc.bn{i}.rm"), self.S(f"enc.bn{i}.rv"), A[f"ecv_o{i}"],
+                              Me, d, ACT_RELU, tr, drop=self.drop(SITE_ENC_CONV + i, c.prenet_dropout),
+                              eps=c.bn_eps, momentum=c.bn_momentum, ws=self.ws)
+            x = A[f"ecv_o{i}"]
+        self._lin(x, self.W("enc.proj.w"), A["eproj"], Me, d, d, bias=self.P("enc.proj.b"))
+        ops.posenc_fwd(A["eproj"], self.P("enc.alpha"), self.pe, A["ex0"], Me, Tx,
+                       drop=self.drop(SITE_ENC_PE, c.dropout))
+        x = A["ex0"]
+        # ---------------- encoder layers
+        for l in range(c.n_enc):
+            p, base = f"enc{l}.", SITE_ENC_LAYER + 4 * l
+            qkv = A[f"eqkv{l}"]
+            self._lin(x, self.W(p + "qkv.w"), qkv, Me, 3 * d, d, bias=self.P(p + "qkv.b"))
+            ops.attn_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"eatt{l}"], A[f"else{l}"], 3 * d, 3 * d, 3 * d, d,
+                         B, H, Tx, Tx, A["text_len"], False, scale)
+            self._lin(A[f"eatt{l}"], self.W(p + "o.w"), A[f"eo{l}"], Me, d, d, bias=self.P(p + "o.b"))
+            ops.layernorm_fwd(x, A[f"eo{l}"], self.P(p + "ln1.g"), self.P(p + "ln1.b"), A[f"eh1{l}"],
+                              A[f"eln1m{l}"], A[f"eln1r{l}"], Me, c.ln_eps, drop=self.drop(base, c.dropout))
+            h1 = A[f"eh1{l}"]
+            self._lin(h1, self.W(p + "ffn1.w"), A[f"ef1{l}"], Me, F, d, bias=self.P(p + "ffn1.b"), act=ACT_RELU,
+                      drop=self.drop(base + 1, c.dropout))
+            self._lin(A[f"ef1{l}"], self.W(p + "ffn2.w"), A[f"ef2{l}"], Me, d, F, bias=self.P(p + "ffn2.b"))
+            ops.layernorm_fwd(h1, A[f"ef2{l}"], self.P(p + "ln2.g"), self.P(p + "ln2.b"), A[f"ex{l + 1}"],
+                              A[f"eln2m{l}"], A[f"eln2r{l}"], Me, c.ln_eps, drop=self.drop(base + 2, c.dropout))
+            x = A[f"ex{l + 1}"]
+        mem = x
+        # one GEMM projects the memory to K/V for all decoder layers
+        self._lin(mem, self.W("dec.kv.w"), A["mkv"], Me, c.n_dec * 2 * d, d, bias=self.P("dec.kv.b"))
+        # ---------------- decoder pre-net
+        ops.shift_right(A["mel"], A["din"], B, Ty, c.n_mels)
+        self._lin(A["din"], self.W("dec.fc1.w"), A["dp1"], Md, c.dec_prenet, c.n_mels, bias=self.P("dec.fc1.b"),
+                  act=ACT_RELU, drop=self.drop(SITE_DEC_FC1, c.prenet_dropout))
+        self._lin(A["dp1"], self.W("dec.fc2.w"), A["dp2"], Md, c.dec_prenet, c.dec_prenet,
+                  bias=self.P("dec.fc2.b"), act=ACT_RELU, drop=self.drop(SITE_DEC_FC2, c.prenet_dropout))
+        self._lin(A["dp2"], self.W("dec.proj.w"), A["dproj"], Md, d, c.dec_prenet, bias=self.P("dec.proj.b"))
+        ops.posenc_fwd(A["dproj"], self.P("dec.alpha"), self.pe, A["dx0"], Md, Ty,
+                       drop=self.drop(SITE_DEC_PE, c.dropout))
+        x = A["dx0"]
+        mkv = A["mkv"]
+        kvld = c.n_dec * 2 * d
+        # ---------------- decoder layers
+        for l in range(c.n_dec):
+            p, base = f"dec{l}.", SITE_DEC_LAYER + 4 * l
+            qkv = A[f"dqkv{l}"]
+            self._lin(x, self.W(p + "qkv.w"), qkv, Md, 3 * d, d, bias=self.P(p + "qkv.b"))
+            ops.attn_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"datt{l}"], A[f"dlse{l}"], 3 * d, 3 * d, 3 * d, d,
+                         B, H, Ty, Ty, A["mel_len"], True, scale)
+            self._lin(A[f"datt{l}"], self.W(p + "o.w"), A[f"do{l}"], Md, d, d, bias=self.P(p + "o.b"))
+            ops.layernorm_fwd(x, A[f"do{l}"], self.P(p + "ln1.g"), self.P(p + "ln1.b"), A[f"dh1{l}"],
+                              A[f"dln1m{l}"], A[f"dln1r{l}"], Md, c.ln_eps, drop=self.drop(base, c.dropout))
+            h1 = A[f"dh1{l}"]
+            self._lin(h1, self.W(p + "cq.w"), A[f"dcq{l}"], Md, d, d, bias=self.P(p + "cq.b"))
+            ko = 2 * d * l
+            ops.attn_fwd(A[f"dcq{l}"], mkv[:, ko:], mkv[:, ko + d:], A[f"dcatt{l}"], A[f"dclse{l}"], d, kvld, kvld,
+                         d, B, H, Ty, Tx, A["text_len"], False, scale)
+            self._lin(A[f"dcatt{l}"], self.W(p + "co.w"), A[f"dco{l}"], Md, d, d, bias=self.P(p + "co.b"))
+            ops.layernorm_fwd(h1, A[f"dco{l}"], self.P(p + "ln2.g"), self.P(p + "ln2.b"), A[f"dh2{l}"],
+                              A[f"dln2m{l}"], A[f"dln2r{l}"], Md, c.ln_eps, drop=self.drop(base + 1, c.dropout))
+            h2 = A[f"dh2{l}"]
+            self._lin(h2, self.W(p + "ffn1.w"), A[f"df1{l}"], Md, F, d, bias=self.P(p + "ffn1.b"), act=ACT_RELU,
+                      drop=self.drop(base + 2, c.dropout))
+            self._lin(A[f"df1{l}"], self.W(p + "ffn2.w"), A[f"df2{l}"], Md, d, F, bias=self.P(p + "ffn2.b"))
+            ops.layernorm_fwd(h2, A[f"df2{l}"], self.P(p + "ln3.g"), self.P(p + "ln3.b"), A[f"dx{l + 1}"],
+                              A[f"dln3m{l}"], A[f"dln3r{l}"], Md, c.ln_eps, drop=self.drop(base + 3, c.dropout))
+            x = A[f"dx{l + 1}"]
+        # ---------------- heads (mel 80 + stop 1 in one GEMM, f32 out)
+        nh = c.n_mels + 1
+        self._lin(x, self.W("heads.w"), A["heads"], Md, nh, d, bias=self.P("heads.b"), ldo=A.heads_ld)
+        # ---------------- post-net
+        ops.cast2d(A["heads"], A.heads_ld, A["pin"], c.n_mels, Md, c.n_mels)
+        self._postnet_fwd(A, A["pin"], A["heads"], A.heads_ld, Md, Ty, tr)
+        if tr:
+            for k in self.nbt:
+                self.nbt[k] += 1
+
+    def _postnet_fwd(self, A, x_in, res, res_ld, Md, Ty, tr):
+        c = self.cfg
+        chans = postnet_channels(c)
+        K = c.postnet_kernel
+        pad = (K - 1) // 2
+        x = x_in
+        nl = c.postnet_layers
+        for i in range(nl):
+            cin, cout = chans[i], chans[i + 1]
+            y = A[f"pcv_y{i}"]
+            self._lin(x, self.W(f"post.conv{i}.w"), y, Md, cout, K * cin, bias=self.P(f"post.conv{i}.b"), ldx=cin,
+                      a_conv=(Ty, cin, pad))
+            last = i == nl - 1
+            out = A["mel_after"] if last else A[f"pcv_o{i}"]
+            ops.batchnorm_fwd(y, self.P(f"post.bn{i}.g"), self.P(f"post.bn{i}.b"), A[f"pcv_mean{i}"],
+                              A[f"pcv_rstd{i}"], self.S(f"post.bn{i}.rm"), self.S(f"post.bn{i}.rv"), out, Md, cout,
+                              ACT_NONE if last else ACT_TANH, tr,
+                              drop=self.drop(SITE_POSTNET + i, c.postnet_dropout),
+                              res=res if last else None, res_ld=res_ld, eps=c.bn_eps, momentum=c.bn_momentum,
+                              ws=self.ws)
+            x = out
+
+    # ------------------------------------------------------------ loss
+    def loss(self, A: Arena):
+        c = self.cfg
+        ops.tts_loss(A["heads"], A.heads_ld, A["mel_after"], A["mel"], A["mel_len"], A["loss"], A["g_heads"],
+                     A["g_after"], A.B, A.Ty, c.n_mels, c.stop_pos_weight, self.grad_scale, ws=self.ws)
+
+    # ------------------------------------------------------------ backward
+    def _ready(self, name):
+        if self.grad_ready_hook is not None:
+            self.grad_ready_hook(self.lay.offset(name))
+
+    def backward(self, A: Arena):
+        c, cd = self.cfg, self.cd
+        B, Tx, Ty, Me, Md = A.B, A.Tx, A.Ty, A.Me, A.Md
+        d, F, H, K = c.d_model, c.d_ffn, c.n_heads, c.enc_conv_kernel
+        pad = (K - 1) // 2
+        scale = 1.0 / math.sqrt(c.head_dim)
+        gs = lambda p: 1.0 / (1.0 - p) if (self.training and self.dropout_enabled and p > 0) else 1.0  # noqa: E731
+        # ---------------- post-net
+        chans = postnet_channels(c)
+        nl = c.postnet_layers
+        g = A["g_after"]
+        scratch = [A["g_pa"], A["g_pb"]]
+        for i in reversed(range(nl)):
+            cin, cout = chans[i], chans[i + 1]
+            last = i == nl - 1
+            # BN backward may run in place (g is dead afterwards)
+            dyv = scratch[i % 2].view(-1)[:Md * cout].view(Md, cout)
+            ops.batchnorm_bwd(A[f"pcv_y{i}"], g, self.P(f"post.bn{i}.g"), self.P(f"post.bn{i}.b"),
+                              A[f"pcv_mean{i}"], A[f"pcv_rstd{i}"], dyv, self.G(f"post.bn{i}.g"),
+                              self.G(f"post.bn{i}.b"), Md, cout, ACT_NONE if last else ACT_TANH,
+                              drop=self.drop(SITE_POSTNET + i, c.postnet_dropout), ws=self.ws)
+            x_in = A[f"pcv_o{i - 1}"] if i > 0 else A["pin"]
+            self._wgrad(dyv, x_in, self.G(f"post.conv{i}.w").view(cout, K * cin), cout, K * cin, Md, ldx=cin,
+                        b_conv=(Ty, cin, pad))
+            self._bias(dyv, cout, Md, cout, self.G(f"post.conv{i}.b"))
+            wflip = self._wflip(f"post.conv{i}.w", cout, cin, K)
+            if i > 0:
+                gn = scratch[(i + 1) % 2].view(-1)[:Md * cin].view(Md, cin)
+                self._conv_dgrad(dyv, wflip, gn, Md, cin, cout, K, Ty)
+                g = gn
+            else:
+                # d(mel_before) += postnet input gradient (g_heads already holds direct + residual terms)
+                self._conv_dgrad(dyv, wflip, A["g_heads"], Md, cin, cout, K, Ty, ldo=A.heads_ld, beta=1.0)
+        self._ready("post.conv0.w")
+        # ---------------- heads
+        nh = c.n_mels + 1
+        ops.cast2d(A["g_heads"], A.heads_ld, A["gh_cd"], A.heads_ld, Md, nh)
+        x_top = A[f"dx{c.n_dec}"]
+        self._wgrad(A["gh_cd"], x_top, self.G("heads.w"), nh, d, Md, ldy=A.heads_ld)
+        self._bias(A["gh_cd"], A.heads_ld, Md, nh, self.G("heads.b"))
+        gx, gx2 = A["g_xa"], A["g_xb"]
+        self._dgrad(A["gh_cd"], self.W("heads.w"), gx, Md, d, nh, ldy=A.heads_ld)
+        self._ready("heads.w")
+        # ---------------- decoder layers
+        mkv = A["mkv"]
+        kvld = c.n_dec * 2 * d
+        g_mkv = A["g_mkv"]
+        for l in reversed(range(c.n_dec)):
+            p, base = f"dec{l}.", SITE_DEC_LAYER + 4 * l
+            x_in = A[f"dx{l}"]
+            h1, h2 = A[f"dh1{l}"], A[f"dh2{l}"]
+            # LN3 + FFN
+            ops.layernorm_bwd(gx, h2, A[f"df2{l}"], self.P(p + "ln3.g"), A[f"dln3m{l}"], A[f"dln3r{l}"], A["g_res"],
+                              A["g_br"], self.G(p + "ln3.g"), self.G(p + "ln3.b"), Md,
+                              drop=self.drop(base + 3, c.dropout), ws=self.ws)
+            self._wgrad(A["g_br"], A[f"df1{l}"], self.G(p + "ffn2.w"), d, F, Md)
+            self._bias(A["g_br"], d, Md, d, self.G(p + "ffn2.b"))
+            self._dgrad(A["g_br"], self.W(p + "ffn2.w"), A["g_f1"], Md, F, d, gate=A[f"df1{l}"],
+                        gate_scale=gs(c.dropout))
+            self._wgrad(A["g_f1"], h2, self.G(p + "ffn1.w"), F, d, Md)
+            self._bias(A["g_f1"], F, Md, F, self.G(p + "ffn1.b"))
+            self._dgrad(A["g_f1"], self.W(p + "ffn1.w"), gx2, Md, d, F, res=A["g_res"])
+            gx, gx2 = gx2, gx
+            # LN2 + cross attention
+            ops.layernorm_bwd(gx, h1, A[f"dco{l}"], self.P(p + "ln2.g"), A[f"dln2m{l}"], A[f"dln2r{l}"], A["g_res"],
+                              A["g_br"], self.G(p + "ln2.g"), self.G(p + "ln2.b"), Md,
+                              drop=self.drop(base + 1, c.dropout), ws=self.ws)
+            self._wgrad(A["g_br"], A[f"dcatt{l}"], self.G(p + "co.w"), d, d, Md)
+            self._bias(A["g_br"], d, Md, d, self.G(p + "co.b"))
+            self._dgrad(A["g_br"], self.W(p + "co.w"), A["g_att"], Md, d, d)
+            ko = 2 * d * l
+            g_cq = A["g_qkv"][:, :d]
+            ops.attn_bwd(A[f"dcq{l}"], mkv[:, ko:], mkv[:, ko + d:], A[f"dcatt{l}"], A["g_att"], A[f"dclse{l}"],
+                         A["delta"], g_cq, g_mkv[:, ko:], g_mkv[:, ko + d:], d, kvld, kvld, d, d, 3 * d, kvld, kvld,
+                         B, H, Ty, Tx, A["text_len"], False, scale)
+            self._wgrad(g_cq, h1, self.G(p + "cq.w"), d, d, Md, ldy=3 * d)
+            self._bias(g_cq, 3 * d, Md, d, self.G(p + "cq.b"))
+            self._dgrad(g_cq, self.W(p + "cq.w"), gx2, Md, d, d, ldy=3 * d, res=A["g_res"])
+            gx, gx2 = gx2, gx
+            # LN1 + self attention
+            ops.layernorm_bwd(gx, x_in, A[f"do{l}"], self.P(p + "ln1.g"), A[f"dln1m{l}"], A[f"dln1r{l}"],
+                              A["g_res"], A["g_br"], self.G(p + "ln1.g"), self.G(p + "ln1.b"), Md,
+                              drop=self.drop(base, c.dropout), ws=self.ws)
+            self._wgrad(A["g_br"], A[f"datt{l}"], self.G(p + "o.w"), d, d, Md)
+            self._bias(A["g_br"], d, Md, d, self.G(p + "o.b"))
+            self._dgrad(A["g_br"], self.W(p + "o.w"), A["g_att"], Md, d, d)
+            qkv, gq = A[f"dqkv{l}"], A["g_qkv"]
+            ops.attn_bwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"datt{l}"], A["g_att"], A[f"dlse{l}"], A["delta"],
+                         gq, gq[:, d:], gq[:, 2 * d:], 3 * d, 3 * d, 3 * d, d, d, 3 * d, 3 * d, 3 * d,
+                         B, H, Ty, Ty, A["mel_len"], True, scale)
+            self._wgrad(gq, x_in, self.G(p + "qkv.w"), 3 * d, d, Md)
+            self._bias(gq, 3 * d, Md, 3 * d, self.G(p + "qkv.b"))
+            self._dgrad(gq, self.W(p + "qkv.w"), gx2, Md, d, 3 * d, res=A["g_res"])
+            gx, gx2 = gx2, gx
+            self._ready(p + "qkv.w")
+        # ---------------- decoder pre-net
+        g_proj = A["g_br"]
+        ops.posenc_bwd(gx, self.pe, g_proj, self.G("dec.alpha"), Md, Ty, drop=self.drop(SITE_DEC_PE, c.dropout),
+                       ws=self.ws)
+        self._wgrad(g_proj, A["dp2"], self.G("dec.proj.w"), d, c.dec_prenet, Md)
+        self._bias(g_proj, d, Md, d, self.G("dec.proj.b"))
+        self._dgrad(g_proj, self.W("dec.proj.w"), A["g_p2"], Md, c.dec_prenet, d, gate=A["dp2"],
+                    gate_scale=gs(c.prenet_dropout))
+        self._wgrad(A["g_p2"], A["dp1"], self.G("dec.fc2.w"), c.dec_prenet, c.dec_prenet, Md)
+        self._bias(A["g_p2"], c.dec_prenet, Md, c.dec_prenet, self.G("dec.fc2.b"))
+        self._dgrad(A["g_p2"], self.W("dec.fc2.w"), A["g_p1"], Md, c.dec_prenet, c.dec_prenet, gate=A["dp1"],
+                    gate_scale=gs(c.prenet_dropout))
+        self._wgrad(A["g_p1"], A["din"], self.G("dec.fc1.w"), c.dec_prenet, c.n_mels, Md)
+        self._bias(A["g_p1"], c.dec_prenet, Md, c.dec_prenet, self.G("dec.fc1.b"))
+        # ---------------- memory (all layers' cross K/V)
+        mem = A[f"ex{c.n_enc}"]
+        self._wgrad(g_mkv, mem, self.G("dec.kv.w"), kvld, d, Me)
+        self._bias(g_mkv, kvld, Me, kvld, self.G("dec.kv.b"))
+        self._ready("dec.fc1.w")
+        gxe = A["g_xa"].view(-1)[:Me * d].view(Me, d)
+        gxe2 = A["g_xb"].view(-1)[:Me * d].view(Me, d)
+        gres = A["g_res"].view(-1)[:Me * d].view(Me, d)
+        gbr = A["g_br"].view(-1)[:Me * d].view(Me, d)
+        gf1 = A["g_f1"].view(-1)[:Me * F].view(Me, F)
+        gatt = A["g_att"].view(-1)[:Me * d].view(Me, d)
+        gq = A["g_qkv"].view(-1)[:Me * 3 * d].view(Me, 3 * d)
+        self._dgrad(g_mkv, self.W("dec.kv.w"), gxe, Me, d, kvld)
+        # ---------------- encoder layers
+        for l in reversed(range(c.n_enc)):
+            p, base = f"enc{l}.", SITE_ENC_LAYER + 4 * l
+            x_in, h1 = A[f"ex{l}"], A[f"eh1{l}"]
+            ops.layernorm_bwd(gxe, h1, A[f"ef2{l}"], self.P(p + "ln2.g"), A[f"eln2m{l}"], A[f"eln2r{l}"], gres, gbr,
+                              self.G(p + "ln2.g"), self.G(p + "ln2.b"), Me, drop=self.drop(base + 2, c.dropout),
+                              ws=self.ws)
+            self._wgrad(gbr, A[f"ef1{l}"], self.G(p + "ffn2.w"), d, F, Me)
+            self._bias(gbr, d, Me, d, self.G(p + "ffn2.b"))
+            self._dgrad(gbr, self.W(p + "ffn2.w"), gf1, Me, F, d, gate=A[f"ef1{l}"], gate_scale=gs(c.dropout))
+            self._wgrad(gf1, h1, self.G(p + "ffn1.w"), F, d, Me)
+            self._bias(gf1, F, Me, F, self.G(p + "ffn1.b"))
+            self._dgrad(gf1, self.W(p + "ffn1.w"), gxe2, Me, d, F, res=gres)
+            gxe, gxe2 = gxe2, gxe
+            ops.layernorm_bwd(gxe, x_in, A[f"eo{l}"], self.P(p + "ln1.g"), A[f"eln1m{l}"], A[f"eln1r{l}"], gres, gbr,
+                              self.G(p + "ln1.g"), self.G(p + "ln1.b"), Me, drop=self.drop(base, c.dropout),
+                              ws=self.ws)
+            self._wgrad(gbr, A[f"eatt{l}"], self.G(p + "o.w"), d, d, Me)
+            self._bias(gbr, d, Me, d, self.G(p + "o.b"))
+            self._dgrad(gbr, self.W(p + "o.w"), gatt, Me, d, d)
+            qkv = A[f"eqkv{l}"]
+            ops.attn_bwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"eatt{l}"], gatt, A[f"else{l}"], A["delta"],
+                         gq, gq[:, d:], gq[:, 2 * d:], 3 * d, 3 * d, 3 * d, d, d, 3 * d, 3 * d, 3 * d,
+                         B, H, Tx, Tx, A["text_len"], False, scale)
+            self._wgrad(gq, x_in, self.G(p + "qkv.w"), 3 * d, d, Me)
+            self._bias(gq, 3 * d, Me, 3 * d, self.G(p + "qkv.b"))
+            self._dgrad(gq, self.W(p + "qkv.w"), gxe2, Me, d, 3 * d, res=gres)
+            gxe, gxe2 = gxe2, gxe
+            self._ready(p + "qkv.w")
+        # ---------------- encoder pre-net
+        ops.posenc_bwd(gxe, self.pe, gbr, self.G("enc.alpha"), Me, Tx, drop=self.drop(SITE_ENC_PE, c.dropout),
+                       ws=self.ws)
+        self._wgrad(gbr, A[f"ecv_o{c.enc_conv_layers - 1}"], self.G("enc.proj.w"), d, d, Me)
+        self._bias(gbr, d, Me, d, self.G("enc.proj.b"))
+        gc = gxe2
+        self._dgrad(gbr, self.W("enc.proj.w"), gc, Me, d, d)
+        gdy = gres
+        for i in reversed(range(c.enc_conv_layers)):
+            ops.batchnorm_bwd(A[f"ecv_y{i}"], gc, self.P(f"enc.bn{i}.g"), self.P(f"enc.bn{i}.b"), A[f"ecv_mean{i}"],
+                              A[f"ecv_rstd{i}"], gdy, self.G(f"enc.bn{i}.g"), self.G(f"enc.bn{i}.b"), Me, d,
+                              ACT_RELU, drop=self.drop(SITE_ENC_CONV + i, c.prenet_dropout), ws=self.ws)
+            x_in = A[f"ecv_o{i - 1}"] if i > 0 else A["emb"]
+            self._wgrad(gdy, x_in, self.G(f"enc.conv{i}.w").view(d, K * d), d, K * d, Me, ldx=d,
+                        b_conv=(Tx, d, pad))
+            self._bias(gdy, d, Me, d, self.G(f"enc.conv{i}.b"))
+            wflip = self._wflip(f"enc.conv{i}.w", d, d, K)
+            self._conv_dgrad(gdy, wflip, gc, Me, d, d, K, Tx)
+        ops.embedding_bwd(A["text"], gc, self.G("enc.embed"), Me, c.vocab, pad_idx=0)
+        self._ready("enc.embed")
+
+    def _wflip(self, name, cout, cin, K):
+        key = ("wflip", name)
+        buf = self.__dict__.setdefault("_wflip_bufs", {}).get(key)
+        if buf is None:
+            buf = torch.empty(cin, K * cout, dtype=self.cd, device=self.dev)
+            self._wflip_bufs[key] = buf
+        ops.conv_weight_flip(self.W(name), buf, cout, cin, K)
+        return buf
+
+    # ------------------------------------------------------------ optimizer
+    def init_optimizer(self, **kw):
+        self.opt.update(kw)
+        if self.exp_avg is None:
+            self.exp_avg = torch.zeros_like(self.params)
+            self.exp_avg_sq = torch.zeros_like(self.params)
+
+    def optimizer_step(self):
+        o = self.opt
+        ops.adam_step(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.shadow, self.step_t,
+                      self.lay.numel, o["lr"], o["beta1"], o["beta2"], o["eps"], o["weight_decay"], o["clip_norm"],
+                      o["warmup"], o["noam"], self.cfg.d_model, ws=self.ws)
+        ops.step_bump(self.step_t, self.seed)

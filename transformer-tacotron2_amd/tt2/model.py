@@ -1,0 +1,164 @@
+"""TransformerTTS -- the drop-in model API of SURVEY 8(b) on the MI355X engine.
+
+    model = TransformerTTS(cfg, dtype=torch.bfloat16)
+    model.load_state_dict(sd)                      # SURVEY 8(b) checkpoint layout
+    mel_before, mel_after, stop_logits, _ = model(text, text_len, mel, mel_len)
+    total, parts = model.loss(outputs, mel, mel_len)
+    model.backward()                               # grads -> model.grads_state_dict()
+    model.train_step(text, text_len, mel, mel_len) # fwd + loss + bwd + Adam
+
+Every compute step runs in libtt2's gfx950 kernels; there is no CPU or
+PyTorch-op fallback (a missing library or GPU raises).
+"""
+from __future__ import annotations
+
+import torch
+
+from .config import TTSConfig
+from .engine import Arena, TTSEngine
+from .params import from_state_dict, grads_to_state_dict_names, to_state_dict
+
+
+class TransformerTTS:
+    def __init__(self, cfg: TTSConfig | None = None, dtype: torch.dtype = torch.bfloat16, device="cuda",
+                 seed: int = 0):
+        self.cfg = cfg or TTSConfig()
+        self.engine = TTSEngine(self.cfg, dtype, device, seed)
+        self._last: Arena | None = None
+        self._graphs: dict = {}
+
+    # ------------------------------------------------------------ modes
+    def train(self, mode: bool = True):
+        self.engine.training = mode
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    @property
+    def training(self) -> bool:
+        return self.engine.training
+
+    def set_seed(self, seed: int):
+        """Per-step dropout seed (uint32), same meaning as the oracle's set_seed."""
+        self.engine.seed.fill_(seed)
+
+    # ------------------------------------------------------------ checkpoint
+    def state_dict(self):
+        e = self.engine
+        return to_state_dict(self.cfg, e.lay, e.params, e.slay, e.stats, e.nbt)
+
+    def load_state_dict(self, sd):
+        P, S, nbt = from_state_dict(self.cfg, sd)
+        self.engine.load_slots(P, S, nbt)
+
+    def grads_state_dict(self):
+        e = self.engine
+        return grads_to_state_dict_names(self.cfg, e.lay, e.grads)
+
+    def n_params(self) -> int:
+        return self.engine.lay.n_params()
+
+    # ------------------------------------------------------------ forward / loss / backward
+    def _stage(self, text, text_len, mel, mel_len) -> Arena:
+        B, Tx = text.shape
+        Ty = mel.shape[1]
+        A = self.engine.arena(B, Tx, Ty)
+        dev = self.engine.dev
+        self.engine.stage_inputs(A, text.to(dev), text_len.to(dev, torch.int32), mel.to(dev, torch.float32),
+                                 mel_len.to(dev, torch.int32))
+        return A
+
+    def forward(self, text, text_len, mel, mel_len):
+        """Teacher-forced forward (shift-right with a zero go frame).  Returns
+        (mel_before [B,Ty,80], mel_after [B,Ty,80], stop_logits [B,Ty], None), f32."""
+        A = self._stage(text, text_len, mel, mel_len)
+        self.engine.forward(A)
+        self._last = A
+        return self.outputs(A)
+
+    __call__ = forward
+
+    def outputs(self, A: Arena):
+        c = self.cfg
+        B, Ty = A.B, A.Ty
+        heads = A["heads"]
+        mel_before = heads[:, :c.n_mels].reshape(B, Ty, c.n_mels).clone()
+        stop = heads[:, c.n_mels].reshape(B, Ty).clone()
+        mel_after = A["mel_after"].view(B, Ty, c.n_mels).clone()
+        return mel_before, mel_after, stop, None
+
+    def loss(self, outputs=None, mel=None, mel_len=None):
+        """Loss of the last forward (targets are the mel it was given); returns
+        (total, {"mel_before", "mel_after", "stop"}) as device scalars."""
+        A = self._last
+        if A is None:
+            raise RuntimeError("loss() needs a forward() first")
+        if mel is not None:
+            A["mel"].copy_(mel)
+        if mel_len is not None:
+            A["mel_len"].copy_(mel_len)
+        self.engine.loss(A)
+        L = A["loss"]
+        return L[0], {"mel_before": L[1], "mel_after": L[2], "stop": L[3]}
+
+    def backward(self):
+        if self._last is None:
+            raise RuntimeError("backward() needs forward() + loss() first")
+        self.engine.backward(self._last)
+
+    # ------------------------------------------------------------ training
+    def configure_optimizer(self, **kw):
+        self.engine.init_optimizer(**kw)
+
+    def _step_body(self, A: Arena, sync_grads=None):
+        e = self.engine
+        e.forward(A)
+        e.loss(A)
+        e.backward(A)
+        if sync_grads is not None:
+            sync_grads()
+        e.optimizer_step()
+
+    def train_step(self, text, text_len, mel, mel_len, sync_grads=None):
+        """One optimisation step, eagerly.  Returns the device loss vector
+        [total, mse_before, mse_after, bce_stop] (no host sync)."""
+        if self.engine.exp_avg is None:
+            self.engine.init_optimizer()
+        A = self._stage(text, text_len, mel, mel_len)
+        self._step_body(A, sync_grads)
+        self._last = A
+        return A["loss"]
+
+    def capture_train_step(self, B: int, Tx: int, Ty: int, warmup_batch=None):
+        """Capture fwd + loss + bwd + Adam for one shape into a hipGraph (via
+        torch.cuda.CUDAGraph, which records our kernels on its capture stream).
+        Returns a callable run(text, text_len, mel, mel_len) -> loss vector."""
+        e = self.engine
+        if e.exp_avg is None:
+            e.init_optimizer()
+        A = e.arena(B, Tx, Ty)
+        # the caller's warm-up eager steps size every workspace; capture must not allocate
+        g = torch.cuda.CUDAGraph()
+        nbt_saved = dict(e.nbt)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                e.forward(A)
+                e.loss(A)
+                e.backward(A)
+                e.optimizer_step()
+        torch.cuda.current_stream().wait_stream(s)
+        e.nbt = nbt_saved  # capture records kernels only; each replay counts one batch
+        self._graphs[(B, Tx, Ty)] = g
+
+        def run(text, text_len, mel, mel_len):
+            e.stage_inputs(A, text, text_len.to(torch.int32), mel, mel_len.to(torch.int32))
+            g.replay()
+            for k in e.nbt:
+                e.nbt[k] += 1
+            self._last = A
+            return A["loss"]
+
+        return run

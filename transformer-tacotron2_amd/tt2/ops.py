@@ -1,0 +1,270 @@
+"""Thin torch-tensor wrappers over the libtt2 C ABI (no compute in Python).
+
+Every function takes preallocated output tensors and launches on the current
+torch stream; nothing here allocates except ``Workspace.get`` outside capture.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+from ._lib import GemmArgs, check, dt, lib, ptr, stream_ptr
+
+
+def drop_thr(p: float) -> int:
+    """floor(p * 2^32) -- identical to the oracle's threshold."""
+    return int(p * 4294967296.0) if p > 0 else 0
+
+
+class Drop:
+    """Dropout site descriptor: (device seed tensor uint32[1], site id, p)."""
+
+    __slots__ = ("seed", "site", "p")
+
+    def __init__(self, seed: torch.Tensor | None, site: int, p: float):
+        self.seed, self.site, self.p = seed, site, p
+
+    @property
+    def active(self) -> bool:
+        return self.seed is not None and self.p > 0
+
+    def fields(self):
+        if not self.active:
+            return None, 0, 0, 1.0
+        return self.seed.data_ptr(), self.site, drop_thr(self.p), 1.0 / (1.0 - self.p)
+
+
+NO_DROP = Drop(None, 0, 0.0)
+
+
+class Workspace:
+    """Grow-only device scratch buffer (size it before graph capture)."""
+
+    def __init__(self):
+        self.buf: torch.Tensor | None = None
+
+    def get(self, nbytes: int) -> torch.Tensor:
+        if self.buf is None or self.buf.numel() < nbytes:
+            if torch.cuda.is_current_stream_capturing():
+                raise _lib.TT2Error("workspace must be sized before graph capture")
+            self.buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device="cuda")
+        return self.buf
+
+
+_WS = Workspace()
+
+
+def gemm(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=None, res=None, ldr=0,
+         gate=None, ldg=0, gate_scale=1.0, alpha=1.0, beta=0.0, act=0, drop: Drop = NO_DROP, splits=1,
+         a_conv=None, b_conv=None, ws: Workspace | None = None):
+    """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see tt2_capi.h tt2_gemm_args."""
+    L = lib()
+    g = GemmArgs()
+    g.a, g.b, g.c = a.data_ptr(), b.data_ptr(), c.data_ptr()
+    g.bias = ptr(bias)
+    g.res, g.gate = ptr(res), ptr(gate)
+    g.lda, g.ldb, g.ldc, g.ldr, g.ldg = lda, ldb, ldc, ldr, ldg
+    g.m, g.n, g.k = m, n, k
+    g.dtype_in, g.dtype_out = dt(a), dt(c)
+    if b.dtype != a.dtype:
+        raise _lib.TT2Error("gemm: A and B dtypes differ")
+    g.res_dtype = dt(res) if res is not None else 0
+    g.gate_dtype = dt(gate) if gate is not None else 0
+    if bias is not None and bias.dtype != torch.float32:
+        raise _lib.TT2Error("gemm: bias must be f32")
+    g.trans_a, g.trans_b = int(trans_a), int(trans_b)
+    g.act = act
+    g.alpha, g.beta, g.gate_scale = alpha, beta, gate_scale
+    g.drop_seed, g.drop_site, g.drop_thr, g.drop_scale = drop.fields()
+    if a_conv is not None:
+        g.a_conv_t, g.a_conv_c, g.a_conv_pad = a_conv
+    if b_conv is not None:
+        g.b_conv_t, g.b_conv_c, g.b_conv_pad = b_conv
+    g.splits = max(1, splits)
+    if g.splits > 1:
+        need = L.tt2_gemm_workspace_size(C.byref(g))
+        buf = (ws or _WS).get(need)
+        g.workspace, g.ws_bytes = buf.data_ptr(), buf.numel()
+    check(L.tt2_gemm(C.byref(g), stream_ptr()), "tt2_gemm")
+    return c
+
+
+def _attn_common(q, k, v, q_ld, k_ld, v_ld, batch, heads, tq, tk, key_len, causal, scale):
+    a = _lib.AttnArgs()
+    a.q, a.k, a.v = q.data_ptr(), k.data_ptr(), v.data_ptr()
+    a.q_ld, a.k_ld, a.v_ld = q_ld, k_ld, v_ld
+    if key_len is not None and key_len.dtype != torch.int32:
+        raise _lib.TT2Error("attn: key_len must be int32")
+    a.key_len = ptr(key_len)
+    a.batch, a.heads, a.head_dim, a.tq, a.tk, a.causal = batch, heads, 64, tq, tk, int(causal)
+    a.dtype = dt(q)
+    a.scale = scale
+    return a
+
+
+def attn_fwd(q, k, v, out, lse, q_ld, k_ld, v_ld, o_ld, batch, heads, tq, tk, key_len=None, causal=False,
+             scale=0.125):
+    """out[b*tq+t, 64h:64h+64] = softmax(scale q k^T + mask) v ; lse [batch*heads, tq] (log2 domain)."""
+    L = lib()
+    a = _attn_common(q, k, v, q_ld, k_ld, v_ld, batch, heads, tq, tk, key_len, causal, scale)
+    a.o_out, a.o_ld, a.lse = out.data_ptr(), o_ld, lse.data_ptr()
+    check(L.tt2_attn_fwd(C.byref(a), stream_ptr()), "tt2_attn_fwd")
+    return out
+
+
+def attn_bwd(q, k, v, o, dout, lse, delta, dq, dk, dv, q_ld, k_ld, v_ld, o_ld, do_ld, dq_ld, dk_ld, dv_ld,
+             batch, heads, tq, tk, key_len=None, causal=False, scale=0.125):
+    L = lib()
+    a = _attn_common(q, k, v, q_ld, k_ld, v_ld, batch, heads, tq, tk, key_len, causal, scale)
+    a.o, a.dout, a.o_ld, a.do_ld = o.data_ptr(), dout.data_ptr(), o_ld, do_ld
+    a.dq, a.dk, a.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
+    a.dq_ld, a.dk_ld, a.dv_ld = dq_ld, dk_ld, dv_ld
+    a.lse, a.delta = lse.data_ptr(), delta.data_ptr()
+    check(L.tt2_attn_bwd(C.byref(a), stream_ptr()), "tt2_attn_bwd")
+
+
+def _drop_into(s, drop: Drop):
+    s.drop_seed, s.drop_site, s.drop_thr, s.drop_scale = drop.fields()
+
+
+def colsum(x, ld, m, n, dst, beta=0.0, ws: Workspace | None = None):
+    """dst[n] (f32) = beta*dst + sum over m rows of x[:, :n]  (bias gradient)."""
+    L = lib()
+    buf = (ws or _WS).get(L.tt2_colsum_workspace_size(m, n))
+    check(L.tt2_colsum(x.data_ptr(), dt(x), ld, m, n, dst.data_ptr(), beta, buf.data_ptr(), buf.numel(),
+                       stream_ptr()), "tt2_colsum")
+
+
+def layernorm_fwd(x, branch, gamma, beta, y, mean, rstd, m, eps=1e-5, drop: Drop = NO_DROP):
+    L = lib()
+    a = _lib.LnArgs()
+    a.x, a.branch, a.y = x.data_ptr(), ptr(branch), y.data_ptr()
+    a.gamma, a.beta = gamma.data_ptr(), beta.data_ptr()
+    a.mean, a.rstd = ptr(mean), ptr(rstd)
+    a.m, a.c, a.dtype, a.eps = m, x.shape[-1], dt(x), eps
+    _drop_into(a, drop)
+    check(L.tt2_layernorm_fwd(C.byref(a), stream_ptr()), "tt2_layernorm_fwd")
+
+
+def layernorm_bwd(dy, x, branch, gamma, mean, rstd, dx, dbranch, dgamma, dbeta, m, drop: Drop = NO_DROP,
+                  ws: Workspace | None = None):
+    L = lib()
+    a = _lib.LnArgs()
+    a.dy, a.x, a.branch = dy.data_ptr(), x.data_ptr(), ptr(branch)
+    a.dx, a.dbranch = dx.data_ptr(), ptr(dbranch)
+    a.gamma, a.mean, a.rstd = gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr()
+    a.dgamma, a.dbeta = dgamma.data_ptr(), dbeta.data_ptr()
+    a.m, a.c, a.dtype = m, x.shape[-1], dt(x)
+    _drop_into(a, drop)
+    buf = (ws or _WS).get(L.tt2_layernorm_bwd_workspace_size(C.byref(a)))
+    a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
+    check(L.tt2_layernorm_bwd(C.byref(a), stream_ptr()), "tt2_layernorm_bwd")
+
+
+def _bn(y, gamma, beta, mean, rstd, m, c, act, training, drop, eps, momentum, ws):
+    a = _lib.BnArgs()
+    a.y, a.gamma, a.beta, a.mean, a.rstd = y.data_ptr(), gamma.data_ptr(), beta.data_ptr(), mean.data_ptr(), \
+        rstd.data_ptr()
+    a.m, a.c, a.act, a.dtype, a.training, a.eps, a.momentum = m, c, act, dt(y), int(training), eps, momentum
+    _drop_into(a, drop)
+    return a
+
+
+def batchnorm_fwd(y, gamma, beta, mean, rstd, run_mean, run_var, out, m, c, act, training, drop: Drop = NO_DROP,
+                  res=None, res_ld=0, eps=1e-5, momentum=0.1, ws: Workspace | None = None):
+    L = lib()
+    a = _bn(y, gamma, beta, mean, rstd, m, c, act, training, drop, eps, momentum, ws)
+    a.run_mean, a.run_var = ptr(run_mean), ptr(run_var)
+    a.out, a.out_dtype = out.data_ptr(), dt(out)
+    a.res, a.res_dtype, a.res_ld = ptr(res), (dt(res) if res is not None else 0), res_ld
+    buf = (ws or _WS).get(L.tt2_batchnorm_workspace_size(C.byref(a)))
+    a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
+    check(L.tt2_batchnorm_fwd(C.byref(a), stream_ptr()), "tt2_batchnorm_fwd")
+
+
+def batchnorm_bwd(y, dout, gamma, beta, mean, rstd, dy, dgamma, dbeta, m, c, act, drop: Drop = NO_DROP,
+                  ws: Workspace | None = None):
+    L = lib()
+    a = _bn(y, gamma, beta, mean, rstd, m, c, act, True, drop, 1e-5, 0.1, ws)
+    a.dout, a.dout_dtype, a.dy = dout.data_ptr(), dt(dout), dy.data_ptr()
+    a.dgamma, a.dbeta = dgamma.data_ptr(), dbeta.data_ptr()
+    buf = (ws or _WS).get(L.tt2_batchnorm_workspace_size(C.byref(a)))
+    a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
+    check(L.tt2_batchnorm_bwd(C.byref(a), stream_ptr()), "tt2_batchnorm_bwd")
+
+
+def embedding_fwd(ids, table, out, m, vocab):
+    check(lib().tt2_embedding_fwd(ids.data_ptr(), table.data_ptr(), out.data_ptr(), m, table.shape[-1], vocab,
+                                  dt(table), stream_ptr()), "tt2_embedding_fwd")
+
+
+def embedding_bwd(ids, dout, dtable, m, vocab, pad_idx=0):
+    check(lib().tt2_embedding_bwd(ids.data_ptr(), dout.data_ptr(), dtable.data_ptr(), m, dtable.shape[-1], vocab,
+                                  pad_idx, dt(dout), stream_ptr()), "tt2_embedding_bwd")
+
+
+def posenc_fwd(x, alpha, pe, out, m, t, drop: Drop = NO_DROP, t_offset=0):
+    a = _lib.PeArgs()
+    a.x, a.out, a.alpha, a.pe = x.data_ptr(), out.data_ptr(), alpha.data_ptr(), pe.data_ptr()
+    a.m, a.c, a.t, a.t_offset, a.dtype = m, x.shape[-1], t, t_offset, dt(x)
+    _drop_into(a, drop)
+    check(lib().tt2_posenc_fwd(C.byref(a), stream_ptr()), "tt2_posenc_fwd")
+
+
+def posenc_bwd(dout, pe, dx, dalpha, m, t, drop: Drop = NO_DROP, ws: Workspace | None = None):
+    L = lib()
+    a = _lib.PeArgs()
+    a.dout, a.dx, a.pe, a.dalpha = dout.data_ptr(), dx.data_ptr(), pe.data_ptr(), dalpha.data_ptr()
+    a.m, a.c, a.t, a.dtype = m, dout.shape[-1], t, dt(dout)
+    _drop_into(a, drop)
+    buf = (ws or _WS).get(L.tt2_posenc_bwd_workspace_size())
+    a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
+    check(L.tt2_posenc_bwd(C.byref(a), stream_ptr()), "tt2_posenc_bwd")
+
+
+def shift_right(mel, out, batch, t, c):
+    check(lib().tt2_shift_right(mel.data_ptr(), out.data_ptr(), batch, t, c, dt(out), stream_ptr()),
+          "tt2_shift_right")
+
+
+def cast2d(src, src_ld, dst, dst_ld, m, n):
+    check(lib().tt2_cast2d(src.data_ptr(), dt(src), src_ld, dst.data_ptr(), dt(dst), dst_ld, m, n, stream_ptr()),
+          "tt2_cast2d")
+
+
+def tts_loss(heads, heads_ld, mel_after, target, mel_len, loss_out, g_heads, g_after, batch, t, n_mels,
+             pos_weight=5.0, grad_scale=1.0, ws: Workspace | None = None):
+    L = lib()
+    a = _lib.LossArgs()
+    a.heads, a.mel_after, a.target, a.mel_len = heads.data_ptr(), mel_after.data_ptr(), target.data_ptr(), \
+        mel_len.data_ptr()
+    a.loss_out, a.g_heads, a.g_after = loss_out.data_ptr(), g_heads.data_ptr(), g_after.data_ptr()
+    a.heads_ld, a.batch, a.t, a.n_mels, a.grad_dtype = heads_ld, batch, t, n_mels, dt(g_after)
+    a.pos_weight, a.grad_scale = pos_weight, grad_scale
+    buf = (ws or _WS).get(L.tt2_loss_workspace_size())
+    a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
+    check(L.tt2_tts_loss(C.byref(a), stream_ptr()), "tt2_tts_loss")
+
+
+def conv_weight_flip(w, wd, cout, cin, k):
+    check(lib().tt2_conv_weight_flip(w.data_ptr(), wd.data_ptr(), cout, cin, k, dt(w), stream_ptr()),
+          "tt2_conv_weight_flip")
+
+
+def adam_step(params, grads, m, v, shadow, step, n, lr, beta1=0.9, beta2=0.98, eps=1e-9, weight_decay=0.0,
+              clip_norm=1.0, warmup=4000.0, noam=True, d_model=512, ws: Workspace | None = None):
+    L = lib()
+    a = _lib.AdamArgs()
+    a.params, a.grads, a.exp_avg, a.exp_avg_sq = params.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr()
+    a.shadow_bf16, a.step, a.n = ptr(shadow), step.data_ptr(), n
+    a.lr, a.beta1, a.beta2, a.eps, a.weight_decay = lr, beta1, beta2, eps, weight_decay
+    a.clip_norm, a.warmup, a.noam, a.d_model = clip_norm, warmup, int(noam), d_model
+    buf = (ws or _WS).get(L.tt2_adam_workspace_size())
+    a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
+    check(L.tt2_adam_step(C.byref(a), stream_ptr()), "tt2_adam_step")
+
+
+def step_bump(step, seed=None):
+    check(lib().tt2_step_bump(step.data_ptr(), ptr(seed), stream_ptr()), "tt2_step_bump")
