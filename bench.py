@@ -1,0 +1,212 @@
+"""bench.py -- mel frames/s of the Transformer-TTS training step on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1], the metric's single-GPU config): one
+training step = forward + loss + backward + (RCCL gradient all-reduce when
+N > 1) + fused Adam/clip, bf16 compute with f32 master weights, B = 16
+utterances per GPU of LJSpeech shape (phoneme 128, mel 800 x 80), synthetic
+seeded data (seed 0 + rank), random-init weights of the 52.99M-parameter
+architecture.  Weak scaling: every rank trains its own 16 utterances.
+
+Rank 0 prints ONE JSON line: value = all ranks' frames / max-over-ranks time;
+roofline = the dominant kernel (bf16 forward GEMM) measured with HIP events
+around each launch in an instrumented step right after the timed region;
+cpu_baseline = the CPU oracle's training step on a bounded sample of the same
+workload on this box's host cores (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "transformer-tacotron2_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+B_PER_GPU, TX, TY, NMEL = 16, 128, 800, 80
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, no sparsity)
+METRIC = "mel frames/sec (train step) at 1/2/4/8 GPUs; decode frames/sec b=32"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def synth_batch(rank: int, B: int = B_PER_GPU, dev="cuda"):
+    g = torch.Generator().manual_seed(0 + rank)
+    text = torch.randint(1, 80, (B, TX), generator=g)
+    mel = torch.randn(B, TY, NMEL, generator=g)
+    tl = torch.full((B,), TX, dtype=torch.int32)
+    ml = torch.full((B,), TY, dtype=torch.int32)
+    return text.to(dev), tl.to(dev), mel.to(dev), ml.to(dev)
+
+
+def cpu_baseline(budget_s: float = 20.0):
+    """The CPU oracle (pure PyTorch fp32) training step on a bounded sample
+    (B=2 utterances of the same 128/800 shape), timed on the host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from tt2_oracle import OracleConfig, TransformerTTSOracle, init_deterministic
+    cores = len(os.sched_getaffinity(0))
+    threads = min(16, cores)
+    torch.set_num_threads(threads)
+    model = init_deterministic(TransformerTTSOracle(OracleConfig()), 0).train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    text, tl, mel, ml = [t.cpu() for t in synth_batch(0, B=2, dev="cpu")]
+    tl, ml = tl.long(), ml.long()
+
+    def step(i):
+        model.set_seed(i)
+        opt.zero_grad()
+        out = model(text, tl, mel, ml)
+        loss, _ = model.loss(out[:3], mel, ml)
+        loss.backward()
+        opt.step()
+
+    step(0)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step(n + 1)
+        n += 1
+        if time.perf_counter() - t0 > budget_s / 2 or n >= 8:
+            break
+    dt = (time.perf_counter() - t0) / n
+    return {"value": round(2 * TY / dt, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"CPU oracle fp32 train step (fwd+loss+bwd+Adam), B=2 x (128 phonemes, 800x80 mel), "
+                      f"{n} timed steps after 1 warm-up, {threads} torch threads of {cores} visible cores"}
+
+
+def roofline(model, text, tl, mel, ml):
+    """Live per-launch timing of the dominant kernel family in one eager step."""
+    from tt2 import ops
+    ops.PROBE = ops.LaunchProbe()
+    try:
+        model.train_step(text, tl, mel, ml)
+        summ = ops.PROBE.summary()
+    finally:
+        ops.PROBE = None
+    # dominant = the GEMM variant with the most device time
+    key, (n, flops, secs) = max(summ.items(), key=lambda kv: kv[1][2])
+    tot_t = sum(v[2] for v in summ.values())
+    tot_f = sum(v[1] for v in summ.values())
+    achieved = flops / secs / 1e12
+    names = {(1, 0, 0): "gemm_kernel<bf16,Kcontig,Kcontig> (forward linear/conv)",
+             (1, 0, 1): "gemm_kernel<bf16,Kcontig,Ncontig> (dgrad)",
+             (1, 1, 1): "gemm_kernel<bf16,Mcontig,Ncontig> (wgrad)"}
+    return {
+        "kernel": names.get(key[1:4], str(key)) + (" +split-K reduce" if key[4] else ""),
+        "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+        "launches_per_step": n, "flops_per_launch": flops / n, "avg_launch_us": round(secs / n * 1e6, 2),
+        "all_gemms": {"launches": sum(v[0] for v in summ.values()), "ms_per_step": round(tot_t * 1e3, 3),
+                      "tflops": round(tot_f / tot_t / 1e12, 1)},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    from tt2.config import TTSConfig
+    from tt2.dist import attach, broadcast_params, init_from_env
+    from tt2.model import TransformerTTS
+
+    rank, world, local = init_from_env()
+    torch.cuda.set_device(local)
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}")
+    torch.manual_seed(0)
+    model = TransformerTTS(TTSConfig(), dtype=torch.bfloat16)
+    # random init of the architecture (seeded), then the standard Transformer-TTS Adam/Noam setup
+    eng = model.engine
+    with torch.no_grad():
+        g = torch.Generator(device="cuda").manual_seed(0)
+        for name, (off, shape, n) in eng.lay.slots.items():
+            v = eng.P(name)
+            if len(shape) >= 2:
+                fan_in = n // shape[0]
+                v.copy_(torch.randn(shape, generator=g, device="cuda") / fan_in ** 0.5)
+            elif not (name.endswith(".g") or name.endswith("alpha")):
+                v.zero_()
+        eng.sync_shadow()
+    model.configure_optimizer(lr=1.0, warmup=4000.0, clip_norm=1.0)
+    sync = None
+    if world > 1:
+        broadcast_params(model)
+        sync = attach(model)
+    model.train()
+    text, tl, mel, ml = synth_batch(rank)
+    sync_fn = sync.finish if sync is not None else None
+
+    log(f"[bench] rank {rank}/{world}: warm-up {args.warmup} eager steps")
+    for _ in range(max(1, args.warmup)):
+        model.train_step(text, tl, mel, ml, sync_grads=sync_fn)
+    torch.cuda.synchronize()
+    if args.no_graph:
+        def step():
+            return model.train_step(text, tl, mel, ml, sync_grads=sync_fn)
+    else:
+        run = model.capture_train_step(B_PER_GPU, TX, TY, sync_grads=sync_fn)
+        for _ in range(2):
+            run(text, tl, mel, ml)
+
+        def step():
+            return run(text, tl, mel, ml)
+    torch.cuda.synchronize()
+    log(f"[bench] timing {args.steps} steps")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    lval = loss[0].item()
+    frames = world * B_PER_GPU * TY * args.steps
+    value = frames / dt
+    log(f"[bench] {dt / args.steps * 1e3:.2f} ms/step, loss {lval:.4f}")
+
+    rl = roofline(model, text, tl, mel, ml) if rank == 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("[bench] cpu baseline (oracle on host cores)")
+        cpu = cpu_baseline()
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": "train step (fwd+loss+bwd+grad all-reduce+Adam), LJSpeech-shape synthetic batch",
+                       "global_batch": world * B_PER_GPU, "per_gpu_batch": B_PER_GPU, "seq_len": TY,
+                       "text_len": TX, "n_mels": NMEL, "params": model.n_params(), "parallelism": f"dp{world}",
+                       "graph": not args.no_graph},
+            "loss": round(lval, 5),
+            "roofline": rl,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

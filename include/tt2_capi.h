@@ -39,8 +39,6 @@ extern "C" {
 const char* tt2_last_error(void);
 int tt2_version(void);
 int tt2_init(int device);
-int tt2_set_error(int code, const char* msg);
-int tt2_check_launch(hipError_t err, const char* what);
 
 /* --------------------------------------------------------------------- GEMM
  * C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)), epi = (+bias[n]) (+res[m,n]) (act)

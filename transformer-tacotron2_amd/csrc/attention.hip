@@ -22,6 +22,7 @@
 #include <math.h>
 
 #include "tt2_capi.h"
+#include "tt2_internal.h"
 #include "tt2_common.h"
 
 namespace {

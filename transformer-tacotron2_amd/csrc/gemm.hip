@@ -22,6 +22,7 @@
 // reproducible) and applies the epilogue.
 #include "tt2_common.h"
 #include "tt2_capi.h"
+#include "tt2_internal.h"
 
 namespace {
 

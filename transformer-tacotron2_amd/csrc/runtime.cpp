@@ -4,6 +4,7 @@
 #include <string>
 
 #include "tt2_capi.h"
+#include "tt2_internal.h"
 
 namespace {
 thread_local std::string g_err;

@@ -130,7 +130,7 @@ class TransformerTTS:
         self._last = A
         return A["loss"]
 
-    def capture_train_step(self, B: int, Tx: int, Ty: int, warmup_batch=None):
+    def capture_train_step(self, B: int, Tx: int, Ty: int, sync_grads=None):
         """Capture fwd + loss + bwd + Adam for one shape into a hipGraph (via
         torch.cuda.CUDAGraph, which records our kernels on its capture stream).
         Returns a callable run(text, text_len, mel, mel_len) -> loss vector."""
@@ -139,23 +139,33 @@ class TransformerTTS:
             e.init_optimizer()
         A = e.arena(B, Tx, Ty)
         # the caller's warm-up eager steps size every workspace; capture must not allocate
-        g = torch.cuda.CUDAGraph()
         nbt_saved = dict(e.nbt)
+        hook, e.grad_ready_hook = e.grad_ready_hook, None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
+        g1 = torch.cuda.CUDAGraph()
+        g2 = torch.cuda.CUDAGraph() if sync_grads is not None else None
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
+            with torch.cuda.graph(g1, stream=s):
                 e.forward(A)
                 e.loss(A)
                 e.backward(A)
-                e.optimizer_step()
+                if g2 is None:
+                    e.optimizer_step()
+            if g2 is not None:
+                with torch.cuda.graph(g2, stream=s):
+                    e.optimizer_step()
         torch.cuda.current_stream().wait_stream(s)
+        e.grad_ready_hook = hook
         e.nbt = nbt_saved  # capture records kernels only; each replay counts one batch
-        self._graphs[(B, Tx, Ty)] = g
+        self._graphs[(B, Tx, Ty)] = (g1, g2)
 
         def run(text, text_len, mel, mel_len):
             e.stage_inputs(A, text, text_len.to(torch.int32), mel, mel_len.to(torch.int32))
-            g.replay()
+            g1.replay()
+            if g2 is not None:
+                sync_grads()          # bucketed RCCL all-reduce between the two graphs
+                g2.replay()
             for k in e.nbt:
                 e.nbt[k] += 1
             self._last = A

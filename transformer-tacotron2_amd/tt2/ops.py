@@ -87,8 +87,45 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=Non
         need = L.tt2_gemm_workspace_size(C.byref(g))
         buf = (ws or _WS).get(need)
         g.workspace, g.ws_bytes = buf.data_ptr(), buf.numel()
+    if PROBE is not None:
+        key = ("gemm", g.dtype_in, int(trans_a), int(trans_b), g.splits > 1)
+        PROBE.begin()
+        check(L.tt2_gemm(C.byref(g), stream_ptr()), "tt2_gemm")
+        PROBE.end(key, 2.0 * m * n * k)
+        return c
     check(L.tt2_gemm(C.byref(g), stream_ptr()), "tt2_gemm")
     return c
+
+
+class LaunchProbe:
+    """Brackets each GEMM launch with HIP events on the launching (current)
+    stream; used by bench.py for the live per-kernel roofline figure."""
+
+    def __init__(self):
+        self.rec = []
+        self._s = None
+
+    def begin(self):
+        self._s = torch.cuda.Event(enable_timing=True)
+        self._s.record()
+
+    def end(self, key, flops):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.rec.append((key, flops, self._s, e))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for key, flops, s, e in self.rec:
+            d = out.setdefault(key, [0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += flops
+            d[2] += s.elapsed_time(e) * 1e-3
+        return out
+
+
+PROBE: LaunchProbe | None = None
 
 
 def _attn_common(q, k, v, q_ld, k_ld, v_ld, batch, heads, tq, tk, key_len, causal, scale):
