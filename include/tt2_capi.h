@@ -66,6 +66,7 @@ typedef struct tt2_gemm_args {
   float drop_scale;
   int32_t a_conv_t, a_conv_c, a_conv_pad;
   int32_t b_conv_t, b_conv_c, b_conv_pad;
+  int32_t kernel_variant;  /* 0 auto, 1 register-staged (any shape), 2 LDS-DMA (bf16, 8-aligned inner dims) */
 } tt2_gemm_args;
 
 size_t tt2_gemm_workspace_size(const tt2_gemm_args* a);
@@ -102,7 +103,7 @@ int tt2_attn_bwd(const tt2_attn_args* a, hipStream_t stream);
 #define TT2_BN_ROWS_PER_CHUNK 64
 #define TT2_PE_BWD_BLOCKS 256
 #define TT2_LOSS_BLOCKS 256
-#define TT2_ADAM_NORM_BLOCKS 256
+#define TT2_ADAM_NORM_BLOCKS 1024
 
 /* dst[c] = beta*dst[c] + sum_r src[r*ld + c] (fixed summation order) */
 typedef struct tt2_reduce_args {

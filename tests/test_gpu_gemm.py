@@ -21,16 +21,21 @@ def _mk(shape, dtype, gen):
     return torch.randn(shape, generator=gen, dtype=torch.float32).to(dtype).cuda()
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+VARIANTS = [(torch.float32, 1), (torch.bfloat16, 1), (torch.bfloat16, 2)]
+
+
+@pytest.mark.parametrize("dtype,variant", VARIANTS)
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
-@pytest.mark.parametrize("mnk", [(200, 136, 72), (128, 128, 32), (40, 264, 520)])
-def test_gemm_layouts(dtype, ta, tb, mnk):
+@pytest.mark.parametrize("mnk", [(200, 136, 72), (128, 128, 32), (40, 264, 520), (256, 384, 1000), (96, 80, 46)])
+def test_gemm_layouts(dtype, variant, ta, tb, mnk):
     m, n, k = mnk
+    if (ta and m % 8) or (tb and n % 8) or (not ta and k % 8) or (not tb and k % 8):
+        pytest.skip("inner dims must keep 16-B aligned rows")
     g = torch.Generator().manual_seed(m * 7 + n * 3 + k + ta * 2 + tb)
     A = _mk((k, m) if ta else (m, k), dtype, g)
     B = _mk((k, n) if tb else (n, k), dtype, g)
     C = torch.empty(m, n, dtype=torch.float32, device="cuda")
-    ops.gemm(A, B, C, m, n, k, A.shape[1], B.shape[1], n, trans_a=ta, trans_b=tb)
+    ops.gemm(A, B, C, m, n, k, A.shape[1], B.shape[1], n, trans_a=ta, trans_b=tb, variant=variant)
     Am = (A.t() if ta else A).double()
     Bm = (B.t() if tb else B).double()
     ref = Am @ Bm.t()
@@ -38,9 +43,10 @@ def test_gemm_layouts(dtype, ta, tb, mnk):
     assert rel(C, ref) < tol
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_epilogue(dtype):
-    m, n, k = 300, 200, 96
+@pytest.mark.parametrize("dtype,variant", VARIANTS)
+@pytest.mark.parametrize("n", [200, 81])
+def test_gemm_epilogue(dtype, variant, n):
+    m, k = 300, 96
     g = torch.Generator().manual_seed(1)
     A, B = _mk((m, k), dtype, g), _mk((n, k), dtype, g)
     bias = torch.randn(n, generator=g).cuda()
@@ -49,7 +55,7 @@ def test_gemm_epilogue(dtype):
     seed = torch.tensor([1234], dtype=torch.int32).cuda()
     out = torch.empty(m, n, dtype=dtype, device="cuda")
     ops.gemm(A, B, out, m, n, k, k, k, n, bias=bias, res=R, ldr=n, act=ops._lib.ACT_RELU, gate=G, ldg=n,
-             gate_scale=1.7, alpha=0.5, drop=ops.Drop(seed, 77, 0.3))
+             gate_scale=1.7, alpha=0.5, drop=ops.Drop(seed, 77, 0.3), variant=variant)
     ref = 0.5 * (A.double() @ B.double().t()) + bias.double() + R.double()
     ref = ref.relu() * (G.double() != 0) * 1.7
     keep = torch.from_numpy(dropout_keep(1234, 77, m * n, 0.3)).view(m, n).cuda()
@@ -58,22 +64,22 @@ def test_gemm_epilogue(dtype):
     assert rel(out, ref) < tol
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_splitk_tanh_beta(dtype):
+@pytest.mark.parametrize("dtype,variant", VARIANTS)
+def test_gemm_splitk_tanh_beta(dtype, variant):
     m, n, k = 160, 96, 1000
     g = torch.Generator().manual_seed(2)
     A, B = _mk((k, m), dtype, g), _mk((k, n), dtype, g)
     C0 = torch.randn(m, n, generator=g).cuda()
     C = C0.clone()
     ops.gemm(A, B, C, m, n, k, m, n, n, trans_a=True, trans_b=True, beta=1.0, alpha=0.01, act=ops._lib.ACT_TANH,
-             splits=7)
+             splits=7, variant=variant)
     ref = torch.tanh(0.01 * (A.double().t() @ B.double())) + C0.double()
     assert rel(C, ref) < 1e-5
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype,variant", VARIANTS)
 @pytest.mark.parametrize("cin,cout", [(80, 136), (64, 80)])
-def test_conv_implicit_gemm(dtype, cin, cout):
+def test_conv_implicit_gemm(dtype, variant, cin, cout):
     """Conv1d(k5, pad2) fwd / dgrad / wgrad as implicit GEMMs, channels-last."""
     Bsz, T, KS, pad = 3, 37, 5, 2
     g = torch.Generator().manual_seed(cin + cout)
@@ -85,7 +91,7 @@ def test_conv_implicit_gemm(dtype, cin, cout):
     wflip = w.flip(2).permute(1, 2, 0).contiguous().to(dtype).cuda()  # [Cin][tap'][Cout]
     M = Bsz * T
     y = torch.empty(M, cout, device="cuda")
-    ops.gemm(xd, wp, y, M, cout, KS * cin, cin, KS * cin, cout, a_conv=(T, cin, pad))
+    ops.gemm(xd, wp, y, M, cout, KS * cin, cin, KS * cin, cout, a_conv=(T, cin, pad), variant=variant)
     xr = x.to(dtype).double()
     wr = w.to(dtype).double()
     dyr = dy.to(dtype).double()
@@ -93,7 +99,7 @@ def test_conv_implicit_gemm(dtype, cin, cout):
     assert rel(y, ref) < 1e-5
     # dgrad
     dx = torch.empty(M, cin, device="cuda")
-    ops.gemm(dyd, wflip, dx, M, cin, KS * cout, cout, KS * cout, cin, a_conv=(T, cout, pad))
+    ops.gemm(dyd, wflip, dx, M, cin, KS * cout, cout, KS * cout, cin, a_conv=(T, cout, pad), variant=variant)
     xq = xr.clone().requires_grad_(True)
     yq = F.conv1d(xq.transpose(1, 2), wr.clone().requires_grad_(True), padding=pad)
     (yq * dyr.transpose(1, 2)).sum().backward()
@@ -101,7 +107,7 @@ def test_conv_implicit_gemm(dtype, cin, cout):
     # wgrad: dW[co][tap][ci] = sum_m dy[m,co] x(m + tap - pad, ci)
     dw = torch.empty(cout, KS * cin, device="cuda")
     ops.gemm(dyd, xd, dw, cout, KS * cin, M, cout, cin, KS * cin, trans_a=True, trans_b=True,
-             b_conv=(T, cin, pad), splits=3)
+             b_conv=(T, cin, pad), splits=3, variant=variant)
     wq = wr.clone().requires_grad_(True)
     yq = F.conv1d(xr.transpose(1, 2), wq, padding=pad)
     (yq * dyr.transpose(1, 2)).sum().backward()

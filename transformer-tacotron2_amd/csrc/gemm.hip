@@ -236,6 +236,216 @@ hipError_t launch_t(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M,
   return hipGetLastError();
 }
 
+// =====================================================================================
+// v2 (bf16): BK = 64, LDS-DMA staging (global_load_lds_dwordx4: each lane's 16-B chunk
+// lands at lds_base + 16*lane), two LDS stages, one barrier per K-tile, XOR swizzles
+// applied on the per-lane GLOBAL source address so the lane-linear LDS image reads
+// conflict-free with ds_read_b128 (K-contiguous tiles) and ds_read_b64_tr_b16
+// (M/N-contiguous tiles).  Out-of-range / conv-padding chunks load from a zero page.
+// Epilogue: accumulators -> LDS (f32) -> 16-B vectorised epilogue + stores.
+// =====================================================================================
+constexpr int BK2 = 64;
+constexpr int TILE_BYTES = 128 * BK2 * 2;               // 16 KB per operand tile
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;             // A + B
+constexpr int EPI_LD = 132;                             // f32 words per staged C row (pad: conflict-free)
+constexpr int SMEM2 = (2 * STAGE_BYTES > 128 * EPI_LD * 4) ? 2 * STAGE_BYTES : 128 * EPI_LD * 4;
+
+__device__ __attribute__((aligned(64))) uint4 g_zero_page[64];
+
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+// swizzle of the 16-B chunk index for an M/N-contiguous tile row k (256-B rows)
+TT2_DEV int mc_swz(int k) { return ((k & 3) << 1) ^ (((k >> 3) & 1) << 3); }
+
+TT2_DEV const void* chunk_src(const OpDesc& d, int outer, int inner) {
+  if (outer >= d.outer_max || inner >= d.inner_max) return g_zero_page;
+  const bf16* base = reinterpret_cast<const bf16*>(d.p);
+  if (d.conv_t > 0) {
+    const int ts = outer % d.conv_t + inner / d.conv_c - d.conv_pad;
+    if (ts < 0 || ts >= d.conv_t) return g_zero_page;
+    return base + (int64_t)outer * d.ld + inner - (int64_t)d.conv_pad * d.conv_c;
+  }
+  return base + (int64_t)outer * d.ld + inner;
+}
+
+// issue this wave's 4 of the 16 LDS-DMA instructions of one 128 x 64 operand tile
+template <bool KC>
+TT2_DEV void issue_tile(const OpDesc& d, char* lds_tile, int r0, int k0, int lane, int wave) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int inst = wave * 4 + i;
+    const void* src;
+    if (KC) {
+      const int row = inst * 8 + (lane >> 3);
+      const int gc = (lane & 7) ^ (row & 7);
+      src = chunk_src(d, r0 + row, k0 + gc * 8);
+    } else {
+      const int kr = inst * 4 + (lane >> 4);
+      const int gc = (lane & 15) ^ mc_swz(kr);
+      src = chunk_src(d, k0 + kr, r0 + gc * 8);
+    }
+    __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(lds_tile + inst * 1024), 16, 0, 0);
+  }
+}
+
+// fragment (8 consecutive k of row r0 + (lane&15)) for k-step kk (0/1) of the 64-deep tile
+template <bool KC>
+TT2_DEV void frag2(Frag8<bf16>& f, const char* tile, int r0, int kk, int lane) {
+  if (KC) {
+    const int row = r0 + (lane & 15);
+    const int h = 4 * kk + (lane >> 4);
+    f.v = *reinterpret_cast<const bf16x8*>(tile + row * 128 + ((h ^ (row & 7)) << 4));
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int c = (r0 + 4 * p) >> 3;
+    typedef __attribute__((address_space(3))) short4v lds_s4;
+    const int k_lo = 32 * kk + 8 * g + q;
+    const int k_hi = k_lo + 4;
+    const char* a0 = tile + k_lo * 256 + ((c ^ mc_swz(k_lo)) << 4) + ((p & 1) << 3);
+    const char* a1 = tile + k_hi * 256 + ((c ^ mc_swz(k_hi)) << 4) + ((p & 1) << 3);
+    short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a0));
+    short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a1));
+    union { short s[8]; bf16x8 v; } u;
+    u.s[0] = lo[0]; u.s[1] = lo[1]; u.s[2] = lo[2]; u.s[3] = lo[3];
+    u.s[4] = hi[0]; u.s[5] = hi[1]; u.s[6] = hi[2]; u.s[7] = hi[3];
+    f.v = u.v;
+  }
+}
+
+TT2_DEV void epi_store8(const EpiParams& E, uint32_t seed, int m, int n0, int N, const float (&v)[8]) {
+  const bool full = n0 + 8 <= N;
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (full || n0 + j < N) ? epi_value(E, seed, m, n0 + j, v[j]) : 0.f;
+  const int64_t off = (int64_t)m * E.ldc + n0;
+  if (full && E.c_dt == TT2_BF16 && (off % 8) == 0) {
+    bf16x8 x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = (bf16)o[j];
+    *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(E.c) + off) = x;
+  } else if (full && E.c_dt == TT2_F32 && (off % 4) == 0) {
+    float* c = reinterpret_cast<float*>(E.c) + off;
+    *reinterpret_cast<f32x4*>(c) = f32x4{o[0], o[1], o[2], o[3]};
+    *reinterpret_cast<f32x4*>(c + 4) = f32x4{o[4], o[5], o[6], o[7]};
+  } else {
+    for (int j = 0; j < 8; ++j)
+      if (n0 + j < N) st_any(E.c, off + j, E.c_dt, o[j]);
+  }
+}
+
+template <bool AK, bool BKC>
+__global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
+                                                      int k_split, float* ws, int ntm, int ntn) {
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware tile order: blocks b and b+8 share an XCD, so give each XCD a
+  // contiguous run of tiles (walking n for a fixed m: the A row panel stays in that L2).
+  const int nt = ntm * ntn;
+  const int bid = blockIdx.x;
+  const int q = nt / 8, rr = nt % 8, x = bid % 8;
+  const int tile = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + bid / 8;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const int kb = blockIdx.y * k_split;
+  const int ke = min(K, kb + k_split);
+  if (AK) A.inner_max = ke; else A.outer_max = ke;
+  if (BKC) B.inner_max = ke; else B.outer_max = ke;
+  const int nkt = (ke - kb + BK2 - 1) / BK2;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue_tile<AK>(A, smem, m0, kb, lane, wave);
+  issue_tile<BKC>(B, smem + TILE_BYTES, n0, kb, lane, wave);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const char* sa = smem + (kt & 1) * STAGE_BYTES;
+    const char* sb = sa + TILE_BYTES;
+    if (kt + 1 < nkt) {
+      char* na = smem + ((kt + 1) & 1) * STAGE_BYTES;
+      issue_tile<AK>(A, na, m0, kb + (kt + 1) * BK2, lane, wave);
+      issue_tile<BKC>(B, na + TILE_BYTES, n0, kb + (kt + 1) * BK2, lane, wave);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      Frag8<bf16> fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) frag2<AK>(fa[i], sa, wm * 64 + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) frag2<BKC>(fb[j], sb, wn * 64 + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mma16(fa[i], fb[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // stage C (f32) through LDS: row-major [128][EPI_LD]
+  float* cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cs[(wm * 64 + 16 * i + 4 * (lane >> 4) + r) * EPI_LD + wn * 64 + 16 * j + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
+#pragma unroll 2
+  for (int it = 0; it < 8; ++it) {
+    const int id = tid + NT * it;
+    const int row = id >> 4, c8 = (id & 15) * 8;
+    const int m = m0 + row, n = n0 + c8;
+    if (m >= M || n >= N) continue;
+    float v[8];
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + row * EPI_LD + c8);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * EPI_LD + c8 + 4);
+    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+    v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+    if (ws) {
+      float* w = ws + ((int64_t)blockIdx.y * M + m) * N + n;
+      if (n + 8 <= N && (N % 4) == 0) {
+        *reinterpret_cast<f32x4*>(w) = lo;
+        *reinterpret_cast<f32x4*>(w + 4) = hi;
+      } else {
+        for (int j = 0; j < 8; ++j)
+          if (n + j < N) w[j] = v[j];
+      }
+    } else {
+      epi_store8(E, seed, m, n, N, v);
+    }
+  }
+}
+
+template <bool AK, bool BKC>
+hipError_t launch2(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
+                   hipStream_t s) {
+  int k_split = K;
+  if (splits > 1) {
+    k_split = ((K + splits - 1) / splits + BK2 - 1) / BK2 * BK2;
+    splits = (K + k_split - 1) / k_split;
+  }
+  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
+  dim3 grid(ntm * ntn, splits);
+  hipLaunchKernelGGL((gemm2_kernel<AK, BKC>), grid, dim3(NT), 0, s, A, B, E, M, N, K, k_split,
+                     splits > 1 ? ws : nullptr, ntm, ntn);
+  if (splits > 1) {
+    const int64_t total = (int64_t)M * N;
+    int64_t nb = (total + 255) / 256;
+    int blocks = (int)(nb < 4096 ? nb : 4096);
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, splits, E, M, N);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" size_t tt2_gemm_workspace_size(const tt2_gemm_args* a) {
@@ -279,6 +489,16 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   const int sp = a->splits > 1 ? a->splits : 1;
 
   hipError_t err;
+  // v2 (LDS-DMA) path: bf16, every chunk either fully inside or fully outside its row
+  const bool v2 = a->dtype_in == TT2_BF16 && a->kernel_variant != 1 &&
+                  A.inner_max % 8 == 0 && B.inner_max % 8 == 0;
+  if (v2) {
+    if (!a->trans_a && !a->trans_b) err = launch2<true, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    else if (!a->trans_a && a->trans_b) err = launch2<true, false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    else if (a->trans_a && !a->trans_b) err = launch2<false, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    else err = launch2<false, false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    return tt2_check_launch(err, "tt2_gemm");
+  }
 #define TT2_GEMM_CASE(T)                                                                              \
   if (!a->trans_a && !a->trans_b) err = launch_t<T, true, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);   \
   else if (!a->trans_a && a->trans_b) err = launch_t<T, true, false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \

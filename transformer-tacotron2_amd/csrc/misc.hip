@@ -27,22 +27,71 @@ TT2_DEV void stf(void* p, int64_t i, int dt, float v) {
 }
 
 // dst[c] = beta * dst[c] + sum_r src[r * ld + c]   (fixed order)
-__global__ void reduce_rows_kernel(const float* src, int rows, int cols, int64_t ld, float* dst, float beta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
+// block = 64 columns x 4 row groups; LDS combine in a fixed order.
+__global__ __launch_bounds__(NT) void reduce_rows_kernel(const float* src, int rows, int cols, int64_t ld, float* dst,
+                                                         float beta) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += src[(int64_t)r * ld + c];
-  dst[c] = beta != 0.f ? beta * dst[c] + s : s;
+  if (c < cols)
+    for (int r = g; r < rows; r += 4) s += src[(int64_t)r * ld + c];
+  red[g][cl] = s;
+  __syncthreads();
+  if (g == 0 && c < cols) {
+    s = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+    dst[c] = beta != 0.f ? beta * dst[c] + s : s;
+  }
 }
 
-// partial column sums of a [M, N] matrix: part[blockIdx.y][n]
-__global__ void colsum_partial_kernel(const void* x, int dt, int64_t ld, int M, int N, int rows_per, float* part) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+// partial column sums of a [M, N] matrix: part[blockIdx.y][n] over rows [y*rows_per, ...).
+// block = 64 columns (8 lanes x 8 columns, 16-B loads) x 32 row lanes; LDS combine.
+template <typename T>
+__global__ __launch_bounds__(NT) void colsum_partial_kernel(const T* x, int64_t ld, int M, int N, int rows_per,
+                                                            int vec, float* part) {
+  __shared__ float red[32][65];
+  const int cg = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int n0 = blockIdx.x * 64 + cg * 8;
   const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
-  float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += ldf(x, (int64_t)r * ld + n, dt);
-  part[(int64_t)blockIdx.y * N + n] = s;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (vec && n0 + 8 <= N) {
+    for (int r = r0 + rg; r < r1; r += 32) {
+      const T* p = x + (int64_t)r * ld + n0;
+      ChunkV<T> c0 = ld_chunk<T>(p);
+      if (Chunk<T>::N == 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += to_f32(c0.e[j % Chunk<T>::N]);
+      } else {
+        ChunkV<T> c1 = ld_chunk<T>(p + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { acc[j] += to_f32(c0.e[j]); acc[4 + j] += to_f32(c1.e[j]); }
+      }
+    }
+  } else {
+    for (int r = r0 + rg; r < r1; r += 32)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (n0 + j < N) acc[j] += to_f32(x[(int64_t)r * ld + n0 + j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rg][cg * 8 + j] = acc[j];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int n = blockIdx.x * 64 + threadIdx.x;
+    float s = 0.f;
+    for (int r = 0; r < 32; ++r) s += red[r][threadIdx.x];
+    if (n < N) part[(int64_t)blockIdx.y * N + n] = s;
+  }
+}
+
+// number of row chunks for a colsum over [m, n]: ~1024 blocks total, >= 32 rows each
+int colsum_chunks(int m, int n) {
+  const int cb = (n + 63) / 64;
+  int r = 1024 / cb;
+  if (r < 1) r = 1;
+  const int max_r = (m + 31) / 32;
+  if (r > max_r) r = max_r;
+  return r < 1 ? 1 : r;
 }
 
 // ------------------------------------------------------------ embedding
@@ -220,7 +269,13 @@ __global__ void conv_wflip_kernel(const T* w, T* wd, int Cout, int Cin, int K) {
 __global__ __launch_bounds__(NT) void sumsq_kernel(const float* g, int64_t n, float* part) {
   __shared__ float red[NT / 64];
   float s = 0.f;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) s += g[i] * g[i];
+  const int64_t n4 = n / 4;
+  const f32x4* g4 = reinterpret_cast<const f32x4*>(g);
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
+    const f32x4 v = g4[i];
+    s += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  }
+  for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) s += g[i] * g[i];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -234,19 +289,30 @@ __global__ __launch_bounds__(NT) void sumsq_kernel(const float* g, int64_t n, fl
 struct AdamArgs {
   float* p; const float* g; float* m; float* v; bf16* shadow;
   int64_t n;
-  const float* norm_part; int n_part;   // clip: sum of partial squared norms
-  int32_t* step;                        // device step counter (read; bumped by tt2_step_bump)
+  const float* sumsq;   // clip: global squared gradient norm (device scalar) or null
+  int32_t* step;        // device step counter (read; bumped by tt2_step_bump)
   float lr, beta1, beta2, eps, wd, clip, warmup, d_model_rsqrt;
   int noam;
 };
 
+TT2_DEV void adam_one(const AdamArgs& a, int64_t i, float g, float lr, float step_size, float bc2_sqrt) {
+  float p = a.p[i];
+  if (a.wd != 0.f) p -= lr * a.wd * p;  // decoupled (AdamW) weight decay
+  const float m = a.beta1 * a.m[i] + (1.f - a.beta1) * g;
+  const float v = a.beta2 * a.v[i] + (1.f - a.beta2) * g * g;
+  a.m[i] = m;
+  a.v[i] = v;
+  p -= step_size * m / (sqrtf(v) / bc2_sqrt + a.eps);
+  a.p[i] = p;
+  if (a.shadow) a.shadow[i] = (bf16)p;
+}
+
+// one thread updates 4 consecutive parameters (n is a multiple of 16: slots are 16-aligned)
 __global__ __launch_bounds__(NT) void adam_kernel(AdamArgs a) {
   const int step = *a.step + 1;
   float scale = 1.f;
-  if (a.clip > 0.f && a.norm_part) {
-    float s = 0.f;
-    for (int i = 0; i < a.n_part; ++i) s += a.norm_part[i];
-    const float nrm = sqrtf(s);
+  if (a.clip > 0.f && a.sumsq) {
+    const float nrm = sqrtf(*a.sumsq);
     if (nrm > a.clip) scale = a.clip / (nrm + 1e-6f);
   }
   float lr = a.lr;
@@ -255,18 +321,35 @@ __global__ __launch_bounds__(NT) void adam_kernel(AdamArgs a) {
   const float bc2 = 1.f - powf(a.beta2, (float)step);
   const float step_size = lr / bc1;
   const float bc2_sqrt = sqrtf(bc2);
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * NT) {
-    const float g = a.g[i] * scale;
-    float p = a.p[i];
-    if (a.wd != 0.f) p -= lr * a.wd * p;  // decoupled (AdamW) weight decay
-    const float m = a.beta1 * a.m[i] + (1.f - a.beta1) * g;
-    const float v = a.beta2 * a.v[i] + (1.f - a.beta2) * g * g;
-    a.m[i] = m;
-    a.v[i] = v;
-    p -= step_size * m / (sqrtf(v) / bc2_sqrt + a.eps);
-    a.p[i] = p;
-    if (a.shadow) a.shadow[i] = (bf16)p;
+  const int64_t n4 = a.n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
+    const f32x4 g = reinterpret_cast<const f32x4*>(a.g)[i];
+    const f32x4 p = reinterpret_cast<const f32x4*>(a.p)[i];
+    const f32x4 m = reinterpret_cast<const f32x4*>(a.m)[i];
+    const f32x4 v = reinterpret_cast<const f32x4*>(a.v)[i];
+    f32x4 po, mo, vo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = g[j] * scale;
+      float pj = p[j];
+      if (a.wd != 0.f) pj -= lr * a.wd * pj;
+      mo[j] = a.beta1 * m[j] + (1.f - a.beta1) * gj;
+      vo[j] = a.beta2 * v[j] + (1.f - a.beta2) * gj * gj;
+      po[j] = pj - step_size * mo[j] / (sqrtf(vo[j]) / bc2_sqrt + a.eps);
+    }
+    reinterpret_cast<f32x4*>(a.p)[i] = po;
+    reinterpret_cast<f32x4*>(a.m)[i] = mo;
+    reinterpret_cast<f32x4*>(a.v)[i] = vo;
+    if (a.shadow) {
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 sh;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sh[j] = (bf16)po[j];
+      reinterpret_cast<bf16x4*>(a.shadow)[i] = sh;
+    }
   }
+  for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)NT + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * NT)
+    adam_one(a, i, a.g[i] * scale, lr, step_size, bc2_sqrt);
 }
 
 __global__ void step_bump_kernel(int32_t* step, uint32_t* seed) {
@@ -281,25 +364,31 @@ __global__ void step_bump_kernel(int32_t* step, uint32_t* seed) {
 // =============================================================== C ABI
 extern "C" int tt2_reduce_rows(const tt2_reduce_args* p, hipStream_t s) {
   if (p->cols <= 0) return TT2_OK;
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((p->cols + 255) / 256), dim3(256), 0, s, p->src, p->rows, p->cols,
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((p->cols + 63) / 64), dim3(NT), 0, s, p->src, p->rows, p->cols,
                      p->ld, p->dst, p->beta);
   return tt2_check_launch(hipGetLastError(), "tt2_reduce_rows");
 }
 
 extern "C" size_t tt2_colsum_workspace_size(int m, int n) {
-  const int R = (m + TT2_COLSUM_ROWS - 1) / TT2_COLSUM_ROWS;
-  return (size_t)R * n * sizeof(float);
+  return (size_t)colsum_chunks(m, n) * n * sizeof(float);
 }
 
 extern "C" int tt2_colsum(const void* x, int dtype, int64_t ld, int m, int n, float* dst, float beta, void* ws,
                           size_t ws_bytes, hipStream_t s) {
   if (n <= 0) return TT2_OK;
   if (ws_bytes < tt2_colsum_workspace_size(m, n)) return tt2_set_error(TT2_E_INVALID, "tt2_colsum: workspace");
-  const int R = (m + TT2_COLSUM_ROWS - 1) / TT2_COLSUM_ROWS;
+  const int R = colsum_chunks(m, n);
+  const int rows_per = (m + R - 1) / R;
   float* part = reinterpret_cast<float*>(ws);
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3((n + 255) / 256, R), dim3(256), 0, s, x, dtype, ld, m, n,
-                     TT2_COLSUM_ROWS, part);
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, R, n, (int64_t)n, dst, beta);
+  const int esz = dtype == TT2_DT_BF16 ? 2 : 4;
+  const int vec = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && ((ld * esz) % 16 == 0);
+  dim3 g((n + 63) / 64, R);
+  if (dtype == TT2_DT_BF16)
+    hipLaunchKernelGGL(colsum_partial_kernel<bf16>, g, dim3(NT), 0, s, (const bf16*)x, ld, m, n, rows_per, vec, part);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<float>, g, dim3(NT), 0, s, (const float*)x, ld, m, n, rows_per, vec,
+                       part);
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((n + 63) / 64), dim3(NT), 0, s, part, R, n, (int64_t)n, dst, beta);
   return tt2_check_launch(hipGetLastError(), "tt2_colsum");
 }
 
@@ -353,7 +442,7 @@ extern "C" int tt2_posenc_bwd(const tt2_pe_args* p, hipStream_t s) {
   else
     hipLaunchKernelGGL(pe_bwd_kernel<float>, dim3(TT2_PE_BWD_BLOCKS), dim3(NT), 0, s, (const float*)p->dout, p->pe,
                        (float*)p->dx, part, p->m, p->c, p->t, d);
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(1), dim3(64), 0, s, part, TT2_PE_BWD_BLOCKS, 1, (int64_t)1,
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(1), dim3(NT), 0, s, part, TT2_PE_BWD_BLOCKS, 1, (int64_t)1,
                      p->dalpha, 0.f);
   return tt2_check_launch(hipGetLastError(), "tt2_posenc_bwd");
 }
@@ -404,7 +493,7 @@ extern "C" int tt2_conv_weight_flip(const void* w, void* wd, int cout, int cin, 
   return tt2_check_launch(hipGetLastError(), "tt2_conv_weight_flip");
 }
 
-extern "C" size_t tt2_adam_workspace_size(void) { return TT2_ADAM_NORM_BLOCKS * sizeof(float); }
+extern "C" size_t tt2_adam_workspace_size(void) { return (TT2_ADAM_NORM_BLOCKS + 16) * sizeof(float); }
 
 extern "C" int tt2_adam_step(const tt2_adam_args* p, hipStream_t s) {
   AdamArgs a{};
@@ -413,15 +502,21 @@ extern "C" int tt2_adam_step(const tt2_adam_args* p, hipStream_t s) {
   a.lr = p->lr; a.beta1 = p->beta1; a.beta2 = p->beta2; a.eps = p->eps; a.wd = p->weight_decay;
   a.clip = p->clip_norm; a.warmup = p->warmup; a.noam = p->noam;
   a.d_model_rsqrt = p->d_model > 0 ? 1.f / sqrtf((float)p->d_model) : 1.f;
+  if ((reinterpret_cast<uintptr_t>(p->params) | reinterpret_cast<uintptr_t>(p->grads) |
+       reinterpret_cast<uintptr_t>(p->exp_avg) | reinterpret_cast<uintptr_t>(p->exp_avg_sq)) % 16 ||
+      reinterpret_cast<uintptr_t>(p->shadow_bf16) % 8)
+    return tt2_set_error(TT2_E_INVALID, "tt2_adam_step: buffers must be 16-B aligned");
   if (p->clip_norm > 0.f) {
     if (!p->workspace || p->ws_bytes < tt2_adam_workspace_size())
       return tt2_set_error(TT2_E_INVALID, "tt2_adam_step: workspace");
     float* part = reinterpret_cast<float*>(p->workspace);
+    float* total = part + TT2_ADAM_NORM_BLOCKS;
     hipLaunchKernelGGL(sumsq_kernel, dim3(TT2_ADAM_NORM_BLOCKS), dim3(NT), 0, s, p->grads, p->n, part);
-    a.norm_part = part;
-    a.n_part = TT2_ADAM_NORM_BLOCKS;
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3(1), dim3(NT), 0, s, part, TT2_ADAM_NORM_BLOCKS, 1, (int64_t)1, total,
+                       0.f);
+    a.sumsq = total;
   }
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(p->n, NT * 4)), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(p->n / 4)), dim3(NT), 0, s, a);
   return tt2_check_launch(hipGetLastError(), "tt2_adam_step");
 }
 

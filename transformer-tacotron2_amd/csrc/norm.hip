@@ -180,26 +180,38 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
   a.part[((int64_t)blockIdx.y * 2 + 1) * a.C + c] = m2;
 }
 
-__global__ void bn_finalize_kernel(BnArgs a) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.C) return;
+// Chan/Welford combine of per-chunk (mean, M2); 64 columns x 4 chunk groups per block.
+TT2_DEV void chan_add(double& n, double& mu, double& m2, double nb, double mb, double m2b) {
+  if (nb <= 0) return;
+  const double nn = n + nb;
+  const double d = mb - mu;
+  mu += d * nb / nn;
+  m2 += m2b + d * d * n * nb / nn;
+  n = nn;
+}
+
+__global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
+  __shared__ double red[3][4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   if (!a.training) {
-    a.mean[c] = a.run_mean[c];
-    a.rstd[c] = rsqrtf(a.run_var[c] + a.eps);
+    if (g == 0 && c < a.C) {
+      a.mean[c] = a.run_mean[c];
+      a.rstd[c] = rsqrtf(a.run_var[c] + a.eps);
+    }
     return;
   }
   double n = 0.0, mu = 0.0, m2 = 0.0;
-  for (int r = 0; r < a.R; ++r) {
-    const int nb = min(a.rows_per, a.M - r * a.rows_per);
-    if (nb <= 0) break;
-    const double mb = a.part[((int64_t)r * 2 + 0) * a.C + c];
-    const double m2b = a.part[((int64_t)r * 2 + 1) * a.C + c];
-    const double nn = n + nb;
-    const double d = mb - mu;
-    mu += d * nb / nn;
-    m2 += m2b + d * d * n * nb / nn;
-    n = nn;
-  }
+  if (c < a.C)
+    for (int r = g; r < a.R; r += 4) {
+      const int nb = min(a.rows_per, a.M - r * a.rows_per);
+      chan_add(n, mu, m2, nb, a.part[((int64_t)r * 2 + 0) * a.C + c], a.part[((int64_t)r * 2 + 1) * a.C + c]);
+    }
+  red[0][g][cl] = n; red[1][g][cl] = mu; red[2][g][cl] = m2;
+  __syncthreads();
+  if (g != 0 || c >= a.C) return;
+  n = 0.0; mu = 0.0; m2 = 0.0;
+  for (int k = 0; k < 4; ++k) chan_add(n, mu, m2, red[0][k][cl], red[1][k][cl], red[2][k][cl]);
   const double var = n > 0 ? m2 / n : 0.0;
   a.mean[c] = (float)mu;
   a.rstd[c] = (float)(1.0 / sqrt(var + a.eps));
@@ -257,16 +269,22 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
   a.part[((int64_t)blockIdx.y * 2 + 1) * a.C + c] = s2;
 }
 
-__global__ void bn_bwd_finalize_kernel(BnArgs a) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.C) return;
+__global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(BnArgs a) {
+  __shared__ float red[2][4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float s1 = 0.f, s2 = 0.f;
-  for (int r = 0; r < a.R; ++r) {
-    s1 += a.part[((int64_t)r * 2 + 0) * a.C + c];
-    s2 += a.part[((int64_t)r * 2 + 1) * a.C + c];
-  }
-  a.dbeta[c] = s1;
-  a.dgamma[c] = s2;
+  if (c < a.C)
+    for (int r = g; r < a.R; r += 4) {
+      s1 += a.part[((int64_t)r * 2 + 0) * a.C + c];
+      s2 += a.part[((int64_t)r * 2 + 1) * a.C + c];
+    }
+  red[0][g][cl] = s1;
+  red[1][g][cl] = s2;
+  __syncthreads();
+  if (g != 0 || c >= a.C) return;
+  a.dbeta[c] = (red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]);
+  a.dgamma[c] = (red[1][0][cl] + red[1][1][cl]) + (red[1][2][cl] + red[1][3][cl]);
 }
 
 template <typename T, typename TD>
@@ -367,7 +385,7 @@ extern "C" int tt2_batchnorm_fwd(const tt2_bn_args* p, hipStream_t s) {
     if (bf) hipLaunchKernelGGL(bn_stats_kernel<bf16>, g, dim3(NT), 0, s, a);
     else hipLaunchKernelGGL(bn_stats_kernel<float>, g, dim3(NT), 0, s, a);
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + 255) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + 63) / 64), dim3(NT), 0, s, a);
   const int g = grid_for((int64_t)p->m * p->c);
   if (bf) hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(g), dim3(NT), 0, s, a);
   else hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(g), dim3(NT), 0, s, a);
@@ -388,7 +406,7 @@ extern "C" int tt2_batchnorm_bwd(const tt2_bn_args* p, hipStream_t s) {
   else if (dbf) hipLaunchKernelGGL((KER<float, bf16>), grid, dim3(NT), 0, s, a);                \
   else hipLaunchKernelGGL((KER<float, float>), grid, dim3(NT), 0, s, a);
   TT2_BN_DISPATCH(bn_bwd_stats_kernel, g)
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + 255) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + 63) / 64), dim3(NT), 0, s, a);
   const int ga = grid_for((int64_t)p->m * p->c);
   TT2_BN_DISPATCH(bn_bwd_apply_kernel, dim3(ga))
 #undef TT2_BN_DISPATCH

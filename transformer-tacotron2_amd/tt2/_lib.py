@@ -37,6 +37,7 @@ class GemmArgs(C.Structure):
         ("drop_site", u32), ("drop_thr", u32), ("drop_scale", f32),
         ("a_conv_t", i32), ("a_conv_c", i32), ("a_conv_pad", i32),
         ("b_conv_t", i32), ("b_conv_c", i32), ("b_conv_pad", i32),
+        ("kernel_variant", i32),
     ]
 
 
