@@ -209,6 +209,18 @@ __global__ __launch_bounds__(NT) void gemm_kernel(OpDesc A, OpDesc B, EpiParams 
 __global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int M, int N) {
   const int64_t total = (int64_t)M * N;
   const uint32_t seed = E.drop.thr ? *E.drop.seed : 0u;
+  if ((N & 3) == 0) {
+    // 4 consecutive columns per thread (16-B partial-slab loads), fixed split order
+    const int64_t t4 = total / 4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < t4; i += (int64_t)gridDim.x * blockDim.x) {
+      f32x4 v = reinterpret_cast<const f32x4*>(ws)[i];
+      for (int z = 1; z < splits; ++z) v += reinterpret_cast<const f32x4*>(ws + z * total)[i];
+      const int m = (int)(4 * i / N), n = (int)(4 * i % N);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st_any(E.c, (int64_t)m * E.ldc + n + j, E.c_dt, epi_value(E, seed, m, n + j, v[j]));
+    }
+    return;
+  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     float v = 0.f;
     for (int z = 0; z < splits; ++z) v += ws[z * total + i];

@@ -27,19 +27,28 @@ TT2_DEV void stf(void* p, int64_t i, int dt, float v) {
 }
 
 // dst[c] = beta * dst[c] + sum_r src[r * ld + c]   (fixed order)
-// block = 64 columns x 4 row groups; LDS combine in a fixed order.
+// block = 16 columns x 16 row groups (short dependent chains); LDS combine in a fixed order.
+constexpr int RR_COLS = 16;
 __global__ __launch_bounds__(NT) void reduce_rows_kernel(const float* src, int rows, int cols, int64_t ld, float* dst,
                                                          float beta) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  float s = 0.f;
-  if (c < cols)
-    for (int r = g; r < rows; r += 4) s += src[(int64_t)r * ld + c];
-  red[g][cl] = s;
+  __shared__ float red[16][RR_COLS + 1];
+  const int cl = threadIdx.x & (RR_COLS - 1), g = threadIdx.x / RR_COLS;
+  const int c = blockIdx.x * RR_COLS + cl;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < cols) {
+    int r = g;
+    for (; r + 16 < rows; r += 32) {
+      s0 += src[(int64_t)r * ld + c];
+      s1 += src[(int64_t)(r + 16) * ld + c];
+    }
+    if (r < rows) s0 += src[(int64_t)r * ld + c];
+  }
+  red[g][cl] = s0 + s1;
   __syncthreads();
   if (g == 0 && c < cols) {
-    s = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][cl];
     dst[c] = beta != 0.f ? beta * dst[c] + s : s;
   }
 }
@@ -364,7 +373,8 @@ __global__ void step_bump_kernel(int32_t* step, uint32_t* seed) {
 // =============================================================== C ABI
 extern "C" int tt2_reduce_rows(const tt2_reduce_args* p, hipStream_t s) {
   if (p->cols <= 0) return TT2_OK;
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((p->cols + 63) / 64), dim3(NT), 0, s, p->src, p->rows, p->cols,
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((p->cols + RR_COLS - 1) / RR_COLS), dim3(NT), 0, s, p->src, p->rows,
+                     p->cols,
                      p->ld, p->dst, p->beta);
   return tt2_check_launch(hipGetLastError(), "tt2_reduce_rows");
 }
@@ -388,7 +398,8 @@ extern "C" int tt2_colsum(const void* x, int dtype, int64_t ld, int m, int n, fl
   else
     hipLaunchKernelGGL(colsum_partial_kernel<float>, g, dim3(NT), 0, s, (const float*)x, ld, m, n, rows_per, vec,
                        part);
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((n + 63) / 64), dim3(NT), 0, s, part, R, n, (int64_t)n, dst, beta);
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((n + RR_COLS - 1) / RR_COLS), dim3(NT), 0, s, part, R, n, (int64_t)n,
+                     dst, beta);
   return tt2_check_launch(hipGetLastError(), "tt2_colsum");
 }
 
