@@ -83,6 +83,46 @@ def cpu_baseline(budget_s: float = 20.0):
                       f"{n} timed steps after 1 warm-up, {threads} torch threads of {cores} visible cores"}
 
 
+DEC_B, DEC_T = 32, 800
+# algorithmic HBM bytes of one forced 800-frame decode at B=32:
+# bf16 weights read per step + self-KV cache reads (sum over t) + cross-KV reads per step
+DEC_BYTES = 2.019e11
+
+
+def decode_bench(model, reps: int = 3):
+    """cfg3: AR decode B=32, 128 phonemes, forced 800 frames, bf16, hipGraph step."""
+    from tt2.infer import Decoder
+    g = torch.Generator().manual_seed(1)
+    text = torch.randint(1, 80, (DEC_B, TX), generator=g).cuda()
+    tl = torch.full((DEC_B,), TX, dtype=torch.int32, device="cuda")
+    was = model.engine.training
+    model.eval()
+    dec = Decoder(model.engine, DEC_B, TX, DEC_T)
+    dec.encode(text, tl)
+    dec.capture()
+    dec.reset()
+    dec.decode_loop(16)            # warm
+    times = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dec.encode(text, tl)
+        dec.reset()
+        dec.decode_loop(DEC_T, stop_threshold=None)
+        mel, _ = dec.postnet(DEC_T, None)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    model.train(was)
+    dt = min(times)
+    return {"value": round(DEC_B * DEC_T / dt, 1), "unit": "frames/s", "ms_per_run": round(dt * 1e3, 2),
+            "ms_per_frame_step": round(dt / DEC_T * 1e3, 4),
+            "config": {"workload": "AR decode: encoder + 800 forced hipGraph decode steps + post-net", "batch": DEC_B,
+                       "text_len": TX, "frames": DEC_T, "dtype": "bf16"},
+            "roofline": {"bound": "hbm", "achieved": round(DEC_BYTES / dt / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+                         "frac": round(DEC_BYTES / dt / 8e12, 4), "traffic": None,
+                         "note": "whole-run algorithmic bytes / wall time (launch-bound: ~80 kernels per step)"}}
+
+
 def roofline(model, text, tl, mel, ml):
     """Live per-launch timing of the dominant kernel family in one eager step."""
     from tt2 import ops
@@ -117,6 +157,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-decode", action="store_true", help="skip the cfg3 decode measurement")
     args = ap.parse_args()
 
     from tt2.config import TTSConfig
@@ -186,6 +227,11 @@ def main():
     log(f"[bench] {dt / args.steps * 1e3:.2f} ms/step, loss {lval:.4f}")
 
     rl = roofline(model, text, tl, mel, ml) if rank == 0 else None
+    dec = None
+    if rank == 0 and world == 1 and not args.no_decode:
+        log("[bench] decode (cfg3)")
+        dec = decode_bench(model)
+        log(f"[bench] decode {dec['value']:.0f} frames/s ({dec['ms_per_frame_step']} ms/step)")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[bench] cpu baseline (oracle on host cores)")
@@ -202,6 +248,7 @@ def main():
             "loss": round(lval, 5),
             "roofline": rl,
             "cpu_baseline": cpu,
+            "decode": dec,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -97,6 +97,29 @@ typedef struct tt2_attn_args {
 int tt2_attn_fwd(const tt2_attn_args* a, hipStream_t stream);
 int tt2_attn_bwd(const tt2_attn_args* a, hipStream_t stream);
 
+/* ------------------------------------------------------------------ decode
+ * One query row per batch element (the AR decode step):
+ * out[b*o_ld + 64h ..] = softmax(scale q k^T) v over keys j < n_b of batch b,
+ * key j of batch b at k + b*k_bstride + j*k_ld + 64h.  n_b = min(tk, *t_ptr + 1
+ * if t_ptr, key_len[b] if key_len): t_ptr is the DEVICE step counter, so the
+ * call is replayable from a captured graph. */
+typedef struct tt2_attn_decode_args {
+  const void* q; const void* k; const void* v; void* out;
+  int64_t q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld;
+  const int32_t* key_len;
+  const int32_t* t_ptr;
+  int32_t batch, heads, head_dim, tk, dtype;
+  float scale;
+} tt2_attn_decode_args;
+int tt2_attn_decode(const tt2_attn_decode_args* a, hipStream_t stream);
+/* cache[b*c_bstride + (*t_ptr)*c_ld + c] = src[b*src_ld + c], c < n */
+int tt2_kv_append(const void* src, int64_t src_ld, void* cache, int64_t c_bstride, int64_t c_ld, int n, int batch,
+                  const int32_t* t_ptr, int dtype, hipStream_t stream);
+/* heads [batch, heads_ld] f32 -> mel_seq[b, t, :], stop_seq[b, t], prev[b, :] (prev_dtype);
+ * then *t_ptr += 1 and *seed += 1 (seed may be NULL) */
+int tt2_decode_emit(const float* heads, int64_t heads_ld, int batch, int n_mels, int t_max, float* mel_seq,
+                    float* stop_seq, void* prev, int prev_dtype, int32_t* t_ptr, uint32_t* seed, hipStream_t stream);
+
 /* ------------------------------------------------------------- reductions */
 #define TT2_COLSUM_ROWS 128
 #define TT2_LN_BWD_BLOCKS 256
@@ -171,12 +194,14 @@ int tt2_embedding_fwd(const int64_t* ids, const void* table, void* out, int m, i
 int tt2_embedding_bwd(const int64_t* ids, const void* dout, float* dtable, int m, int c, int vocab, int pad_idx,
                       int dtype, hipStream_t stream);
 
-/* out = drop(x + alpha*pe[row % t + t_offset]); bwd: dx = drop'(dout), *dalpha = sum dx*pe */
+/* out = drop(x + alpha*pe[row % t + t_offset (+ *t_ptr if t_ptr)]); bwd: dx = drop'(dout),
+ * *dalpha = sum dx*pe */
 typedef struct tt2_pe_args {
   const void* x; const void* dout; void* out; void* dx;
   const float* alpha; const float* pe; float* dalpha;
   void* workspace; size_t ws_bytes;
   const uint32_t* drop_seed;
+  const int32_t* t_ptr;
   int32_t m, c, t, t_offset, dtype;
   uint32_t drop_site, drop_thr;
   float drop_scale;

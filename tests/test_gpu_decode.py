@@ -1,0 +1,76 @@
+"""AR decode path vs the CPU oracle (GPU): forced length, prenet dropout off.
+fp32 mode must match within 1e-3; the hipGraph replay must equal eager launches."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from tt2.config import TTSConfig  # noqa: E402
+from tt2.infer import Decoder  # noqa: E402
+from tt2.model import TransformerTTS  # noqa: E402
+from tt2 import ops  # noqa: E402
+from tt2_oracle import OracleConfig, TransformerTTSOracle, init_deterministic  # noqa: E402
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def setup(dtype):
+    oracle = init_deterministic(TransformerTTSOracle(OracleConfig()), 3).eval()
+    model = TransformerTTS(TTSConfig(), dtype=dtype).eval()
+    model.load_state_dict(oracle.state_dict())
+    g = torch.Generator().manual_seed(5)
+    B, Tx = 3, 17
+    text = torch.randint(1, 80, (B, Tx), generator=g)
+    tl = torch.tensor([17, 12, 6])
+    for b in range(B):
+        text[b, tl[b]:] = 0
+    return oracle, model, text, tl
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 6e-2)])
+def test_decode_matches_oracle(dtype, tol):
+    oracle, model, text, tl = setup(dtype)
+    T = 14
+    ref_after, _, ref_before, ref_stop = oracle.infer(text, tl, T, force_len=True)
+    after, out_len = model.infer(text, tl, T, stop_threshold=None)
+    assert after.shape == ref_after.shape
+    assert rel(after, ref_after) < tol
+    dec = model._decoders[(3, 17, T, False)]
+    assert rel(dec.mel_seq[:, :T], ref_before) < tol
+    assert rel(dec.stop_seq[:, :T], ref_stop) < tol
+    assert (out_len.cpu() == T).all()
+
+
+def test_graph_replay_equals_eager():
+    _, model, text, tl = setup(torch.bfloat16)
+    T = 10
+    a1, _ = model.infer(text, tl, T, stop_threshold=None, use_graph=True)
+    a2, _ = model.infer(text, tl, T, stop_threshold=None, use_graph=False)
+    assert torch.equal(a1, a2)
+
+
+def test_stop_token_early_exit():
+    _, model, text, tl = setup(torch.bfloat16)
+    e = model.engine
+    with torch.no_grad():   # push the stop logit up so every utterance stops immediately
+        e.P("heads.b")[80] = 50.0
+        e.sync_shadow()
+    after, out_len = model.infer(text, tl, 64, stop_threshold=0.5)
+    assert (out_len.cpu() == 1).all()
+    assert after.shape[1] < 64
+
+
+@pytest.mark.parametrize("m", [1, 5, 32])
+def test_skinny_gemm(m):
+    g = torch.Generator().manual_seed(m)
+    n, k = 200, 520
+    A = torch.randn(m, k, generator=g).bfloat16().cuda()
+    B = torch.randn(n, k, generator=g).bfloat16().cuda()
+    bias = torch.randn(n, generator=g).cuda()
+    C = torch.empty(m, n, dtype=torch.float32, device="cuda")
+    ops.gemm(A, B, C, m, n, k, k, k, n, bias=bias, act=1, variant=3)
+    ref = (A.double() @ B.double().t() + bias.double()).relu()
+    assert rel(C, ref) < 1e-5

@@ -1,0 +1,197 @@
+// decode.hip -- the autoregressive decode step, gfx950.
+//
+// One decode step per utterance of the batch: a single query row per (batch,
+// head) against (i) the layer's self-attention KV cache [B][T_max][K|V] holding
+// positions 0..t, and (ii) the encoder memory's precomputed cross K/V.  The step
+// index t lives in DEVICE memory and every kernel here reads it, so the whole
+// step (prenet -> 6 layers -> heads -> emit) is captured once as a hipGraph and
+// replayed T times with no host round trip.
+//
+// attn_decode: workgroup = one (batch, head), 4 waves split the keys into
+// contiguous quarters; each wave takes 8 keys per iteration (8 lanes x 16-B per
+// 64-wide head row, for K and for V), keeps an online softmax, and the four
+// partial (max, sum, o[64]) are merged through LDS.  HBM-bound on the cache.
+#include <math.h>
+
+#include "tt2_capi.h"
+#include "tt2_internal.h"
+#include "tt2_common.h"
+
+namespace {
+constexpr int NT = 256;
+constexpr int D = 64;
+constexpr float LOG2E = 1.4426950408889634f;
+
+template <typename T> TT2_DEV void load8f(const T* p, float (&v)[8]);
+template <> TT2_DEV void load8f(const bf16* p, float (&v)[8]) {
+  const bf16x8 x = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+}
+template <> TT2_DEV void load8f(const float* p, float (&v)[8]) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+}
+
+struct DecArgs {
+  const void* q; const void* k; const void* v; void* out;
+  int64_t q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld;
+  const int32_t* key_len;   // per-batch number of keys (cross attention) or null
+  const int32_t* t_ptr;     // self attention: keys = *t_ptr + 1
+  int tk, H;
+  float scale;
+};
+
+template <typename T>
+__global__ __launch_bounds__(NT) void attn_decode_kernel(DecArgs a) {
+  __shared__ float sm[4], sl[4], so[4][D];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  int nk = a.tk;
+  if (a.t_ptr) nk = min(nk, *a.t_ptr + 1);
+  if (a.key_len) nk = min(nk, a.key_len[b]);
+  nk = max(nk, 0);
+  const int dc = lane & 7, kg = lane >> 3;   // 8-dim chunk, key slot within an 8-key group
+  float qv[8];
+  load8f(reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld + h * D + dc * 8, qv);
+  const float c = a.scale * LOG2E;
+  const int per = (nk + 3) / 4;
+  const int k0 = w * per, k1 = min(nk, k0 + per);
+  const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)b * a.k_bstride + h * D + dc * 8;
+  const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)b * a.v_bstride + h * D + dc * 8;
+  float m = -INFINITY, l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int kb = k0; kb < k1; kb += 8) {
+    const int key = kb + kg;
+    const bool ok = key < k1;
+    float kv[8], vv[8];
+    if (ok) {
+      load8f(K + (int64_t)key * a.k_ld, kv);
+      load8f(V + (int64_t)key * a.v_ld, vv);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { kv[j] = 0.f; vv[j] = 0.f; }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += qv[j] * kv[j];
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    s = ok ? s * c : -INFINITY;
+    float mx = s;
+    mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);   // m = -inf -> 0
+    const float p = exp2f(s - mn);       // masked -> 0
+    l = l * alpha + p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = o[j] * alpha + p * vv[j];
+    m = mn;
+  }
+  // combine the 8 key slots (same m across the wave)
+#pragma unroll
+  for (int off = 8; off < 64; off <<= 1) {
+    l += __shfl_xor(l, off, 64);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] += __shfl_xor(o[j], off, 64);
+  }
+  if (lane == 0) { sm[w] = m; sl[w] = l; }
+  if (lane < 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) so[w][lane * 8 + j] = o[j];
+  __syncthreads();
+  if (threadIdx.x < D) {
+    const int d = threadIdx.x;
+    float M = -INFINITY;
+    for (int i = 0; i < 4; ++i) M = fmaxf(M, sm[i]);
+    float L = 0.f, O = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      const float f = sm[i] == -INFINITY ? 0.f : exp2f(sm[i] - M);
+      L += sl[i] * f;
+      O += so[i][d] * f;
+    }
+    reinterpret_cast<T*>(a.out)[(int64_t)b * a.o_ld + h * D + d] = from_f32<T>(L > 0.f ? O / L : 0.f);
+  }
+}
+
+// cache[b][*t][0:n] = src[b][0:n]
+template <typename T>
+__global__ void kv_append_kernel(const T* src, int64_t src_ld, T* cache, int64_t c_bstride, int64_t c_ld, int n,
+                                 int B, const int32_t* t_ptr) {
+  const int t = *t_ptr;
+  const int64_t total = (int64_t)B * n;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int b = (int)(i / n), c = (int)(i % n);
+    cache[(int64_t)b * c_bstride + (int64_t)t * c_ld + c] = src[(int64_t)b * src_ld + c];
+  }
+}
+
+// heads [B, hld] f32 -> mel_seq[b][t][:], stop_seq[b][t], prev frame (T); then t += 1, seed += 1
+template <typename T>
+__global__ void decode_emit_kernel(const float* heads, int64_t hld, int B, int NM, int tmax, float* mel_seq,
+                                   float* stop_seq, T* prev, int32_t* t_ptr, uint32_t* seed) {
+  const int t = *t_ptr;
+  for (int i = threadIdx.x; i < B * (NM + 1); i += blockDim.x) {
+    const int b = i / (NM + 1), c = i % (NM + 1);
+    const float v = heads[(int64_t)b * hld + c];
+    if (t < tmax) {
+      if (c < NM) {
+        mel_seq[((int64_t)b * tmax + t) * NM + c] = v;
+        prev[(int64_t)b * NM + c] = from_f32<T>(v);
+      } else {
+        stop_seq[(int64_t)b * tmax + t] = v;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    t_ptr[0] = t + 1;
+    if (seed) seed[0] += 1u;
+  }
+}
+
+}  // namespace
+
+extern "C" int tt2_attn_decode(const tt2_attn_decode_args* p, hipStream_t s) {
+  if (p->head_dim != D) return tt2_set_error(TT2_E_INVALID, "tt2_attn_decode: head_dim must be 64");
+  const int esz = p->dtype == TT2_DT_BF16 ? 2 : 4;
+  const int64_t lds[] = {p->q_ld, p->k_ld, p->v_ld, p->k_bstride, p->v_bstride};
+  for (int64_t ld : lds)
+    if ((ld * esz) % 16) return tt2_set_error(TT2_E_INVALID, "tt2_attn_decode: strides must be 16-B multiples");
+  DecArgs a;
+  a.q = p->q; a.k = p->k; a.v = p->v; a.out = p->out;
+  a.q_ld = p->q_ld; a.k_bstride = p->k_bstride; a.k_ld = p->k_ld; a.v_bstride = p->v_bstride; a.v_ld = p->v_ld;
+  a.o_ld = p->o_ld; a.key_len = p->key_len; a.t_ptr = p->t_ptr; a.tk = p->tk; a.H = p->heads; a.scale = p->scale;
+  dim3 g(p->batch * p->heads);
+  if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(attn_decode_kernel<bf16>, g, dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(attn_decode_kernel<float>, g, dim3(NT), 0, s, a);
+  return tt2_check_launch(hipGetLastError(), "tt2_attn_decode");
+}
+
+extern "C" int tt2_kv_append(const void* src, int64_t src_ld, void* cache, int64_t c_bstride, int64_t c_ld, int n,
+                             int batch, const int32_t* t_ptr, int dtype, hipStream_t s) {
+  const int64_t total = (int64_t)batch * n;
+  const int g = (int)((total + NT - 1) / NT);
+  if (dtype == TT2_DT_BF16)
+    hipLaunchKernelGGL(kv_append_kernel<bf16>, dim3(g), dim3(NT), 0, s, (const bf16*)src, src_ld, (bf16*)cache,
+                       c_bstride, c_ld, n, batch, t_ptr);
+  else
+    hipLaunchKernelGGL(kv_append_kernel<float>, dim3(g), dim3(NT), 0, s, (const float*)src, src_ld, (float*)cache,
+                       c_bstride, c_ld, n, batch, t_ptr);
+  return tt2_check_launch(hipGetLastError(), "tt2_kv_append");
+}
+
+extern "C" int tt2_decode_emit(const float* heads, int64_t heads_ld, int batch, int n_mels, int t_max,
+                               float* mel_seq, float* stop_seq, void* prev, int prev_dtype, int32_t* t_ptr,
+                               uint32_t* seed, hipStream_t s) {
+  if (prev_dtype == TT2_DT_BF16)
+    hipLaunchKernelGGL(decode_emit_kernel<bf16>, dim3(1), dim3(NT), 0, s, heads, heads_ld, batch, n_mels, t_max,
+                       mel_seq, stop_seq, (bf16*)prev, t_ptr, seed);
+  else
+    hipLaunchKernelGGL(decode_emit_kernel<float>, dim3(1), dim3(NT), 0, s, heads, heads_ld, batch, n_mels, t_max,
+                       mel_seq, stop_seq, (float*)prev, t_ptr, seed);
+  return tt2_check_launch(hipGetLastError(), "tt2_decode_emit");
+}

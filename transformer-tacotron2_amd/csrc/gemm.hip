@@ -437,6 +437,57 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
   }
 }
 
+// =====================================================================================
+// skinny-M (decode, M <= 32) bf16: out[M, N] = X[M, K] W[N, K]^T.  The problem is a
+// weight stream: every workgroup owns 16 output columns and streams their W rows
+// straight to registers (no LDS round trip), the 4 waves split K, and one MFMA
+// 16x16x32 per 16 rows x 16 columns x 32 k.  Cross-wave sums go through LDS.
+// =====================================================================================
+constexpr int SK_COLS = 16;
+
+__global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t ldx, const bf16* W, int64_t ldw,
+                                                         EpiParams E, int M, int N, int K) {
+  __shared__ float red[4][32][SK_COLS + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * SK_COLS;
+  const int kq = ((K + 127) / 128) * 32;                 // per-wave K slice, multiple of 32
+  const int kb = wave * kq, ke = min(K, kb + kq);
+  const int r = lane & 15, g = lane >> 4;
+  const int n = n0 + r;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const bool nok = n < N, r0ok = r < M, r1ok = r + 16 < M;
+  const bf16* wrow = W + (int64_t)(nok ? n : 0) * ldw;
+  const bf16* x0 = X + (int64_t)(r0ok ? r : 0) * ldx;
+  const bf16* x1 = X + (int64_t)(r1ok ? r + 16 : 0) * ldx;
+  union U { uint4 u; bf16x8 v; };
+  for (int k = kb; k < ke; k += 32) {
+    const int kk = k + 8 * g;
+    const bool kok = kk < ke;
+    U w, a0, a1;
+    w.u = (nok && kok) ? *reinterpret_cast<const uint4*>(wrow + kk) : make_uint4(0, 0, 0, 0);
+    a0.u = (r0ok && kok) ? *reinterpret_cast<const uint4*>(x0 + kk) : make_uint4(0, 0, 0, 0);
+    a1.u = (r1ok && kok) ? *reinterpret_cast<const uint4*>(x1 + kk) : make_uint4(0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0.v, w.v, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1.v, w.v, acc1, 0, 0, 0);
+  }
+  // acc layout: row 4*(lane>>4) + i, col lane & 15
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    red[wave][4 * g + i][r] = acc0[i];
+    red[wave][16 + 4 * g + i][r] = acc1[i];
+  }
+  __syncthreads();
+  const uint32_t seed = E.drop.thr ? *E.drop.seed : 0u;
+  for (int o = threadIdx.x; o < 32 * SK_COLS; o += NT) {
+    const int row = o / SK_COLS, col = o % SK_COLS;
+    const int m = row, nn = n0 + col;
+    if (m < M && nn < N) {
+      const float v = (red[0][row][col] + red[1][row][col]) + (red[2][row][col] + red[3][row][col]);
+      st_any(E.c, (int64_t)m * E.ldc + nn, E.c_dt, epi_value(E, seed, m, nn, v));
+    }
+  }
+}
+
 template <bool AK, bool BKC>
 hipError_t launch2(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
                    hipStream_t s) {
@@ -501,6 +552,15 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   const int sp = a->splits > 1 ? a->splits : 1;
 
   hipError_t err;
+  // skinny-M weight-streaming path (decode step)
+  const bool skinny = a->dtype_in == TT2_BF16 && a->m <= 32 && !a->trans_a && !a->trans_b && a->k % 8 == 0 &&
+                      a->a_conv_t == 0 && a->splits <= 1 && (a->kernel_variant == 0 || a->kernel_variant == 3);
+  if (skinny) {
+    hipLaunchKernelGGL(gemm_skinny_kernel, dim3((a->n + SK_COLS - 1) / SK_COLS), dim3(NT), 0, stream,
+                       reinterpret_cast<const bf16*>(a->a), a->lda, reinterpret_cast<const bf16*>(a->b), a->ldb, ep,
+                       a->m, a->n, a->k);
+    return tt2_check_launch(hipGetLastError(), "tt2_gemm(skinny)");
+  }
   // v2 (LDS-DMA) path: bf16, every chunk either fully inside or fully outside its row
   const bool v2 = a->dtype_in == TT2_BF16 && a->kernel_variant != 1 &&
                   A.inner_max % 8 == 0 && B.inner_max % 8 == 0;

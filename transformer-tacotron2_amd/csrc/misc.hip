@@ -127,9 +127,10 @@ __global__ void embed_bwd_kernel(const int64_t* ids, const T* dout, float* dtabl
 // out = drop(x + alpha * pe[t]),  t = row % T
 template <typename T>
 __global__ void pe_fwd_kernel(const T* x, const float* alpha, const float* pe, T* out, int M, int C, int Tlen,
-                              int t_off, DropDesc drop) {
+                              int t_off, const int32_t* t_ptr, DropDesc drop) {
   const int64_t total = (int64_t)M * C;
   const float al = *alpha;
+  if (t_ptr) t_off += *t_ptr;
   const uint32_t seed = drop.thr ? *drop.seed : 0u;
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
     const int m = (int)(i / C), c = (int)(i % C);
@@ -433,10 +434,10 @@ extern "C" int tt2_posenc_fwd(const tt2_pe_args* p, hipStream_t s) {
   const int g = grid_for((int64_t)p->m * p->c);
   if (p->dtype == TT2_DT_BF16)
     hipLaunchKernelGGL(pe_fwd_kernel<bf16>, dim3(g), dim3(NT), 0, s, (const bf16*)p->x, p->alpha, p->pe,
-                       (bf16*)p->out, p->m, p->c, p->t, p->t_offset, d);
+                       (bf16*)p->out, p->m, p->c, p->t, p->t_offset, p->t_ptr, d);
   else
     hipLaunchKernelGGL(pe_fwd_kernel<float>, dim3(g), dim3(NT), 0, s, (const float*)p->x, p->alpha, p->pe,
-                       (float*)p->out, p->m, p->c, p->t, p->t_offset, d);
+                       (float*)p->out, p->m, p->c, p->t, p->t_offset, p->t_ptr, d);
   return tt2_check_launch(hipGetLastError(), "tt2_posenc_fwd");
 }
 

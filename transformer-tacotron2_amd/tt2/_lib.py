@@ -158,7 +158,7 @@ class BnArgs(C.Structure):
 class PeArgs(C.Structure):
     _fields_ = [
         ("x", vp), ("dout", vp), ("out", vp), ("dx", vp), ("alpha", vp), ("pe", vp), ("dalpha", vp),
-        ("workspace", vp), ("ws_bytes", sz), ("drop_seed", vp),
+        ("workspace", vp), ("ws_bytes", sz), ("drop_seed", vp), ("t_ptr", vp),
         ("m", i32), ("c", i32), ("t", i32), ("t_offset", i32), ("dtype", i32),
         ("drop_site", u32), ("drop_thr", u32), ("drop_scale", f32),
     ]
@@ -205,4 +205,21 @@ SIGNATURES.update({
     "tt2_adam_workspace_size": ([], sz),
     "tt2_adam_step": ([P_(AdamArgs), vp], C.c_int),
     "tt2_step_bump": ([vp, vp, vp], C.c_int),
+})
+
+
+class AttnDecodeArgs(C.Structure):
+    _fields_ = [
+        ("q", vp), ("k", vp), ("v", vp), ("out", vp),
+        ("q_ld", i64), ("k_bstride", i64), ("k_ld", i64), ("v_bstride", i64), ("v_ld", i64), ("o_ld", i64),
+        ("key_len", vp), ("t_ptr", vp),
+        ("batch", i32), ("heads", i32), ("head_dim", i32), ("tk", i32), ("dtype", i32),
+        ("scale", f32),
+    ]
+
+
+SIGNATURES.update({
+    "tt2_attn_decode": ([C.POINTER(AttnDecodeArgs), vp], C.c_int),
+    "tt2_kv_append": ([vp, i64, vp, i64, i64, C.c_int, C.c_int, vp, C.c_int, vp], C.c_int),
+    "tt2_decode_emit": ([vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp], C.c_int),
 })

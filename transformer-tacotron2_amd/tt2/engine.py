@@ -53,10 +53,12 @@ class Arena:
         Me, Md = B * Tx, B * Ty
         self.Me, self.Md = Me, Md
         self.t = {}
+        self.spec = {}
+        self.dev = dev
         f32 = torch.float32
 
-        def mk(name, shape, dtype=cd):
-            self.t[name] = torch.empty(shape, dtype=dtype, device=dev)
+        def mk(name, shape, dtype=cd, zero=False):
+            self.spec[name] = (shape, dtype, zero)
 
         mk("text", (Me,), torch.int64)
         mk("text_len", (B,), torch.int32)
@@ -107,7 +109,7 @@ class Arena:
                 mk(f"dln{k}m{l}", (Md,), f32)
                 mk(f"dln{k}r{l}", (Md,), f32)
         self.heads_ld = 96
-        self.t["heads"] = torch.zeros(Md, self.heads_ld, dtype=f32, device=dev)
+        mk("heads", (Md, self.heads_ld), f32, zero=True)
         mk("pin", (Md, c.n_mels))
         chans = postnet_channels(c)
         for i in range(c.postnet_layers):
@@ -120,7 +122,7 @@ class Arena:
         mk("loss", (4,), f32)
         # ---- gradient scratch
         mk("g_heads", (Md, self.heads_ld), f32)
-        self.t["gh_cd"] = torch.zeros(Md, self.heads_ld, dtype=cd, device=dev)
+        mk("gh_cd", (Md, self.heads_ld), cd, zero=True)
         mk("g_after", (Md, c.n_mels))
         mk("g_pa", (Md, c.postnet_channels))
         mk("g_pb", (Md, c.postnet_channels))
@@ -137,7 +139,20 @@ class Arena:
         mk("delta", (B * H, max(Tx, Ty)), f32)
 
     def __getitem__(self, k):
-        return self.t[k]
+        t = self.t.get(k)
+        if t is None:
+            # allocated on first use (inference touches a subset); never inside a capture
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError(f"arena buffer {k} first touched during graph capture")
+            shape, dtype, zero = self.spec[k]
+            t = (torch.zeros if zero else torch.empty)(shape, dtype=dtype, device=self.dev)
+            self.t[k] = t
+        return t
+
+    def materialize(self):
+        for k in self.spec:
+            self[k]
+        return self
 
 
 class TTSEngine:
@@ -250,8 +265,18 @@ class TTSEngine:
         A["mel"].copy_(mel, non_blocking=True)
 
     def forward(self, A: Arena):
-        c, cd = self.cfg, self.cd
-        B, Tx, Ty, Me, Md = A.B, A.Tx, A.Ty, A.Me, A.Md
+        """Teacher-forced forward: encoder -> decoder -> heads -> post-net."""
+        self.forward_encoder(A)
+        self.forward_decoder(A)
+        if self.training:
+            for k in self.nbt:
+                self.nbt[k] += 1
+
+    def forward_encoder(self, A: Arena):
+        """Encoder pre-net + layers, then the K/V projection of the memory for
+        all decoder layers (A["mkv"])."""
+        c = self.cfg
+        B, Tx, Me = A.B, A.Tx, A.Me
         d, F, H, K = c.d_model, c.d_ffn, c.n_heads, c.enc_conv_kernel
         pad = (K - 1) // 2
         tr = self.training
@@ -292,6 +317,13 @@ class TTSEngine:
         mem = x
         # one GEMM projects the memory to K/V for all decoder layers
         self._lin(mem, self.W("dec.kv.w"), A["mkv"], Me, c.n_dec * 2 * d, d, bias=self.P("dec.kv.b"))
+
+    def forward_decoder(self, A: Arena):
+        c = self.cfg
+        B, Tx, Ty, Md = A.B, A.Tx, A.Ty, A.Md
+        d, F, H = c.d_model, c.d_ffn, c.n_heads
+        tr = self.training
+        scale = 1.0 / math.sqrt(c.head_dim)
         # ---------------- decoder pre-net
         ops.shift_right(A["mel"], A["din"], B, Ty, c.n_mels)
         self._lin(A["din"], self.W("dec.fc1.w"), A["dp1"], Md, c.dec_prenet, c.n_mels, bias=self.P("dec.fc1.b"),
@@ -335,9 +367,6 @@ class TTSEngine:
         # ---------------- post-net
         ops.cast2d(A["heads"], A.heads_ld, A["pin"], c.n_mels, Md, c.n_mels)
         self._postnet_fwd(A, A["pin"], A["heads"], A.heads_ld, Md, Ty, tr)
-        if tr:
-            for k in self.nbt:
-                self.nbt[k] += 1
 
     def _postnet_fwd(self, A, x_in, res, res_ld, Md, Ty, tr):
         c = self.cfg

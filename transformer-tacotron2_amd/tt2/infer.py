@@ -1,0 +1,181 @@
+"""Autoregressive inference (call stack (C)).
+
+    dec = Decoder(model.engine, batch=32, text_len=128, t_max=800)
+    mel_after, out_len = dec.run(text, text_len, max_len=800)
+
+The encoder runs once (eval mode) and its memory is projected to K/V for all
+six decoder layers by one GEMM.  The per-frame decode step -- pre-net on the
+previous frame, scaled PE, 6 x [self-attention with KV-cache append, cross-
+attention over the cached memory K/V, FFN, post-LN], mel/stop heads, emit --
+reads the step index from a DEVICE counter, so it is captured ONCE as a
+hipGraph (torch.cuda.CUDAGraph records the libtt2 launches) and replayed per
+frame; the host only polls the stop flags every ``check_every`` frames.  The
+post-net runs once over the whole sequence afterwards (as
+modeling_speecht5.py:2261-2263 does).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import ops
+from ._lib import ACT_RELU
+from .config import SITE_INFER_FC1, SITE_INFER_FC2
+from .engine import TTSEngine
+from .ops import NO_DROP, Drop
+
+
+class Decoder:
+    def __init__(self, engine: TTSEngine, batch: int, text_len: int, t_max: int, prenet_dropout: bool = False,
+                 seed: int = 0):
+        self.e = e = engine
+        c = e.cfg
+        self.B, self.Tx, self.Tmax = batch, text_len, t_max
+        if t_max > c.max_len:
+            raise ValueError(f"t_max {t_max} exceeds the positional table ({c.max_len})")
+        self.prenet_dropout = prenet_dropout
+        self.seed0 = seed
+        dev, cd = e.dev, e.cd
+        d, F = c.d_model, c.d_ffn
+        B = batch
+        self.A = e.arena(batch, text_len, t_max)   # encoder + post-net buffers (lazy)
+        z = lambda *s, dt=cd: torch.zeros(s, dtype=dt, device=dev)  # noqa: E731
+        self.prev = z(B, c.n_mels)
+        self.p1, self.p2 = z(B, c.dec_prenet), z(B, c.dec_prenet)
+        self.proj, self.x0 = z(B, d), z(B, d)
+        self.xa, self.xb = z(B, d), z(B, d)
+        self.qkv = z(B, 3 * d)
+        self.att, self.o, self.h1, self.cq, self.catt, self.co, self.h2 = (z(B, d) for _ in range(7))
+        self.f1, self.f2 = z(B, F), z(B, d)
+        self.cache = z(c.n_dec, B, t_max, 2 * d)           # per layer [B][t_max][K | V]
+        self.heads = z(B, 96, dt=torch.float32)
+        self.mel_seq = z(B, t_max, c.n_mels, dt=torch.float32)
+        self.stop_seq = z(B, t_max, dt=torch.float32)
+        self.t = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.seed = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.graph = None
+
+    # ----------------------------------------------------------------- one step
+    def step(self):
+        """Launch one decode step (graph-capturable: no host sync, no allocation)."""
+        e, c = self.e, self.e.cfg
+        A, B = self.A, self.B
+        d, F, H = c.d_model, c.d_ffn, c.n_heads
+        scale = 1.0 / math.sqrt(c.head_dim)
+        pd = c.prenet_dropout if self.prenet_dropout else 0.0
+        d1 = Drop(self.seed, SITE_INFER_FC1, pd) if pd > 0 else NO_DROP
+        d2 = Drop(self.seed, SITE_INFER_FC2, pd) if pd > 0 else NO_DROP
+        lin = e._lin
+        lin(self.prev, e.W("dec.fc1.w"), self.p1, B, c.dec_prenet, c.n_mels, bias=e.P("dec.fc1.b"), act=ACT_RELU,
+            drop=d1)
+        lin(self.p1, e.W("dec.fc2.w"), self.p2, B, c.dec_prenet, c.dec_prenet, bias=e.P("dec.fc2.b"), act=ACT_RELU,
+            drop=d2)
+        lin(self.p2, e.W("dec.proj.w"), self.proj, B, d, c.dec_prenet, bias=e.P("dec.proj.b"))
+        ops.posenc_fwd(self.proj, e.P("dec.alpha"), e.pe, self.x0, B, 1, t_ptr=self.t)
+        x, xn = self.x0, self.xa
+        mkv = A["mkv"]
+        kvld = c.n_dec * 2 * d
+        for l in range(c.n_dec):
+            p = f"dec{l}."
+            lin(x, e.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"))
+            cache = self.cache[l]
+            ops.kv_append(self.qkv[:, d:], 3 * d, cache, self.Tmax * 2 * d, 2 * d, 2 * d, B, self.t)
+            ops.attn_decode(self.qkv, cache, cache[:, :, d:], self.att, 3 * d, self.Tmax * 2 * d, 2 * d,
+                            self.Tmax * 2 * d, 2 * d, d, B, H, self.Tmax, t_ptr=self.t, scale=scale)
+            lin(self.att, e.W(p + "o.w"), self.o, B, d, d, bias=e.P(p + "o.b"))
+            ops.layernorm_fwd(x, self.o, e.P(p + "ln1.g"), e.P(p + "ln1.b"), self.h1, None, None, B, c.ln_eps)
+            lin(self.h1, e.W(p + "cq.w"), self.cq, B, d, d, bias=e.P(p + "cq.b"))
+            ko = 2 * d * l
+            ops.attn_decode(self.cq, mkv[:, ko:], mkv[:, ko + d:], self.catt, d, self.Tx * kvld, kvld,
+                            self.Tx * kvld, kvld, d, B, H, self.Tx, key_len=A["text_len"], scale=scale)
+            lin(self.catt, e.W(p + "co.w"), self.co, B, d, d, bias=e.P(p + "co.b"))
+            ops.layernorm_fwd(self.h1, self.co, e.P(p + "ln2.g"), e.P(p + "ln2.b"), self.h2, None, None, B, c.ln_eps)
+            lin(self.h2, e.W(p + "ffn1.w"), self.f1, B, F, d, bias=e.P(p + "ffn1.b"), act=ACT_RELU)
+            lin(self.f1, e.W(p + "ffn2.w"), self.f2, B, d, F, bias=e.P(p + "ffn2.b"))
+            ops.layernorm_fwd(self.h2, self.f2, e.P(p + "ln3.g"), e.P(p + "ln3.b"), xn, None, None, B, c.ln_eps)
+            x, xn = xn, (self.xb if xn is self.xa else self.xa)
+        lin(x, e.W("heads.w"), self.heads, B, c.n_mels + 1, d, bias=e.P("heads.b"), ldo=96)
+        ops.decode_emit(self.heads, 96, B, c.n_mels, self.Tmax, self.mel_seq, self.stop_seq, self.prev, self.t,
+                        self.seed)
+
+    # ----------------------------------------------------------------- driver
+    def reset(self):
+        self.t.zero_()
+        self.seed.fill_(self.seed0)
+        self.prev.zero_()
+
+    def encode(self, text, text_len):
+        e, A = self.e, self.A
+        was = e.training
+        e.training = False
+        A["text"].copy_(text.reshape(-1))
+        A["text_len"].copy_(text_len.to(torch.int32))
+        e.forward_encoder(A)
+        e.training = was
+
+    def capture(self):
+        """Record one decode step as a hipGraph (run after encode(); the warm-up
+        step it takes first is undone by reset())."""
+        self.reset()
+        self.step()                  # warm-up: sizes everything, touches buffers
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(self.graph, stream=s):
+                self.step()
+        torch.cuda.current_stream().wait_stream(s)
+        self.reset()
+
+    def decode_loop(self, n_steps: int, use_graph: bool = True, stop_threshold: float | None = None,
+                    check_every: int = 32) -> int:
+        """Run up to n_steps frames; with stop_threshold, stop once every
+        utterance has emitted a stop probability >= threshold.  Returns frames run."""
+        logit_thr = None if stop_threshold is None else math.log(stop_threshold / (1.0 - stop_threshold))
+        done = 0
+        while done < n_steps:
+            k = min(check_every, n_steps - done)
+            for _ in range(k):
+                if use_graph:
+                    self.graph.replay()
+                else:
+                    self.step()
+            done += k
+            if logit_thr is not None:
+                hit = (self.stop_seq[:, :done] >= logit_thr).any(dim=1)
+                if bool(hit.all()):
+                    break
+        return done
+
+    def postnet(self, n_frames: int, stop_threshold: float | None):
+        e, c, A = self.e, self.e.cfg, self.A
+        B, T = self.B, n_frames
+        was = e.training
+        e.training = False
+        # the post-net sees exactly the n decoded frames (conv zero padding at n)
+        Md = B * T
+        before = self.mel_seq[:, :T].reshape(Md, c.n_mels).contiguous()
+        ops.cast2d(before, c.n_mels, A["pin"], c.n_mels, Md, c.n_mels)
+        e._postnet_fwd(A, A["pin"], before, c.n_mels, Md, T, False)
+        e.training = was
+        mel_after = A["mel_after"][:Md].view(B, T, c.n_mels).clone()
+        out_len = torch.full((B,), n_frames, dtype=torch.long, device=e.dev)
+        if stop_threshold is not None:
+            logit_thr = math.log(stop_threshold / (1.0 - stop_threshold))
+            hit = self.stop_seq[:, :n_frames] >= logit_thr
+            first = torch.where(hit.any(1), hit.float().argmax(1) + 1, torch.full_like(out_len, n_frames))
+            out_len = first.long()
+        return mel_after, out_len
+
+    def run(self, text, text_len, max_len: int | None = None, stop_threshold: float | None = 0.5,
+            use_graph: bool = True):
+        """Greedy decode; returns (mel_after [B, T, 80] f32, out_len [B])."""
+        max_len = max_len or self.Tmax
+        self.encode(text, text_len)
+        if use_graph and self.graph is None:
+            self.capture()
+        self.reset()
+        n = self.decode_loop(max_len, use_graph, stop_threshold)
+        return self.postnet(n, stop_threshold)

@@ -107,6 +107,23 @@ class TransformerTTS:
             raise RuntimeError("backward() needs forward() + loss() first")
         self.engine.backward(self._last)
 
+    # ------------------------------------------------------------ inference
+    def infer(self, text, text_len, max_len: int, stop_threshold: float | None = 0.5, use_graph: bool = True,
+              prenet_dropout: bool = False):
+        """Greedy AR synthesis (hipGraph-replayed decode step, KV cache, cached
+        cross K/V).  Returns (mel_after [B, T, 80] f32, out_len [B]).
+        stop_threshold=None forces max_len frames."""
+        from .infer import Decoder
+        B, Tx = text.shape
+        key = (B, Tx, max_len, prenet_dropout)
+        dec = self._decoders.get(key) if hasattr(self, "_decoders") else None
+        if dec is None:
+            self._decoders = getattr(self, "_decoders", {})
+            dec = Decoder(self.engine, B, Tx, max_len, prenet_dropout=prenet_dropout)
+            self._decoders[key] = dec
+        dev = self.engine.dev
+        return dec.run(text.to(dev), text_len.to(dev), max_len, stop_threshold, use_graph)
+
     # ------------------------------------------------------------ training
     def configure_optimizer(self, **kw):
         self.engine.init_optimizer(**kw)

@@ -243,9 +243,10 @@ def embedding_bwd(ids, dout, dtable, m, vocab, pad_idx=0):
                                   pad_idx, dt(dout), stream_ptr()), "tt2_embedding_bwd")
 
 
-def posenc_fwd(x, alpha, pe, out, m, t, drop: Drop = NO_DROP, t_offset=0):
+def posenc_fwd(x, alpha, pe, out, m, t, drop: Drop = NO_DROP, t_offset=0, t_ptr=None):
     a = _lib.PeArgs()
     a.x, a.out, a.alpha, a.pe = x.data_ptr(), out.data_ptr(), alpha.data_ptr(), pe.data_ptr()
+    a.t_ptr = ptr(t_ptr)
     a.m, a.c, a.t, a.t_offset, a.dtype = m, x.shape[-1], t, t_offset, dt(x)
     _drop_into(a, drop)
     check(lib().tt2_posenc_fwd(C.byref(a), stream_ptr()), "tt2_posenc_fwd")
@@ -306,3 +307,25 @@ def adam_step(params, grads, m, v, shadow, step, n, lr, beta1=0.9, beta2=0.98, e
 
 def step_bump(step, seed=None):
     check(lib().tt2_step_bump(step.data_ptr(), ptr(seed), stream_ptr()), "tt2_step_bump")
+
+
+def attn_decode(q, k, v, out, q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld, batch, heads, tk, key_len=None,
+                t_ptr=None, scale=0.125):
+    """One query row per batch element over a key cache (see tt2_attn_decode_args)."""
+    a = _lib.AttnDecodeArgs()
+    a.q, a.k, a.v, a.out = q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
+    a.q_ld, a.k_bstride, a.k_ld, a.v_bstride, a.v_ld, a.o_ld = q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld
+    a.key_len, a.t_ptr = ptr(key_len), ptr(t_ptr)
+    a.batch, a.heads, a.head_dim, a.tk, a.dtype, a.scale = batch, heads, 64, tk, dt(q), scale
+    check(lib().tt2_attn_decode(C.byref(a), stream_ptr()), "tt2_attn_decode")
+
+
+def kv_append(src, src_ld, cache, c_bstride, c_ld, n, batch, t_ptr):
+    check(lib().tt2_kv_append(src.data_ptr(), src_ld, cache.data_ptr(), c_bstride, c_ld, n, batch, t_ptr.data_ptr(),
+                              dt(src), stream_ptr()), "tt2_kv_append")
+
+
+def decode_emit(heads, heads_ld, batch, n_mels, t_max, mel_seq, stop_seq, prev, t_ptr, seed=None):
+    check(lib().tt2_decode_emit(heads.data_ptr(), heads_ld, batch, n_mels, t_max, mel_seq.data_ptr(),
+                                stop_seq.data_ptr(), prev.data_ptr(), dt(prev), t_ptr.data_ptr(), ptr(seed),
+                                stream_ptr()), "tt2_decode_emit")
