@@ -126,25 +126,34 @@ def decode_bench(model, reps: int = 3):
 def roofline(model, text, tl, mel, ml):
     """Live per-launch timing of the dominant kernel family in one eager step."""
     from tt2 import ops
-    ops.PROBE = ops.LaunchProbe()
+    ops.PROBE = probe = ops.LaunchProbe()
     try:
         model.train_step(text, tl, mel, ml)
-        summ = ops.PROBE.summary()
+        summ = probe.summary()
     finally:
         ops.PROBE = None
     # dominant = the GEMM variant with the most device time
-    key, (n, flops, secs) = max(summ.items(), key=lambda kv: kv[1][2])
+    key, (n, flops, secs, abytes) = max(summ.items(), key=lambda kv: kv[1][2])
+    secs = probe.replay_time(key)      # same launches, back-to-back timing
     tot_t = sum(v[2] for v in summ.values())
     tot_f = sum(v[1] for v in summ.values())
     achieved = flops / secs / 1e12
-    names = {(1, 0, 0): "gemm_kernel<bf16,Kcontig,Kcontig> (forward linear/conv)",
-             (1, 0, 1): "gemm_kernel<bf16,Kcontig,Ncontig> (dgrad)",
-             (1, 1, 1): "gemm_kernel<bf16,Mcontig,Ncontig> (wgrad)"}
+    names = {(1, 0, 0): "gemm2_kernel<true, true> (bf16 forward linear/conv: A, B K-contiguous)",
+             (1, 0, 1): "gemm2_kernel<true, false> (bf16 dgrad)",
+             (1, 1, 1): "gemm2_kernel<false, false> (bf16 wgrad)"}
+    traffic, tsrc = None, None
+    prof = os.path.join(ROOT, "profiles")
+    tfiles = sorted(f for f in os.listdir(prof) if f.endswith("_traffic.json")) if os.path.isdir(prof) else []
+    if tfiles:
+        t = json.load(open(os.path.join(prof, tfiles[-1])))
+        if t.get("kernel", "") in names.get(key[1:4], ""):
+            traffic, tsrc = round(t["hbm_bytes_per_launch"]), "profiles/" + tfiles[-1]
     return {
         "kernel": names.get(key[1:4], str(key)) + (" +split-K reduce" if key[4] else ""),
         "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-        "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-        "launches_per_step": n, "flops_per_launch": flops / n, "avg_launch_us": round(secs / n * 1e6, 2),
+        "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_source": tsrc,
+        "algo_bytes_per_launch": round(abytes / n), "launches_per_step": n, "flops_per_launch": flops / n,
+        "avg_launch_us": round(secs / n * 1e6, 2),
         "all_gemms": {"launches": sum(v[0] for v in summ.values()), "ms_per_step": round(tot_t * 1e3, 3),
                       "tflops": round(tot_f / tot_t / 1e12, 1)},
     }

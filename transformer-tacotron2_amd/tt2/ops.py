@@ -90,9 +90,11 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=Non
         g.workspace, g.ws_bytes = buf.data_ptr(), buf.numel()
     if PROBE is not None:
         key = ("gemm", g.dtype_in, int(trans_a), int(trans_b), g.splits > 1)
+        esz = 2 if g.dtype_in == _lib.DT_BF16 else 4
+        algo_bytes = esz * (m * k + n * k) + (2 if g.dtype_out == _lib.DT_BF16 else 4) * m * n
         PROBE.begin()
         check(L.tt2_gemm(C.byref(g), stream_ptr()), "tt2_gemm")
-        PROBE.end(key, 2.0 * m * n * k)
+        PROBE.end(key, 2.0 * m * n * k, algo_bytes, g)
         return c
     check(L.tt2_gemm(C.byref(g), stream_ptr()), "tt2_gemm")
     return c
@@ -110,20 +112,44 @@ class LaunchProbe:
         self._s = torch.cuda.Event(enable_timing=True)
         self._s.record()
 
-    def end(self, key, flops):
+    def end(self, key, flops, algo_bytes=0, args=None):
         e = torch.cuda.Event(enable_timing=True)
         e.record()
-        self.rec.append((key, flops, self._s, e))
+        saved = None
+        if args is not None:
+            saved = GemmArgs()
+            C.pointer(saved)[0] = args
+        self.rec.append((key, flops, self._s, e, algo_bytes, saved))
 
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for key, flops, s, e in self.rec:
-            d = out.setdefault(key, [0, 0.0, 0.0])
+        for key, flops, s, e, ab, _ in self.rec:
+            d = out.setdefault(key, [0, 0.0, 0.0, 0.0])
             d[0] += 1
             d[1] += flops
             d[2] += s.elapsed_time(e) * 1e-3
+            d[3] += ab
         return out
+
+    def replay_time(self, key, reps: int = 10) -> float:
+        """Total device time of this variant's recorded launches, each re-launched
+        `reps` times back-to-back between one event pair (amortises the
+        per-launch dispatch gap that single-launch brackets include)."""
+        L = lib()
+        total = 0.0
+        for k, _, _, _, _, saved in self.rec:
+            if k != key or saved is None:
+                continue
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                check(L.tt2_gemm(C.byref(saved), stream_ptr()), "tt2_gemm(replay)")
+            e.record()
+            torch.cuda.synchronize()
+            total += s.elapsed_time(e) * 1e-3 / reps
+        return total
 
 
 PROBE: LaunchProbe | None = None
