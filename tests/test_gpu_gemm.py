@@ -21,7 +21,8 @@ def _mk(shape, dtype, gen):
     return torch.randn(shape, generator=gen, dtype=torch.float32).to(dtype).cuda()
 
 
-VARIANTS = [(torch.float32, 1), (torch.bfloat16, 1), (torch.bfloat16, 2)]
+VARIANTS = [(torch.float32, 1), (torch.bfloat16, 1), (torch.bfloat16, 2), (torch.bfloat16, 4), (torch.bfloat16, 5),
+            (torch.bfloat16, 6), (torch.bfloat16, 7)]
 
 
 @pytest.mark.parametrize("dtype,variant", VARIANTS)

@@ -37,6 +37,7 @@ struct EpiParams {
   int act;
   DropDesc drop;
   int n_log;  // logical N for dropout index (m * n_log + n)
+  int vec;    // every row of C/res/gate/bias is 16-B aligned at 8-column boundaries
 };
 
 TT2_DEV float ld_any(const void* p, int64_t i, int dt) {
@@ -325,25 +326,75 @@ TT2_DEV void frag2(Frag8<bf16>& f, const char* tile, int r0, int kk, int lane) {
   }
 }
 
-TT2_DEV void epi_store8(const EpiParams& E, uint32_t seed, int m, int n0, int N, const float (&v)[8]) {
-  const bool full = n0 + 8 <= N;
-  float o[8];
+// 8 consecutive elements of a row from a bf16 or f32 tensor (16-B aligned)
+TT2_DEV void ld8_any(const void* p, int64_t off, int dt, float (&o)[8]) {
+  if (dt == TT2_BF16) {
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(p) + off);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (full || n0 + j < N) ? epi_value(E, seed, m, n0 + j, v[j]) : 0.f;
-  const int64_t off = (int64_t)m * E.ldc + n0;
-  if (full && E.c_dt == TT2_BF16 && (off % 8) == 0) {
-    bf16x8 x;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = (bf16)o[j];
-    *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(E.c) + off) = x;
-  } else if (full && E.c_dt == TT2_F32 && (off % 4) == 0) {
-    float* c = reinterpret_cast<float*>(E.c) + off;
-    *reinterpret_cast<f32x4*>(c) = f32x4{o[0], o[1], o[2], o[3]};
-    *reinterpret_cast<f32x4*>(c + 4) = f32x4{o[4], o[5], o[6], o[7]};
+    for (int j = 0; j < 8; ++j) o[j] = (float)x[j];
   } else {
-    for (int j = 0; j < 8; ++j)
-      if (n0 + j < N) st_any(E.c, off + j, E.c_dt, o[j]);
+    const float* q = reinterpret_cast<const float*>(p) + off;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(q), b = *reinterpret_cast<const f32x4*>(q + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o[j] = a[j]; o[4 + j] = b[j]; }
   }
+}
+
+// Chunk epilogue: 8 consecutive outputs of row m starting at column n0.  Full,
+// aligned chunks (E.vec) take 16-B loads/stores with every option tested once
+// per chunk; edge chunks fall back to the per-element path.
+TT2_DEV void epi_store8(const EpiParams& E, uint32_t seed, int m, int n0, int N, const float (&v)[8]) {
+  const int64_t off = (int64_t)m * E.ldc + n0;
+  if (E.vec && n0 + 8 <= N) {
+    float o[8], t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = v[j] * E.alpha;
+    if (E.bias) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(E.bias + n0), b = *reinterpret_cast<const f32x4*>(E.bias + n0 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { o[j] += a[j]; o[4 + j] += b[j]; }
+    }
+    if (E.res) {
+      ld8_any(E.res, (int64_t)m * E.ldr + n0, E.res_dt, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += t[j];
+    }
+    if (E.act == ACT_RELU) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
+    } else if (E.act == ACT_TANH) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = tanhf(o[j]);
+    }
+    if (E.gate) {
+      ld8_any(E.gate, (int64_t)m * E.ldg + n0, E.gate_dt, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = t[j] != 0.f ? o[j] * E.gate_scale : 0.f;
+    }
+    if (E.drop.thr) {
+      const uint32_t base = (uint32_t)((int64_t)m * E.n_log + n0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = drop_apply(E.drop, seed, base + j, o[j]);
+    }
+    if (E.beta != 0.f) {
+      ld8_any(E.c, off, E.c_dt, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += E.beta * t[j];
+    }
+    if (E.c_dt == TT2_BF16) {
+      bf16x8 x;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = (bf16)o[j];
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(E.c) + off) = x;
+    } else {
+      float* c = reinterpret_cast<float*>(E.c) + off;
+      *reinterpret_cast<f32x4*>(c) = f32x4{o[0], o[1], o[2], o[3]};
+      *reinterpret_cast<f32x4*>(c + 4) = f32x4{o[4], o[5], o[6], o[7]};
+    }
+    return;
+  }
+  for (int j = 0; j < 8; ++j)
+    if (n0 + j < N) st_any(E.c, off + j, E.c_dt, epi_value(E, seed, m, n0 + j, v[j]));
 }
 
 template <bool AK, bool BKC>
@@ -379,11 +430,13 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
   for (int kt = 0; kt < nkt; ++kt) {
     const char* sa = smem + (kt & 1) * STAGE_BYTES;
     const char* sb = sa + TILE_BYTES;
+#ifndef TT2_ABL_NO_LOAD
     if (kt + 1 < nkt) {
       char* na = smem + ((kt + 1) & 1) * STAGE_BYTES;
       issue_tile<AK>(A, na, m0, kb + (kt + 1) * BK2, lane, wave);
       issue_tile<BKC>(B, na + TILE_BYTES, n0, kb + (kt + 1) * BK2, lane, wave);
     }
+#endif
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       Frag8<bf16> fa[4], fb[4];
@@ -391,14 +444,23 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
       for (int i = 0; i < 4; ++i) frag2<AK>(fa[i], sa, wm * 64 + 16 * i, kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) frag2<BKC>(fb[j], sb, wn * 64 + 16 * j, kk, lane);
+#ifdef TT2_ABL_NO_MFMA
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { asm volatile("" :: "v"(fa[i].v)); asm volatile("" :: "v"(fb[i].v)); }
+#else
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) mma16(fa[i], fb[j], acc[i][j]);
+#endif
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+#ifdef TT2_ABL_NO_EPI
+  if (acc[0][0][0] == 1234.5f && acc[3][3][3] == 1234.5f) reinterpret_cast<float*>(E.c)[tid] = acc[1][1][1];
+  return;
+#endif
 
   // stage C (f32) through LDS: row-major [128][EPI_LD]
   float* cs = reinterpret_cast<float*>(smem);
@@ -422,6 +484,9 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
     const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * EPI_LD + c8 + 4);
     v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
     v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+#ifdef TT2_ABL_NO_STORE
+    if (v[0] != 1234.5f) continue;
+#endif
     if (ws) {
       float* w = ws + ((int64_t)blockIdx.y * M + m) * N + n;
       if (n + 8 <= N && (N % 4) == 0) {
@@ -435,6 +500,243 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
       epi_store8(E, seed, m, n, N, v);
     }
   }
+}
+
+// =====================================================================================
+// v3 (bf16): the v2 operand images and swizzles, but a STAGES-deep LDS ring with the
+// next STAGES-1 K tiles in flight across the barrier (counted `s_waitcnt vmcnt` +
+// raw s_barrier, never a full drain inside the loop), BM = 128 or 256 rows
+// (256 = 8 waves, K-contiguous A only), and branch-light per-lane addressing: each
+// lane keeps its chunk pointers / conv tap-time state and advances them by one K
+// tile per iteration instead of recomputing divisions.
+// =====================================================================================
+struct LaneChunk {
+  const bf16* p;   // address of this lane's chunk for the current K tile (unmasked)
+  int outer, inner;
+  int t, tap;      // conv bookkeeping (time of outer, tap of inner)
+};
+
+template <bool KC>
+TT2_DEV void lane_chunk_init(LaneChunk& c, const OpDesc& d, int inst, int lane, int r0, int k0) {
+  if (KC) {
+    const int row = inst * 8 + (lane >> 3);
+    const int gc = (lane & 7) ^ (row & 7);
+    c.outer = r0 + row;
+    c.inner = k0 + gc * 8;
+  } else {
+    const int kr = inst * 4 + (lane >> 4);
+    const int gc = (lane & 15) ^ mc_swz(kr);
+    c.outer = k0 + kr;
+    c.inner = r0 + gc * 8;
+  }
+  c.p = reinterpret_cast<const bf16*>(d.p) + (int64_t)c.outer * d.ld + c.inner;
+  if (d.conv_t > 0) {
+    c.p -= (int64_t)d.conv_pad * d.conv_c;
+    c.t = c.outer % d.conv_t;
+    c.tap = c.inner / d.conv_c;
+  } else {
+    c.t = 0;
+    c.tap = 0;
+  }
+}
+
+template <bool KC>
+TT2_DEV void lane_chunk_advance(LaneChunk& c, const OpDesc& d) {
+  if (KC) {
+    c.inner += BK2;
+    c.p += BK2;
+    if (d.conv_t > 0) {   // inner = tap * C + ci: ci grows by 64 < C (C >= 80 when conv)
+      int ci = c.inner - c.tap * d.conv_c;
+      while (ci >= d.conv_c) { ci -= d.conv_c; ++c.tap; }
+    }
+  } else {
+    c.outer += BK2;
+    c.p += (int64_t)BK2 * d.ld;
+    if (d.conv_t > 0) {
+      c.t += BK2;
+      while (c.t >= d.conv_t) c.t -= d.conv_t;
+    }
+  }
+}
+
+TT2_DEV const void* lane_chunk_src(const LaneChunk& c, const OpDesc& d) {
+  bool ok = c.outer < d.outer_max && c.inner < d.inner_max;
+  if (d.conv_t > 0) {
+    const int ts = c.t + c.tap - d.conv_pad;
+    ok = ok && ts >= 0 && ts < d.conv_t;
+  }
+  return ok ? (const void*)c.p : (const void*)g_zero_page;
+}
+
+template <int N> TT2_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int BM_, int STAGES> struct G3 {
+  static constexpr int WAVES = BM_ / 32;                 // 2 (n) x BM/64 (m)
+  static constexpr int THREADS = WAVES * 64;
+  static constexpr int A_BYTES = BM_ * BK2 * 2;
+  static constexpr int B_BYTES = 128 * BK2 * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_INST = A_BYTES / 1024 / WAVES;  // LDS-DMA instructions per wave per tile
+  static constexpr int B_INST = B_BYTES / 1024 / WAVES;
+  static constexpr int INST = A_INST + B_INST;
+  static constexpr int EPI = BM_ * EPI_LD * 4;
+  static constexpr int SMEM = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
+};
+
+template <bool AK, bool BKC, int BM_, int STAGES>
+__global__ __launch_bounds__((BM_ / 32) * 64) void gemm3_kernel(OpDesc A, OpDesc B, EpiParams E, int M,
+                                                                         int N, int K, int k_split, float* ws,
+                                                                         int ntm, int ntn) {
+  using G = G3<BM_, STAGES>;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nt = ntm * ntn;
+  const int bid = blockIdx.x;
+  const int q = nt / 8, rr = nt % 8, x = bid % 8;
+  const int tile = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + bid / 8;
+  const int m0 = (tile / ntn) * BM_, n0 = (tile % ntn) * BN;
+  const int kb = blockIdx.y * k_split;
+  const int ke = min(K, kb + k_split);
+  if (AK) A.inner_max = ke; else A.outer_max = ke;
+  if (BKC) B.inner_max = ke; else B.outer_max = ke;
+  const int nkt = (ke - kb + BK2 - 1) / BK2;
+
+  LaneChunk ca[G::A_INST], cb[G::B_INST];
+#pragma unroll
+  for (int i = 0; i < G::A_INST; ++i) lane_chunk_init<AK>(ca[i], A, wave * G::A_INST + i, lane, m0, kb);
+#pragma unroll
+  for (int i = 0; i < G::B_INST; ++i) lane_chunk_init<BKC>(cb[i], B, wave * G::B_INST + i, lane, n0, kb);
+
+  auto issue = [&](int stage) {
+    char* sa = smem + stage * G::STAGE;
+    char* sb = sa + G::A_BYTES;
+#pragma unroll
+    for (int i = 0; i < G::A_INST; ++i) {
+      __builtin_amdgcn_global_load_lds((gvoid_t*)lane_chunk_src(ca[i], A),
+                                       (lvoid_t*)(sa + (wave * G::A_INST + i) * 1024), 16, 0, 0);
+      lane_chunk_advance<AK>(ca[i], A);
+    }
+#pragma unroll
+    for (int i = 0; i < G::B_INST; ++i) {
+      __builtin_amdgcn_global_load_lds((gvoid_t*)lane_chunk_src(cb[i], B),
+                                       (lvoid_t*)(sb + (wave * G::B_INST + i) * 1024), 16, 0, 0);
+      lane_chunk_advance<BKC>(cb[i], B);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: tiles 0 .. STAGES-2 in flight
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nkt) issue(s);
+  if (nkt > STAGES - 2) wait_vmcnt<(STAGES - 2) * G::INST>();
+  else wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0; kt < nkt; ++kt) {
+    const bool more = kt + STAGES - 1 < nkt;
+    if (more) issue((kt + STAGES - 1) % STAGES);
+    const char* sa = smem + (kt % STAGES) * G::STAGE;
+    const char* sb = sa + G::A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      Frag8<bf16> fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) frag2<AK>(fa[i], sa, wm * 64 + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) frag2<BKC>(fb[j], sb, wn * 64 + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mma16(fa[i], fb[j], acc[i][j]);
+    }
+    // tile kt+1 must have landed (this wave's part), and every wave must be done
+    // reading tile kt before the NEXT iteration's issue overwrites its slot.
+    if (more) wait_vmcnt<(STAGES - 2) * G::INST>();
+    else wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  float* cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cs[(wm * 64 + 16 * i + 4 * (lane >> 4) + r) * EPI_LD + wn * 64 + 16 * j + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
+  constexpr int ITERS = BM_ * 16 / G::THREADS;
+#pragma unroll 2
+  for (int it = 0; it < ITERS; ++it) {
+    const int id = tid + G::THREADS * it;
+    const int row = id >> 4, c8 = (id & 15) * 8;
+    const int m = m0 + row, n = n0 + c8;
+    if (m >= M || n >= N) continue;
+    float v[8];
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + row * EPI_LD + c8);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * EPI_LD + c8 + 4);
+    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+    v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+    if (ws) {
+      float* w = ws + ((int64_t)blockIdx.y * M + m) * N + n;
+      if (n + 8 <= N && (N % 4) == 0) {
+        *reinterpret_cast<f32x4*>(w) = lo;
+        *reinterpret_cast<f32x4*>(w + 4) = hi;
+      } else {
+        for (int j = 0; j < 8; ++j)
+          if (n + j < N) w[j] = v[j];
+      }
+    } else {
+      epi_store8(E, seed, m, n, N, v);
+    }
+  }
+}
+
+template <bool AK, bool BKC, int BM_, int STAGES>
+hipError_t launch3(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
+                   hipStream_t s) {
+  using G = G3<BM_, STAGES>;
+  int k_split = K;
+  if (splits > 1) {
+    k_split = ((K + splits - 1) / splits + BK2 - 1) / BK2 * BK2;
+    splits = (K + k_split - 1) / k_split;
+  }
+  const int ntm = (M + BM_ - 1) / BM_, ntn = (N + BN - 1) / BN;
+  static bool attr_set = false;   // one-time opt-in to > 64 KB dynamic LDS
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKC, BM_, STAGES>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
+    attr_set = true;
+  }
+  dim3 grid(ntm * ntn, splits);
+  hipLaunchKernelGGL((gemm3_kernel<AK, BKC, BM_, STAGES>), grid, dim3(G::THREADS), G::SMEM, s, A, B, E, M, N, K,
+                     k_split, splits > 1 ? ws : nullptr, ntm, ntn);
+  if (splits > 1) {
+    const int64_t total = (int64_t)M * N;
+    int64_t nb = (total + 255) / 256;
+    int blocks = (int)(nb < 4096 ? nb : 4096);
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, splits, E, M, N);
+  }
+  return hipGetLastError();
 }
 
 // =====================================================================================
@@ -548,6 +850,16 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   ep.drop = DropDesc{a->drop_seed, a->drop_site, a->drop_thr, a->drop_scale};
   if (ep.drop.thr && !ep.drop.seed) return tt2_set_error(TT2_E_INVALID, "tt2_gemm: dropout without seed");
   ep.n_log = a->n;
+  {
+    // vectorised epilogue: rows of C / res / gate start 16-B aligned at every 8th column
+    auto ok = [](const void* p, int64_t ld, int dt) {
+      if (!p) return true;
+      const int esz = dt == TT2_BF16 ? 2 : 4;
+      return reinterpret_cast<uintptr_t>(p) % 16 == 0 && (ld * esz) % 16 == 0 && (8 * esz) % 16 == 0;
+    };
+    ep.vec = ok(a->c, a->ldc, a->dtype_out) && ok(a->res, a->ldr, a->res_dtype) &&
+             ok(a->gate, a->ldg, a->gate_dtype) && (reinterpret_cast<uintptr_t>(a->bias) % 16 == 0);
+  }
   float* ws = reinterpret_cast<float*>(a->workspace);
   const int sp = a->splits > 1 ? a->splits : 1;
 
@@ -564,6 +876,21 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   // v2 (LDS-DMA) path: bf16, every chunk either fully inside or fully outside its row
   const bool v2 = a->dtype_in == TT2_BF16 && a->kernel_variant != 1 &&
                   A.inner_max % 8 == 0 && B.inner_max % 8 == 0;
+  const int var = a->kernel_variant;
+  if (v2 && var >= 4) {
+    // v3 configurations: 4 = BM128/2 stages, 5 = BM128/3, 6 = BM256/3 (K-contiguous A), 7 = BM128/4
+#define TT2_G3(AK_, BK_)                                                                              \
+    if (var == 6 && AK_) err = launch3<AK_, BK_, 256, 3>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
+    else if (var == 5 || var == 6) err = launch3<AK_, BK_, 128, 3>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
+    else if (var == 7) err = launch3<AK_, BK_, 128, 4>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
+    else err = launch3<AK_, BK_, 128, 2>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    if (!a->trans_a && !a->trans_b) { TT2_G3(true, true) }
+    else if (!a->trans_a && a->trans_b) { TT2_G3(true, false) }
+    else if (a->trans_a && !a->trans_b) { TT2_G3(false, true) }
+    else { TT2_G3(false, false) }
+#undef TT2_G3
+    return tt2_check_launch(err, "tt2_gemm(v3)");
+  }
   if (v2) {
     if (!a->trans_a && !a->trans_b) err = launch2<true, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
     else if (!a->trans_a && a->trans_b) err = launch2<true, false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
