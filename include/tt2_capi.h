@@ -92,6 +92,8 @@ typedef struct tt2_attn_args {
   const int32_t* key_len;
   int32_t batch, heads, head_dim, tq, tk, causal, dtype;
   float scale;
+  int32_t variant;   /* 0 auto (bf16: v3 32x32 swapped MFMA products; f32: v1), 1 v1 (P through LDS),
+                        2 v3 with 2-wave workgroups, 3 v3 with 4-wave workgroups (bf16 only) */
 } tt2_attn_args;
 
 int tt2_attn_fwd(const tt2_attn_args* a, hipStream_t stream);

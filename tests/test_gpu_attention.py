@@ -40,12 +40,22 @@ CASES = [
     (3, 2, 100, 37, False, False, [37, 20, 0]),
     (1, 8, 64, 128, False, False, None),
     (2, 2, 200, 200, True, True, None),
+    (2, 2, 300, 300, True, True, [300, 257]),
+    (2, 1, 131, 333, False, False, [333, 129]),
 ]
+
+
+@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "v1", "v3w2", "v3w4"])
+def attn_variant(request):
+    old = ops.ATTN_VARIANT
+    ops.ATTN_VARIANT = request.param
+    yield request.param
+    ops.ATTN_VARIANT = old
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", CASES)
-def test_attention_fwd_bwd(dtype, case):
+def test_attention_fwd_bwd(dtype, case, attn_variant):
     B, H, Tq, Tk, causal, packed, kl = case
     D = 64
     scale = 1.0 / math.sqrt(D)

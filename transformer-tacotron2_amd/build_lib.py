@@ -20,6 +20,9 @@ OUT = os.path.join(PKG, "tt2", "libtt2.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-I" + CSRC,
          "-Wno-unused-result"]
+# Per-file extras.  Attention keeps MFMA accumulators in arch VGPRs: its softmax reads
+# and rescales them every tile, and the default AGPR placement adds a copy per use.
+EXTRA = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
 def _headers_mtime() -> float:
@@ -29,7 +32,7 @@ def _headers_mtime() -> float:
 
 
 def _compile(src: str, obj: str) -> tuple[str, int, str]:
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + EXTRA.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     return src, r.returncode, r.stdout + r.stderr
 

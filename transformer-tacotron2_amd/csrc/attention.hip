@@ -451,6 +451,424 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkdv_kernel(AttnArgs a) {
   }
 }
 
+// =====================================================================================
+// v3 kernels (bf16): v_mfma_f32_32x32x16_bf16 with "swapped" products.  Every product
+// puts the streamed dimension (keys in dQ / forward, queries in dK-dV) on the MFMA rows
+// and the wave's own 32 rows (queries, or keys) on the lane:
+//   forward  S^T = K Q^T      O^T  += V^T  P^T
+//   dQ       S^T = K Q^T, dP^T = V dO^T,   dQ^T += K^T dS^T
+//   dK, dV   S   = Q K^T, dP  = dO V^T,    dV^T += dO^T P,  dK^T += Q^T dS
+// The 32x32 accumulator then holds, per lane, 16 streamed rows crow(r, hi) =
+// (r&3) + 8(r>>2) + 4hi of ONE own row, and those 16 values ARE the B operand of the
+// next product once its A operand is read transposed (ds_read_b64_tr_b16) from rows
+// base + {4hi + 0..3} and base + {8 + 4hi + 0..3}.  P and dS never leave registers,
+// softmax statistics are per lane (one xor-32 shuffle per tile), and each LDS fragment
+// feeds a 32-row MFMA (32 FLOP per LDS byte: the LDS array is not the bound).
+// Tiles are 64 rows x 64 bf16 in LDS with the chunk swizzle below, double-buffered and
+// register-staged (global loads for tile t+1 in flight while tile t computes).
+// =====================================================================================
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+TT2_DEV void mma32(const bf16x8& a, const bf16x8& b, f32x16& c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+TT2_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// 16-B chunk c of tile row r lives at slot c ^ swz(r), swz(r) = h((r >> 1) & 7) with
+// h(x) = ((x & 1) << 2) | (x >> 1).  Row reads (ds_read_b128: 16 distinct rows mod 16
+// per lane group) and 4-row transposed reads (ds_read_b64_tr_b16: rows 4i..4i+3 x one
+// 4-chunk half per 32-lane group) are both bank-conflict-free.
+TT2_DEV int swz(int r) {
+  const int x = (r >> 1) & 7;
+  return ((x & 1) << 2) | (x >> 1);
+}
+TT2_DEV int toff(int r, int col) { return r * D + ((((col >> 3) ^ swz(r))) << 3) + (col & 7); }
+
+template <int NTH> struct Stage3 { static constexpr int PER = 64 * 8 / NTH; };
+
+// Buffer view of one (batch, head) slice of a [T rows][ld] bf16 matrix: rows >= T fall
+// outside num_records and load as zeros (no per-row branches or exec masking).
+struct RowBuf {
+  __amdgpu_buffer_rsrc_t rs;
+  int ldb;   // row stride in bytes
+};
+TT2_DEV RowBuf row_buf(const bf16* base, int64_t ld, int T) {
+  RowBuf r;
+  r.ldb = (int)(ld * 2);
+  const int bytes = T > 0 ? (T - 1) * r.ldb + D * 2 : 0;
+  r.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(base), (short)0, bytes, 0x00020000);
+  return r;
+}
+TT2_DEV uint4 buf_ld16(const RowBuf& b, int row, int chunk) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(b.rs, row * b.ldb + chunk * 16, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+template <int NTH>
+TT2_DEV void g2r3(uint4 (&r)[Stage3<NTH>::PER], const RowBuf& g, int row0, int tid) {
+#pragma unroll
+  for (int i = 0; i < Stage3<NTH>::PER; ++i) {
+    const int c = tid + NTH * i;
+    r[i] = buf_ld16(g, row0 + (c >> 3), c & 7);
+  }
+}
+template <int NTH>
+TT2_DEV void r2s3(const uint4 (&r)[Stage3<NTH>::PER], bf16* s, int tid) {
+#pragma unroll
+  for (int i = 0; i < Stage3<NTH>::PER; ++i) {
+    const int c = tid + NTH * i, rr = c >> 3, cc = c & 7;
+    *reinterpret_cast<uint4*>(s + rr * D + ((cc ^ swz(rr)) << 3)) = r[i];
+  }
+}
+// A operand rows: X[row][16 st + 8 hi + j]
+TT2_DEV bf16x8 rowfrag(const bf16* t, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(t + row * D + ((chunk ^ swz(row)) << 3));
+}
+// A operand X^T[d = 32 db + (lane & 31)][k = 8 hi + j], k <-> tile row base + 8(j>>2) + 4hi + (j&3)
+TT2_DEV bf16x8 trfrag(const bf16* t, int base, int db, int lane) {
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+  const int hi = lane >> 5, q = (lane >> 2) & 3, p = lane & 3, g = (lane >> 4) & 1;
+  const int col = 32 * db + 16 * g + 4 * p;
+  const int r0 = base + 4 * hi + q;
+  short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(t + toff(r0, col)));
+  short4v up = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(t + toff(r0 + 8, col)));
+  union { short4v s[2]; bf16x8 v; } u;
+  u.s[0] = lo;
+  u.s[1] = up;
+  return u.v;
+}
+// own-row fragments: X[row][16 st + 8 hi + j], st = 0..3 (zeros past the last row)
+TT2_DEV void own_frags(bf16x8 (&f)[4], const RowBuf& X, int row, int hi) {
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    union { uint4 u; bf16x8 v; } x;
+    x.u = buf_ld16(X, row, 2 * st + hi);
+    f[st] = x.v;
+  }
+}
+TT2_DEV int crow(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
+// store the lane's 16 accumulator rows (d = 32 db + crow) of one output row
+TT2_DEV void store_rowT(bf16* row, const f32x16 (&acc)[2], float sc, int hi) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      bf16x4 x;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] = (bf16)(acc[db][4 * rr + i] * sc);
+      *reinterpret_cast<bf16x4*>(row + 32 * db + 8 * rr + 4 * hi) = x;
+    }
+}
+TT2_DEV void zero16(f32x16& x) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = 0.f;
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
+  constexpr int NTH = NW * 64, PER = Stage3<NTH>::PER, QB = 32 * NW;
+  __shared__ __attribute__((aligned(16))) bf16 sK[2][64 * D];
+  __shared__ __attribute__((aligned(16))) bf16 sV[2][64 * D];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ql = lane & 31, hi = lane >> 5;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qblk = a.causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;   // heavy blocks first
+  const int q0 = qblk * QB, qw = q0 + 32 * w, qv = qw + ql;
+  const RowBuf Q = row_buf(reinterpret_cast<const bf16*>(a.q) + (int64_t)b * a.Tq * a.q_ld + h * D, a.q_ld, a.Tq);
+  const RowBuf K = row_buf(reinterpret_cast<const bf16*>(a.k) + (int64_t)b * a.Tk * a.k_ld + h * D, a.k_ld, a.Tk);
+  const RowBuf V = row_buf(reinterpret_cast<const bf16*>(a.v) + (int64_t)b * a.Tk * a.v_ld + h * D, a.v_ld, a.Tk);
+  bf16* O = reinterpret_cast<bf16*>(a.out) + (int64_t)b * a.Tq * a.o_ld + h * D;
+
+  bf16x8 fq[4];
+  own_frags(fq, Q, qv, hi);
+  const float c = a.scale * LOG2E;
+  float m_r = -INFINITY, l_r = 0.f;
+  f32x16 o[2];
+  zero16(o[0]);
+  zero16(o[1]);
+
+  const int klim = key_limit(a, b);
+  int kend = klim;
+  if (a.causal) kend = min(kend, q0 + QB);
+  const int ntile = kend > 0 ? (kend + 63) / 64 : 0;
+  uint4 rk[PER], rv[PER];
+  if (ntile > 0) {
+    g2r3<NTH>(rk, K, 0, tid);
+    g2r3<NTH>(rv, V, 0, tid);
+    r2s3<NTH>(rk, sK[0], tid);
+    r2s3<NTH>(rv, sV[0], tid);
+  }
+  __syncthreads();
+  for (int t = 0; t < ntile; ++t) {
+    const int k0 = 64 * t;
+    const bool more = t + 1 < ntile;
+    if (more) {
+      g2r3<NTH>(rk, K, k0 + 64, tid);
+      g2r3<NTH>(rv, V, k0 + 64, tid);
+    }
+    const bf16* cK = sK[t & 1];
+    const bf16* cV = sV[t & 1];
+    if (!(a.causal && k0 > qw + 31)) {   // wave-uniform: some key of the tile is visible
+      f32x16 s[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        zero16(s[kb]);
+#pragma unroll
+        for (int st = 0; st < 4; ++st) mma32(rowfrag(cK, 32 * kb + ql, 2 * st + hi), fq[st], s[kb]);
+      }
+      if (k0 + 64 > klim || (a.causal && k0 + 63 > qw)) {
+        // visible keys: key <= lim (one compare + select per score, no branches)
+        const int lim = (a.causal ? min(klim - 1, qv) : klim - 1) - k0;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[kb][r] = 32 * kb + crow(r, hi) > lim ? -INFINITY : s[kb][r];
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m_r, mx * c);
+      const float base = mn == -INFINITY ? 0.f : mn;
+      if (__any(mn != m_r)) {   // exact: skipped lanes would multiply by 1
+        const float alpha = fast_exp2(m_r - base);
+        l_r *= alpha;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) o[db] *= alpha;
+      }
+      m_r = mn;
+      bf16x8 pf[2][2];
+      float rs = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fast_exp2(fmaf(s[kb][r], c, -base));
+          rs += p;
+          pf[kb][r >> 3][r & 7] = (bf16)p;
+        }
+      l_r += rs;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) mma32(trfrag(cV, 32 * kb + 16 * hh, db, lane), pf[kb][hh], o[db]);
+    }
+    if (more) {
+      r2s3<NTH>(rk, sK[(t + 1) & 1], tid);
+      r2s3<NTH>(rv, sV[(t + 1) & 1], tid);
+    }
+    __syncthreads();
+  }
+  const float l = l_r + __shfl_xor(l_r, 32, 64);
+  if (qv < a.Tq) {
+    store_rowT(O + (int64_t)qv * a.o_ld, o, l > 0.f ? 1.f / l : 0.f, hi);
+    if (hi == 0) a.lse[(int64_t)bh * a.Tq + qv] = l > 0.f ? m_r + log2f(l) : INFINITY;
+  }
+}
+
+// dQ: wave = 32 queries (query on the lane), workgroup walks 64-key tiles in two
+// 32-key halves.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
+  constexpr int NTH = NW * 64, PER = Stage3<NTH>::PER, QB = 32 * NW;
+  __shared__ __attribute__((aligned(16))) bf16 sK[2][64 * D];
+  __shared__ __attribute__((aligned(16))) bf16 sV[2][64 * D];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ql = lane & 31, hi = lane >> 5;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qblk = a.causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int q0 = qblk * QB, qw = q0 + 32 * w, qv = qw + ql;
+  const RowBuf Q = row_buf(reinterpret_cast<const bf16*>(a.q) + (int64_t)b * a.Tq * a.q_ld + h * D, a.q_ld, a.Tq);
+  const RowBuf dO =
+      row_buf(reinterpret_cast<const bf16*>(a.dout) + (int64_t)b * a.Tq * a.do_ld + h * D, a.do_ld, a.Tq);
+  const RowBuf K = row_buf(reinterpret_cast<const bf16*>(a.k) + (int64_t)b * a.Tk * a.k_ld + h * D, a.k_ld, a.Tk);
+  const RowBuf V = row_buf(reinterpret_cast<const bf16*>(a.v) + (int64_t)b * a.Tk * a.v_ld + h * D, a.v_ld, a.Tk);
+  bf16* dQ = reinterpret_cast<bf16*>(a.dq) + (int64_t)b * a.Tq * a.dq_ld + h * D;
+
+  const bool qok = qv < a.Tq;
+  bf16x8 fq[4], fdo[4];
+  own_frags(fq, Q, qv, hi);
+  own_frags(fdo, dO, qv, hi);
+  const float lse = qok ? a.lse[(int64_t)bh * a.Tq + qv] : INFINITY;
+  const float dl = qok ? a.delta[(int64_t)bh * a.Tq + qv] : 0.f;
+  const float c = a.scale * LOG2E;
+  f32x16 dq[2];
+  zero16(dq[0]);
+  zero16(dq[1]);
+
+  const int klim = key_limit(a, b);
+  int kend = klim;
+  if (a.causal) kend = min(kend, q0 + QB);
+  const int ntile = kend > 0 ? (kend + 63) / 64 : 0;
+  uint4 rk[PER], rv[PER];
+  if (ntile > 0) {
+    g2r3<NTH>(rk, K, 0, tid);
+    g2r3<NTH>(rv, V, 0, tid);
+    r2s3<NTH>(rk, sK[0], tid);
+    r2s3<NTH>(rv, sV[0], tid);
+  }
+  __syncthreads();
+  for (int t = 0; t < ntile; ++t) {
+    const int k0 = 64 * t;
+    const bool more = t + 1 < ntile;
+    if (more) {
+      g2r3<NTH>(rk, K, k0 + 64, tid);
+      g2r3<NTH>(rv, V, k0 + 64, tid);
+    }
+    const bf16* cK = sK[t & 1];
+    const bf16* cV = sV[t & 1];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int kb0 = k0 + 32 * kb;
+      if (a.causal && kb0 > qw + 31) continue;   // wave-uniform
+      f32x16 s, dp;
+      zero16(s);
+      zero16(dp);
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        mma32(rowfrag(cK, 32 * kb + ql, 2 * st + hi), fq[st], s);
+        mma32(rowfrag(cV, 32 * kb + ql, 2 * st + hi), fdo[st], dp);
+      }
+      const bool edge = kb0 + 32 > klim || (a.causal && kb0 + 31 > qw);
+      const int lim = edge ? (a.causal ? min(klim - 1, qv) : klim - 1) - kb0 : 64;
+      bf16x8 dsf[2];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = fast_exp2(fmaf(s[r], c, -lse));
+        p = crow(r, hi) > lim ? 0.f : p;
+        dsf[r >> 3][r & 7] = (bf16)(p * (dp[r] - dl));
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int db = 0; db < 2; ++db) mma32(trfrag(cK, 32 * kb + 16 * hh, db, lane), dsf[hh], dq[db]);
+    }
+    if (more) {
+      r2s3<NTH>(rk, sK[(t + 1) & 1], tid);
+      r2s3<NTH>(rv, sV[(t + 1) & 1], tid);
+    }
+    __syncthreads();
+  }
+  if (qok) store_rowT(dQ + (int64_t)qv * a.dq_ld, dq, a.scale, hi);
+}
+
+// dK, dV: wave = 32 keys (key on the lane), workgroup walks 64-query tiles in two
+// 32-query halves.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
+  constexpr int NTH = NW * 64, PER = Stage3<NTH>::PER, KB = 32 * NW;
+  __shared__ __attribute__((aligned(16))) bf16 sQ[2][64 * D];
+  __shared__ __attribute__((aligned(16))) bf16 sdO[2][64 * D];
+  __shared__ __attribute__((aligned(16))) float sL[2][64], sDl[2][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int kl = lane & 31, hi = lane >> 5;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int k0 = blockIdx.x * KB, kw = k0 + 32 * w, kv = kw + kl;   // causal: low blocks (heaviest) first
+  const RowBuf Q = row_buf(reinterpret_cast<const bf16*>(a.q) + (int64_t)b * a.Tq * a.q_ld + h * D, a.q_ld, a.Tq);
+  const RowBuf dO =
+      row_buf(reinterpret_cast<const bf16*>(a.dout) + (int64_t)b * a.Tq * a.do_ld + h * D, a.do_ld, a.Tq);
+  const RowBuf K = row_buf(reinterpret_cast<const bf16*>(a.k) + (int64_t)b * a.Tk * a.k_ld + h * D, a.k_ld, a.Tk);
+  const RowBuf V = row_buf(reinterpret_cast<const bf16*>(a.v) + (int64_t)b * a.Tk * a.v_ld + h * D, a.v_ld, a.Tk);
+  bf16* dK = reinterpret_cast<bf16*>(a.dk) + (int64_t)b * a.Tk * a.dk_ld + h * D;
+  bf16* dV = reinterpret_cast<bf16*>(a.dv) + (int64_t)b * a.Tk * a.dv_ld + h * D;
+  const float* LSE = a.lse + (int64_t)bh * a.Tq;
+  const float* DL = a.delta + (int64_t)bh * a.Tq;
+
+  bf16x8 fk[4], fv[4];
+  own_frags(fk, K, kv, hi);
+  own_frags(fv, V, kv, hi);
+  const float c = a.scale * LOG2E;
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db) {
+    zero16(dk[db]);
+    zero16(dv[db]);
+  }
+  const int klim = key_limit(a, b);
+  const int qstart = a.causal ? (k0 / 64) * 64 : 0;
+  const int ntile = k0 < klim && a.Tq > qstart ? (a.Tq - qstart + 63) / 64 : 0;
+  auto stats = [&](int buf, int qb) {
+    if (tid < 64) {
+      const int q = qb + tid;
+      sL[buf][tid] = q < a.Tq ? LSE[q] : INFINITY;
+      sDl[buf][tid] = q < a.Tq ? DL[q] : 0.f;
+    }
+  };
+  uint4 rq[PER], rd[PER];
+  if (ntile > 0) {
+    g2r3<NTH>(rq, Q, qstart, tid);
+    g2r3<NTH>(rd, dO, qstart, tid);
+    r2s3<NTH>(rq, sQ[0], tid);
+    r2s3<NTH>(rd, sdO[0], tid);
+    stats(0, qstart);
+  }
+  __syncthreads();
+  for (int t = 0; t < ntile; ++t) {
+    const int q0 = qstart + 64 * t;
+    const bool more = t + 1 < ntile;
+    if (more) {
+      g2r3<NTH>(rq, Q, q0 + 64, tid);
+      g2r3<NTH>(rd, dO, q0 + 64, tid);
+    }
+    const bf16* cQ = sQ[t & 1];
+    const bf16* cD = sdO[t & 1];
+    const float* cL = sL[t & 1];
+    const float* cDl = sDl[t & 1];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int qb0 = q0 + 32 * qb;
+      if (kw >= klim || (a.causal && qb0 + 31 < kw)) continue;   // wave-uniform
+      f32x16 s, dp;
+      zero16(s);
+      zero16(dp);
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        mma32(rowfrag(cQ, 32 * qb + kl, 2 * st + hi), fk[st], s);
+        mma32(rowfrag(cD, 32 * qb + kl, 2 * st + hi), fv[st], dp);
+      }
+      // masked: query q < kv (causal) or every query when kv >= klim
+      const int qlo = kv >= klim ? 1 << 20 : (a.causal ? kv - qb0 : -1);   // visible iff crow >= qlo
+      bf16x8 pf[2], dsf[2];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int qi = 32 * qb + 8 * rr + 4 * hi;
+        const f32x4 L = *reinterpret_cast<const f32x4*>(cL + qi);
+        const f32x4 Dl = *reinterpret_cast<const f32x4*>(cDl + qi);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * rr + i;
+          float p = fast_exp2(fmaf(s[r], c, -L[i]));
+          p = crow(r, hi) < qlo ? 0.f : p;
+          pf[r >> 3][r & 7] = (bf16)p;
+          dsf[r >> 3][r & 7] = (bf16)(p * (dp[r] - Dl[i]));
+        }
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          mma32(trfrag(cD, 32 * qb + 16 * hh, db, lane), pf[hh], dv[db]);
+          mma32(trfrag(cQ, 32 * qb + 16 * hh, db, lane), dsf[hh], dk[db]);
+        }
+    }
+    if (more) {
+      r2s3<NTH>(rq, sQ[(t + 1) & 1], tid);
+      r2s3<NTH>(rd, sdO[(t + 1) & 1], tid);
+      stats((t + 1) & 1, q0 + 64);
+    }
+    __syncthreads();
+  }
+  if (kv < a.Tk) {
+    store_rowT(dK + (int64_t)kv * a.dk_ld, dk, a.scale, hi);
+    store_rowT(dV + (int64_t)kv * a.dv_ld, dv, 1.f, hi);
+  }
+}
+
 AttnArgs to_args(const tt2_attn_args* p) {
   AttnArgs a;
   a.q = p->q; a.k = p->k; a.v = p->v; a.o = p->o; a.dout = p->dout;
@@ -475,14 +893,32 @@ int validate(const tt2_attn_args* p) {
 
 }  // namespace
 
+// variant: 0 auto (bf16 -> v3, f32 -> v1), 1 v1, 2 v3 with 2 waves/workgroup, 3 v3 with 4.
+int v3_waves(const tt2_attn_args* p, int rows) {
+  if (p->dtype != TT2_DT_BF16 || p->variant == 1) return 0;
+  if (p->variant == 2) return 2;
+  if (p->variant == 3) return 4;
+  // auto: 4-wave blocks share each K/V (Q/dO) tile across 128 rows; drop to 2 waves
+  // when that leaves fewer than two workgroups per CU.
+  const int64_t wg4 = (int64_t)((rows + 127) / 128) * p->batch * p->heads;
+  return wg4 >= 512 ? 4 : 2;
+}
+
 extern "C" int tt2_attn_fwd(const tt2_attn_args* p, hipStream_t s) {
   if (int rc = validate(p)) return rc;
   if (!p->o_out || !p->lse) return tt2_set_error(TT2_E_INVALID, "tt2_attn_fwd: out/lse required");
   if (p->batch * p->tq == 0) return TT2_OK;
   AttnArgs a = to_args(p);
-  dim3 grid((p->tq + BQ - 1) / BQ, p->batch * p->heads);
-  if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(NT), 0, s, a);
-  else hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(NT), 0, s, a);
+  const int nw = v3_waves(p, p->tq);
+  if (nw == 4) {
+    hipLaunchKernelGGL(attn_fwd3_kernel<4>, dim3((p->tq + 127) / 128, p->batch * p->heads), dim3(256), 0, s, a);
+  } else if (nw == 2) {
+    hipLaunchKernelGGL(attn_fwd3_kernel<2>, dim3((p->tq + 63) / 64, p->batch * p->heads), dim3(128), 0, s, a);
+  } else {
+    dim3 grid((p->tq + BQ - 1) / BQ, p->batch * p->heads);
+    if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(NT), 0, s, a);
+  }
   return tt2_check_launch(hipGetLastError(), "tt2_attn_fwd");
 }
 
@@ -492,17 +928,21 @@ extern "C" int tt2_attn_bwd(const tt2_attn_args* p, hipStream_t s) {
     return tt2_set_error(TT2_E_INVALID, "tt2_attn_bwd: missing buffer");
   if (p->batch * p->tq == 0) return TT2_OK;
   AttnArgs a = to_args(p);
+  const int BH = p->batch * p->heads;
   dim3 gprep((p->batch * p->tq + 3) / 4);
-  dim3 gq((p->tq + BQ - 1) / BQ, p->batch * p->heads);
-  dim3 gk((p->tk + BKV - 1) / BKV, p->batch * p->heads);
   if (p->dtype == TT2_DT_BF16) {
     hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16>, gprep, dim3(NT), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<bf16>, gq, dim3(NT), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<bf16>, gk, dim3(NT), 0, s, a);
+    const int nq = v3_waves(p, p->tq), nk = v3_waves(p, p->tk);
+    if (nq == 4) hipLaunchKernelGGL(attn_bwd_dq3_kernel<4>, dim3((p->tq + 127) / 128, BH), dim3(256), 0, s, a);
+    else if (nq == 2) hipLaunchKernelGGL(attn_bwd_dq3_kernel<2>, dim3((p->tq + 63) / 64, BH), dim3(128), 0, s, a);
+    else hipLaunchKernelGGL(attn_bwd_dq_kernel<bf16>, dim3((p->tq + BQ - 1) / BQ, BH), dim3(NT), 0, s, a);
+    if (nk == 4) hipLaunchKernelGGL(attn_bwd_dkdv3_kernel<4>, dim3((p->tk + 127) / 128, BH), dim3(256), 0, s, a);
+    else if (nk == 2) hipLaunchKernelGGL(attn_bwd_dkdv3_kernel<2>, dim3((p->tk + 63) / 64, BH), dim3(128), 0, s, a);
+    else hipLaunchKernelGGL(attn_bwd_dkdv_kernel<bf16>, dim3((p->tk + BKV - 1) / BKV, BH), dim3(NT), 0, s, a);
   } else {
     hipLaunchKernelGGL(attn_bwd_prep_kernel<float>, gprep, dim3(NT), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<float>, gq, dim3(NT), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<float>, gk, dim3(NT), 0, s, a);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<float>, dim3((p->tq + BQ - 1) / BQ, BH), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<float>, dim3((p->tk + BKV - 1) / BKV, BH), dim3(NT), 0, s, a);
   }
   return tt2_check_launch(hipGetLastError(), "tt2_attn_bwd");
 }

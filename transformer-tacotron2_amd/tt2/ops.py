@@ -6,6 +6,7 @@ torch stream; nothing here allocates except ``Workspace.get`` outside capture.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -155,8 +156,14 @@ class LaunchProbe:
 PROBE: LaunchProbe | None = None
 
 
+# 0 = auto (v2 register-resident P), 1 = v1 (P through LDS); tests A/B both,
+# TT2_ATTN_VARIANT lets bench/profiling runs compare them.
+ATTN_VARIANT = int(os.environ.get("TT2_ATTN_VARIANT", "0"))
+
+
 def _attn_common(q, k, v, q_ld, k_ld, v_ld, batch, heads, tq, tk, key_len, causal, scale):
     a = _lib.AttnArgs()
+    a.variant = ATTN_VARIANT
     a.q, a.k, a.v = q.data_ptr(), k.data_ptr(), v.data_ptr()
     a.q_ld, a.k_ld, a.v_ld = q_ld, k_ld, v_ld
     if key_len is not None and key_len.dtype != torch.int32:
