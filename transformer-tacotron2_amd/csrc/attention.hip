@@ -472,7 +472,21 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 TT2_DEV void mma32(const bf16x8& a, const bf16x8& b, f32x16& c) {
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+#ifdef TT2_ABL_NOEXP   // timing-only ablation builds (tools/attn_ablate.sh)
+TT2_DEV float fast_exp2(float x) { return x; }
+#else
 TT2_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+#endif
+#ifdef TT2_ABL_L2HOT
+#define ABL_ROW(x) 0
+#else
+#define ABL_ROW(x) (x)
+#endif
+#ifdef TT2_ABL_NOSYNC
+#define ABL_SYNC()
+#else
+#define ABL_SYNC() __syncthreads()
+#endif
 
 // 16-B chunk c of tile row r lives at slot c ^ swz(r), swz(r) = h((r >> 1) & 7) with
 // h(x) = ((x & 1) << 2) | (x >> 1).  Row reads (ds_read_b128: 16 distinct rows mod 16
@@ -546,6 +560,15 @@ TT2_DEV void own_frags(bf16x8 (&f)[4], const RowBuf& X, int row, int hi) {
     f[st] = x.v;
   }
 }
+// value of lane l ^ 32 combined with lane l's: v_permlane32_swap instead of ds_bpermute
+TT2_DEV float xor32_max(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+TT2_DEV float xor32_sum(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 TT2_DEV int crow(int r, int hi) { return (r & 3) + 8 * (r >> 2) + 4 * hi; }
 // store the lane's 16 accumulator rows (d = 32 db + crow) of one output row
 TT2_DEV void store_rowT(bf16* row, const f32x16 (&acc)[2], float sc, int hi) {
@@ -572,8 +595,8 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 sV[2][64 * D];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ql = lane & 31, hi = lane >> 5;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int qblk = a.causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;   // heavy blocks first
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;   // x = (batch, head): block index on y
+  const int qblk = a.causal ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;   // heavy blocks first
   const int q0 = qblk * QB, qw = q0 + 32 * w, qv = qw + ql;
   const RowBuf Q = row_buf(reinterpret_cast<const bf16*>(a.q) + (int64_t)b * a.Tq * a.q_ld + h * D, a.q_ld, a.Tq);
   const RowBuf K = row_buf(reinterpret_cast<const bf16*>(a.k) + (int64_t)b * a.Tk * a.k_ld + h * D, a.k_ld, a.Tk);
@@ -604,8 +627,8 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
     const int k0 = 64 * t;
     const bool more = t + 1 < ntile;
     if (more) {
-      g2r3<NTH>(rk, K, k0 + 64, tid);
-      g2r3<NTH>(rv, V, k0 + 64, tid);
+      g2r3<NTH>(rk, K, ABL_ROW(k0 + 64), tid);
+      g2r3<NTH>(rv, V, ABL_ROW(k0 + 64), tid);
     }
     const bf16* cK = sK[t & 1];
     const bf16* cV = sV[t & 1];
@@ -619,18 +642,18 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
       }
       if (k0 + 64 > klim || (a.causal && k0 + 63 > qw)) {
         // visible keys: key <= lim (one compare + select per score, no branches)
-        const int lim = (a.causal ? min(klim - 1, qv) : klim - 1) - k0;
+        const int lim = (a.causal ? min(klim - 1, qv) : klim - 1) - k0 - 4 * hi;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) s[kb][r] = 32 * kb + crow(r, hi) > lim ? -INFINITY : s[kb][r];
+          for (int r = 0; r < 16; ++r) s[kb][r] = 32 * kb + crow(r, 0) > lim ? -INFINITY : s[kb][r];
       }
       float mx = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = xor32_max(mx);
       const float mn = fmaxf(m_r, mx * c);
       const float base = mn == -INFINITY ? 0.f : mn;
       if (__any(mn != m_r)) {   // exact: skipped lanes would multiply by 1
@@ -662,9 +685,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
       r2s3<NTH>(rk, sK[(t + 1) & 1], tid);
       r2s3<NTH>(rv, sV[(t + 1) & 1], tid);
     }
-    __syncthreads();
+    ABL_SYNC();
   }
-  const float l = l_r + __shfl_xor(l_r, 32, 64);
+  const float l = xor32_sum(l_r);
   if (qv < a.Tq) {
     store_rowT(O + (int64_t)qv * a.o_ld, o, l > 0.f ? 1.f / l : 0.f, hi);
     if (hi == 0) a.lse[(int64_t)bh * a.Tq + qv] = l > 0.f ? m_r + log2f(l) : INFINITY;
@@ -680,8 +703,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 sV[2][64 * D];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ql = lane & 31, hi = lane >> 5;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int qblk = a.causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;   // x = (batch, head): block index on y
+  const int qblk = a.causal ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;
   const int q0 = qblk * QB, qw = q0 + 32 * w, qv = qw + ql;
   const RowBuf Q = row_buf(reinterpret_cast<const bf16*>(a.q) + (int64_t)b * a.Tq * a.q_ld + h * D, a.q_ld, a.Tq);
   const RowBuf dO =
@@ -717,8 +740,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
     const int k0 = 64 * t;
     const bool more = t + 1 < ntile;
     if (more) {
-      g2r3<NTH>(rk, K, k0 + 64, tid);
-      g2r3<NTH>(rv, V, k0 + 64, tid);
+      g2r3<NTH>(rk, K, ABL_ROW(k0 + 64), tid);
+      g2r3<NTH>(rv, V, ABL_ROW(k0 + 64), tid);
     }
     const bf16* cK = sK[t & 1];
     const bf16* cV = sV[t & 1];
@@ -735,12 +758,12 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
         mma32(rowfrag(cV, 32 * kb + ql, 2 * st + hi), fdo[st], dp);
       }
       const bool edge = kb0 + 32 > klim || (a.causal && kb0 + 31 > qw);
-      const int lim = edge ? (a.causal ? min(klim - 1, qv) : klim - 1) - kb0 : 64;
+      const int lim = edge ? (a.causal ? min(klim - 1, qv) : klim - 1) - kb0 - 4 * hi : 64;
       bf16x8 dsf[2];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float p = fast_exp2(fmaf(s[r], c, -lse));
-        p = crow(r, hi) > lim ? 0.f : p;
+        p = crow(r, 0) > lim ? 0.f : p;
         dsf[r >> 3][r & 7] = (bf16)(p * (dp[r] - dl));
       }
 #pragma unroll
@@ -752,7 +775,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
       r2s3<NTH>(rk, sK[(t + 1) & 1], tid);
       r2s3<NTH>(rv, sV[(t + 1) & 1], tid);
     }
-    __syncthreads();
+    ABL_SYNC();
   }
   if (qok) store_rowT(dQ + (int64_t)qv * a.dq_ld, dq, a.scale, hi);
 }
@@ -767,8 +790,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float sL[2][64], sDl[2][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int kl = lane & 31, hi = lane >> 5;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int k0 = blockIdx.x * KB, kw = k0 + 32 * w, kv = kw + kl;   // causal: low blocks (heaviest) first
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;   // x = (batch, head): block index on y
+  const int k0 = blockIdx.y * KB, kw = k0 + 32 * w, kv = kw + kl;   // causal: low blocks (heaviest) first
   const RowBuf Q = row_buf(reinterpret_cast<const bf16*>(a.q) + (int64_t)b * a.Tq * a.q_ld + h * D, a.q_ld, a.Tq);
   const RowBuf dO =
       row_buf(reinterpret_cast<const bf16*>(a.dout) + (int64_t)b * a.Tq * a.do_ld + h * D, a.do_ld, a.Tq);
@@ -812,8 +835,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
     const int q0 = qstart + 64 * t;
     const bool more = t + 1 < ntile;
     if (more) {
-      g2r3<NTH>(rq, Q, q0 + 64, tid);
-      g2r3<NTH>(rd, dO, q0 + 64, tid);
+      g2r3<NTH>(rq, Q, ABL_ROW(q0 + 64), tid);
+      g2r3<NTH>(rd, dO, ABL_ROW(q0 + 64), tid);
     }
     const bf16* cQ = sQ[t & 1];
     const bf16* cD = sdO[t & 1];
@@ -832,7 +855,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
         mma32(rowfrag(cD, 32 * qb + kl, 2 * st + hi), fv[st], dp);
       }
       // masked: query q < kv (causal) or every query when kv >= klim
-      const int qlo = kv >= klim ? 1 << 20 : (a.causal ? kv - qb0 : -1);   // visible iff crow >= qlo
+      const int qlo = (kv >= klim ? 1 << 20 : (a.causal ? kv - qb0 : -1)) - 4 * hi;   // visible iff crow >= qlo
       bf16x8 pf[2], dsf[2];
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
@@ -843,7 +866,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * rr + i;
           float p = fast_exp2(fmaf(s[r], c, -L[i]));
-          p = crow(r, hi) < qlo ? 0.f : p;
+          p = crow(r, 0) < qlo ? 0.f : p;
           pf[r >> 3][r & 7] = (bf16)p;
           dsf[r >> 3][r & 7] = (bf16)(p * (dp[r] - Dl[i]));
         }
@@ -861,7 +884,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
       r2s3<NTH>(rd, sdO[(t + 1) & 1], tid);
       stats((t + 1) & 1, q0 + 64);
     }
-    __syncthreads();
+    ABL_SYNC();
   }
   if (kv < a.Tk) {
     store_rowT(dK + (int64_t)kv * a.dk_ld, dk, a.scale, hi);
@@ -893,15 +916,19 @@ int validate(const tt2_attn_args* p) {
 
 }  // namespace
 
+// v3 grids are (batch*heads, row blocks): dispatch walks every (batch, head) of one
+// row block before the next, so under a causal mask the heaviest blocks go first
+// chip-wide (forward / dQ blocks are reversed in-kernel; dK-dV block 0 is heaviest).
 // variant: 0 auto (bf16 -> v3, f32 -> v1), 1 v1, 2 v3 with 2 waves/workgroup, 3 v3 with 4.
-int v3_waves(const tt2_attn_args* p, int rows) {
+int v3_waves(const tt2_attn_args* p, int rows, bool fwd) {
   if (p->dtype != TT2_DT_BF16 || p->variant == 1) return 0;
   if (p->variant == 2) return 2;
   if (p->variant == 3) return 4;
-  // auto: 4-wave blocks share each K/V (Q/dO) tile across 128 rows; drop to 2 waves
-  // when that leaves fewer than two workgroups per CU.
+  // auto: the forward shares each K/V tile across 4 waves (128 queries) while that
+  // still gives two workgroups per CU; the backward kernels (more registers, 2 waves
+  // per SIMD) measure faster with 2-wave workgroups at every shape of the workload.
   const int64_t wg4 = (int64_t)((rows + 127) / 128) * p->batch * p->heads;
-  return wg4 >= 512 ? 4 : 2;
+  return fwd && wg4 >= 512 ? 4 : 2;
 }
 
 extern "C" int tt2_attn_fwd(const tt2_attn_args* p, hipStream_t s) {
@@ -909,11 +936,11 @@ extern "C" int tt2_attn_fwd(const tt2_attn_args* p, hipStream_t s) {
   if (!p->o_out || !p->lse) return tt2_set_error(TT2_E_INVALID, "tt2_attn_fwd: out/lse required");
   if (p->batch * p->tq == 0) return TT2_OK;
   AttnArgs a = to_args(p);
-  const int nw = v3_waves(p, p->tq);
+  const int nw = v3_waves(p, p->tq, true);
   if (nw == 4) {
-    hipLaunchKernelGGL(attn_fwd3_kernel<4>, dim3((p->tq + 127) / 128, p->batch * p->heads), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(attn_fwd3_kernel<4>, dim3(p->batch * p->heads, (p->tq + 127) / 128), dim3(256), 0, s, a);
   } else if (nw == 2) {
-    hipLaunchKernelGGL(attn_fwd3_kernel<2>, dim3((p->tq + 63) / 64, p->batch * p->heads), dim3(128), 0, s, a);
+    hipLaunchKernelGGL(attn_fwd3_kernel<2>, dim3(p->batch * p->heads, (p->tq + 63) / 64), dim3(128), 0, s, a);
   } else {
     dim3 grid((p->tq + BQ - 1) / BQ, p->batch * p->heads);
     if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(attn_fwd_kernel<bf16>, grid, dim3(NT), 0, s, a);
@@ -932,12 +959,12 @@ extern "C" int tt2_attn_bwd(const tt2_attn_args* p, hipStream_t s) {
   dim3 gprep((p->batch * p->tq + 3) / 4);
   if (p->dtype == TT2_DT_BF16) {
     hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16>, gprep, dim3(NT), 0, s, a);
-    const int nq = v3_waves(p, p->tq), nk = v3_waves(p, p->tk);
-    if (nq == 4) hipLaunchKernelGGL(attn_bwd_dq3_kernel<4>, dim3((p->tq + 127) / 128, BH), dim3(256), 0, s, a);
-    else if (nq == 2) hipLaunchKernelGGL(attn_bwd_dq3_kernel<2>, dim3((p->tq + 63) / 64, BH), dim3(128), 0, s, a);
+    const int nq = v3_waves(p, p->tq, false), nk = v3_waves(p, p->tk, false);
+    if (nq == 4) hipLaunchKernelGGL(attn_bwd_dq3_kernel<4>, dim3(BH, (p->tq + 127) / 128), dim3(256), 0, s, a);
+    else if (nq == 2) hipLaunchKernelGGL(attn_bwd_dq3_kernel<2>, dim3(BH, (p->tq + 63) / 64), dim3(128), 0, s, a);
     else hipLaunchKernelGGL(attn_bwd_dq_kernel<bf16>, dim3((p->tq + BQ - 1) / BQ, BH), dim3(NT), 0, s, a);
-    if (nk == 4) hipLaunchKernelGGL(attn_bwd_dkdv3_kernel<4>, dim3((p->tk + 127) / 128, BH), dim3(256), 0, s, a);
-    else if (nk == 2) hipLaunchKernelGGL(attn_bwd_dkdv3_kernel<2>, dim3((p->tk + 63) / 64, BH), dim3(128), 0, s, a);
+    if (nk == 4) hipLaunchKernelGGL(attn_bwd_dkdv3_kernel<4>, dim3(BH, (p->tk + 127) / 128), dim3(256), 0, s, a);
+    else if (nk == 2) hipLaunchKernelGGL(attn_bwd_dkdv3_kernel<2>, dim3(BH, (p->tk + 63) / 64), dim3(128), 0, s, a);
     else hipLaunchKernelGGL(attn_bwd_dkdv_kernel<bf16>, dim3((p->tk + BKV - 1) / BKV, BH), dim3(NT), 0, s, a);
   } else {
     hipLaunchKernelGGL(attn_bwd_prep_kernel<float>, gprep, dim3(NT), 0, s, a);

@@ -12,7 +12,7 @@ import os
 import torch  # noqa: F401  (must precede CDLL: one HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtt2.so")
+LIB_PATH = os.environ.get("TT2_LIB") or os.path.join(_HERE, "libtt2.so")   # TT2_LIB: dev ablation builds
 
 DT_F32 = 0
 DT_BF16 = 1
