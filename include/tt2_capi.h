@@ -160,6 +160,8 @@ typedef struct tt2_ln_args {
   float eps, grad_beta;
   uint32_t drop_site, drop_thr;
   float drop_scale;
+  float* dbias;   /* bwd, optional: grad_beta*dbias + column sums of the branch gradient
+                     (= the bias gradient of the linear layer that produced `branch`) */
 } tt2_ln_args;
 int tt2_layernorm_fwd(const tt2_ln_args* a, hipStream_t stream);
 size_t tt2_layernorm_bwd_workspace_size(const tt2_ln_args* a);

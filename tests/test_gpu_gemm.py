@@ -46,8 +46,11 @@ def test_gemm_layouts(dtype, variant, ta, tb, mnk):
 
 @pytest.mark.parametrize("dtype,variant", VARIANTS)
 @pytest.mark.parametrize("n", [200, 81])
-def test_gemm_epilogue(dtype, variant, n):
-    m, k = 300, 96
+@pytest.mark.parametrize("splits", [1, 3])
+def test_gemm_epilogue(dtype, variant, n, splits):
+    """Fused epilogue (bias, residual, ReLU, gate, dropout), applied in the kernel or
+    in the split-K reduce."""
+    m, k = 300, 96 * splits
     g = torch.Generator().manual_seed(1)
     A, B = _mk((m, k), dtype, g), _mk((n, k), dtype, g)
     bias = torch.randn(n, generator=g).cuda()
@@ -56,7 +59,7 @@ def test_gemm_epilogue(dtype, variant, n):
     seed = torch.tensor([1234], dtype=torch.int32).cuda()
     out = torch.empty(m, n, dtype=dtype, device="cuda")
     ops.gemm(A, B, out, m, n, k, k, k, n, bias=bias, res=R, ldr=n, act=ops._lib.ACT_RELU, gate=G, ldg=n,
-             gate_scale=1.7, alpha=0.5, drop=ops.Drop(seed, 77, 0.3), variant=variant)
+             gate_scale=1.7, alpha=0.5, drop=ops.Drop(seed, 77, 0.3), variant=variant, splits=splits)
     ref = 0.5 * (A.double() @ B.double().t()) + bias.double() + R.double()
     ref = ref.relu() * (G.double() != 0) * 1.7
     keep = torch.from_numpy(dropout_keep(1234, 77, m * n, 0.3)).view(m, n).cuda()
@@ -98,6 +101,9 @@ def test_conv_implicit_gemm(dtype, variant, cin, cout):
     dyr = dy.to(dtype).double()
     ref = F.conv1d(xr.transpose(1, 2), wr, padding=pad).transpose(1, 2).reshape(M, cout)
     assert rel(y, ref) < 1e-5
+    y2 = torch.empty(M, cout, device="cuda")
+    ops.gemm(xd, wp, y2, M, cout, KS * cin, cin, KS * cin, cout, a_conv=(T, cin, pad), variant=variant, splits=2)
+    assert rel(y2, ref) < 1e-5
     # dgrad
     dx = torch.empty(M, cin, device="cuda")
     ops.gemm(dyd, wflip, dx, M, cin, KS * cout, cout, KS * cout, cin, a_conv=(T, cout, pad), variant=variant)

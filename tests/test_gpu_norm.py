@@ -1,0 +1,60 @@
+"""Fused residual + dropout + LayerNorm forward/backward vs float64 torch (GPU)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from tt2 import ops  # noqa: E402
+from tt2_oracle import dropout_keep  # noqa: E402
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("m", [1, 37, 2048, 5000])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_layernorm_fwd_bwd_dbias(dtype, m, p):
+    C = 512
+    g = torch.Generator().manual_seed(m + int(p * 10))
+    x = torch.randn(m, C, generator=g)
+    br = torch.randn(m, C, generator=g)
+    gamma = 1 + 0.1 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    dy = torch.randn(m, C, generator=g)
+    xd, brd, dyd = x.to(dtype).cuda(), br.to(dtype).cuda(), dy.to(dtype).cuda()
+    seed = torch.tensor([99], dtype=torch.int32).cuda()
+    drop = ops.Drop(seed, 17, p)
+    y = torch.empty(m, C, dtype=dtype, device="cuda")
+    mean = torch.empty(m, device="cuda")
+    rstd = torch.empty(m, device="cuda")
+    ops.layernorm_fwd(xd, brd, gamma.cuda(), beta.cuda(), y, mean, rstd, m, drop=drop)
+
+    keep = torch.from_numpy(dropout_keep(99, 17, m * C, p)).view(m, C).double() if p > 0 else torch.ones(m, C,
+                                                                                                           dtype=torch.float64)
+    xr = x.to(dtype).double()
+    brr = br.to(dtype).double().requires_grad_(True)
+    s = xr.requires_grad_(True) + brr * keep / (1 - p)
+    yr = torch.nn.functional.layer_norm(s, (C,), gamma.double().requires_grad_(True),
+                                        beta.double().requires_grad_(True), eps=1e-5)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel(y, yr) < tol
+    yr.backward(dy.to(dtype).double())
+
+    dx = torch.empty(m, C, dtype=dtype, device="cuda")
+    dbr = torch.empty(m, C, dtype=dtype, device="cuda")
+    dgamma = torch.full((C,), 0.5, device="cuda")
+    dbeta = torch.zeros(C, device="cuda")
+    dbias = torch.full((C,), 0.25, device="cuda")
+    ops.layernorm_bwd(dyd, xd, brd, gamma.cuda(), mean, rstd, dx, dbr, dgamma, dbeta, m, drop=drop, dbias=dbias)
+    tol_b = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel(dx, xr.grad) < tol_b
+    assert rel(dbr, brr.grad) < tol_b
+    # grads overwrite (grad_beta 0) the destinations
+    ref_g = (dy.to(dtype).double() * (s - s.mean(1, keepdim=True)) /
+             (s.var(1, unbiased=False, keepdim=True) + 1e-5).sqrt()).sum(0)
+    assert rel(dgamma, ref_g.detach()) < tol_b
+    assert rel(dbeta, dy.to(dtype).double().sum(0)) < tol_b
+    assert rel(dbias, brr.grad.sum(0)) < tol_b

@@ -52,7 +52,9 @@ struct LnArgs {
   void* y; void* dx; void* dbranch;
   const float* gamma; const float* beta;
   float* mean; float* rstd;
-  float* part;  // bwd: [gridDim.x][2][C] (dgamma, dbeta)
+  float* part;  // bwd: [gridDim.x][3][C] (dgamma, dbeta, dbias) partial sums
+  float* dgamma; float* dbeta; float* dbias;
+  float grad_beta;
   int M, C;
   float eps;
   DropDesc drop;
@@ -88,57 +90,106 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(LnArgs a) {
   if (lane == 0 && a.mean) { a.mean[row] = mean; a.rstd[row] = rstd; }
 }
 
+// Backward: 8 waves per workgroup, one 512-wide row per wave and two rows in
+// flight (both rows' x / branch / dy loads issued before either is reduced), so
+// the ~1-row-per-wave latency chain of a plain loop is halved.  Per-workgroup
+// (dgamma, dbeta, dbias) column partials go to part[block][3][C]; ln_bwd_finalize
+// sums them (fixed order: bitwise reproducible).
+constexpr int LNB_NT = 512;
 template <typename T>
-__global__ __launch_bounds__(NT) void ln_bwd_kernel(LnArgs a) {
-  __shared__ float red[4][2][512];
+__global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
+  __shared__ float red[3][4][512];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c0 = lane * 8;
-  float g[8], bt[8];
+  float g[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { g[j] = a.gamma[c0 + j]; bt[j] = 0.f; }
-  float pg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < 8; ++j) g[j] = a.gamma[c0 + j];
+  float pg[8], pb[8], pd[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pg[j] = pb[j] = pd[j] = 0.f;
   const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
-  for (int row = blockIdx.x * 4 + w; row < a.M; row += gridDim.x * 4) {
-    const int64_t off = (int64_t)row * a.C + c0;
-    float s[8], br[8], dy[8];
-    ld8(reinterpret_cast<const T*>(a.x) + off, s);
-    ld8(reinterpret_cast<const T*>(a.dy) + off, dy);
-    if (a.branch) {
-      ld8(reinterpret_cast<const T*>(a.branch) + off, br);
+  const T* X = reinterpret_cast<const T*>(a.x);
+  const T* BR = reinterpret_cast<const T*>(a.branch);
+  const T* DY = reinterpret_cast<const T*>(a.dy);
+  const int stride = gridDim.x * 8;
+  for (int r0 = blockIdx.x * 8 + w; r0 < a.M; r0 += 2 * stride) {
+    const int rows[2] = {r0, r0 + stride};
+    float s[2][8], dy[2][8], br[2][8], mean[2], rstd[2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] += a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)(off + j), br[j]) : br[j];
+    for (int u = 0; u < 2; ++u) {
+      const int row = rows[u] < a.M ? rows[u] : r0;   // duplicate row: loaded, never stored
+      const int64_t off = (int64_t)row * a.C + c0;
+      ld8(X + off, s[u]);
+      ld8(DY + off, dy[u]);
+      if (BR) ld8(BR + off, br[u]);
+      mean[u] = a.mean[row];
+      rstd[u] = a.rstd[row];
     }
-    const float mean = a.mean[row], rstd = a.rstd[row];
-    float c1 = 0.f, c2 = 0.f, xh[8], gd[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      xh[j] = (s[j] - mean) * rstd;
-      gd[j] = g[j] * dy[j];
-      c1 += gd[j];
-      c2 += gd[j] * xh[j];
-      pg[j] += dy[j] * xh[j];
-      pb[j] += dy[j];
-    }
-    c1 = wave_sum(c1) / a.C;
-    c2 = wave_sum(c2) / a.C;
-    float ds[8], db[8];
+    for (int u = 0; u < 2; ++u) {
+      if (rows[u] >= a.M) break;
+      const int64_t off = (int64_t)rows[u] * a.C + c0;
+      if (BR) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      ds[j] = rstd * (gd[j] - c1 - xh[j] * c2);
-      db[j] = a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)(off + j), ds[j]) : ds[j];
+        for (int j = 0; j < 8; ++j)
+          s[u][j] += a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)(off + j), br[u][j]) : br[u][j];
+      }
+      float c1 = 0.f, c2 = 0.f, xh[8], gd[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xh[j] = (s[u][j] - mean[u]) * rstd[u];
+        gd[j] = g[j] * dy[u][j];
+        c1 += gd[j];
+        c2 += gd[j] * xh[j];
+        pg[j] += dy[u][j] * xh[j];
+        pb[j] += dy[u][j];
+      }
+      c1 = wave_sum(c1) / a.C;
+      c2 = wave_sum(c2) / a.C;
+      float ds[8], db[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ds[j] = rstd[u] * (gd[j] - c1 - xh[j] * c2);
+        db[j] = a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)(off + j), ds[j]) : ds[j];
+        pd[j] += db[j];
+      }
+      st8(reinterpret_cast<T*>(a.dx) + off, ds);
+      if (a.dbranch) st8(reinterpret_cast<T*>(a.dbranch) + off, db);
     }
-    st8(reinterpret_cast<T*>(a.dx) + off, ds);
-    if (a.dbranch) st8(reinterpret_cast<T*>(a.dbranch) + off, db);
   }
+  // 8 waves -> 4 rows of LDS partials -> 1
+  if (w >= 4) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { red[w][0][c0 + j] = pg[j]; red[w][1][c0 + j] = pb[j]; }
+    for (int j = 0; j < 8; ++j) { red[0][w - 4][c0 + j] = pg[j]; red[1][w - 4][c0 + j] = pb[j]; red[2][w - 4][c0 + j] = pd[j]; }
+  }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * a.C; i += NT) {
-    const int which = i / a.C, c = i % a.C;
-    a.part[((int64_t)blockIdx.x * 2 + which) * a.C + c] =
-        red[0][which][c] + red[1][which][c] + red[2][which][c] + red[3][which][c];
+  if (w < 4) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { red[0][w][c0 + j] += pg[j]; red[1][w][c0 + j] += pb[j]; red[2][w][c0 + j] += pd[j]; }
   }
-  (void)bt;
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * a.C; i += LNB_NT) {
+    const int which = i / a.C, c = i % a.C;
+    a.part[((int64_t)blockIdx.x * 3 + which) * a.C + c] =
+        red[which][0][c] + red[which][1][c] + red[which][2][c] + red[which][3][c];
+  }
+}
+
+// grid (C / 64, 3): column block x of partial array y; 4 row groups of 64 lanes.
+__global__ __launch_bounds__(256) void ln_bwd_finalize(LnArgs a, int nb) {
+  __shared__ float sm[4][64];
+  const int which = blockIdx.y;
+  float* dst = which == 0 ? a.dgamma : (which == 1 ? a.dbeta : a.dbias);
+  if (!dst) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  float acc = 0.f;
+  for (int r = rg; r < nb; r += 4) acc += a.part[((int64_t)r * 3 + which) * a.C + c];
+  sm[rg][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rg == 0) {
+    const float v = (sm[0][threadIdx.x] + sm[1][threadIdx.x]) + (sm[2][threadIdx.x] + sm[3][threadIdx.x]);
+    dst[c] = a.grad_beta != 0.f ? a.grad_beta * dst[c] + v : v;
+  }
 }
 
 // --------------------------------------------------------------- BatchNorm
@@ -327,29 +378,27 @@ extern "C" int tt2_layernorm_fwd(const tt2_ln_args* p, hipStream_t s) {
 }
 
 extern "C" size_t tt2_layernorm_bwd_workspace_size(const tt2_ln_args* p) {
-  return (size_t)TT2_LN_BWD_BLOCKS * 2 * p->c * sizeof(float);
+  return (size_t)TT2_LN_BWD_BLOCKS * 3 * p->c * sizeof(float);
 }
 
 extern "C" int tt2_layernorm_bwd(const tt2_ln_args* p, hipStream_t s) {
   if (p->c != 512) return tt2_set_error(TT2_E_INVALID, "tt2_layernorm: C must be 512");
   if (!p->workspace || p->ws_bytes < tt2_layernorm_bwd_workspace_size(p))
     return tt2_set_error(TT2_E_INVALID, "tt2_layernorm_bwd: workspace too small");
+  if (p->dbias && !p->branch) return tt2_set_error(TT2_E_INVALID, "tt2_layernorm_bwd: dbias needs a branch");
   LnArgs a{};
   a.x = p->x; a.branch = p->branch; a.dy = p->dy; a.dx = p->dx; a.dbranch = p->dbranch;
   a.gamma = p->gamma; a.beta = p->beta; a.mean = p->mean; a.rstd = p->rstd;
   a.part = reinterpret_cast<float*>(p->workspace);
+  a.dgamma = p->dgamma; a.dbeta = p->dbeta; a.dbias = p->dbias; a.grad_beta = p->grad_beta;
   a.M = p->m; a.C = p->c; a.eps = p->eps;
   a.drop = DropDesc{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
+  if (p->m == 0) return TT2_OK;
   const int nb = TT2_LN_BWD_BLOCKS;
-  if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(NT), 0, s, a);
-  else hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nb), dim3(NT), 0, s, a);
-  if (int rc = tt2_check_launch(hipGetLastError(), "tt2_layernorm_bwd")) return rc;
-  // gamma / beta gradients: sum the per-block partials
-  tt2_reduce_args r{};
-  r.src = a.part; r.rows = nb; r.cols = p->c; r.ld = 2 * p->c; r.dst = p->dgamma; r.beta = p->grad_beta;
-  if (int rc = tt2_reduce_rows(&r, s)) return rc;
-  r.src = a.part + p->c; r.dst = p->dbeta;
-  return tt2_reduce_rows(&r, s);
+  if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(LNB_NT), 0, s, a);
+  else hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nb), dim3(LNB_NT), 0, s, a);
+  hipLaunchKernelGGL(ln_bwd_finalize, dim3(p->c / 64, 3), dim3(256), 0, s, a, nb);
+  return tt2_check_launch(hipGetLastError(), "tt2_layernorm_bwd");
 }
 
 static BnArgs bn_args(const tt2_bn_args* p) {

@@ -140,7 +140,7 @@ class LnArgs(C.Structure):
         ("gamma", vp), ("beta", vp), ("mean", vp), ("rstd", vp), ("dgamma", vp), ("dbeta", vp),
         ("workspace", vp), ("ws_bytes", sz), ("drop_seed", vp),
         ("m", i32), ("c", i32), ("dtype", i32), ("eps", f32), ("grad_beta", f32),
-        ("drop_site", u32), ("drop_thr", u32), ("drop_scale", f32),
+        ("drop_site", u32), ("drop_thr", u32), ("drop_scale", f32), ("dbias", vp),
     ]
 
 

@@ -37,11 +37,22 @@ def sinusoid_table(max_len: int, dim: int) -> torch.Tensor:
 
 
 def auto_splits(n_out: int, n_in: int, k: int) -> int:
+    """Split-K factor for a weight-gradient GEMM (long K = tokens, few output tiles)."""
     tiles = ((n_out + 127) // 128) * ((n_in + 127) // 128)
     if tiles >= 256:
         return 1
     s = max(1, min(32, 512 // tiles, k // 256))
     return s
+
+
+def act_splits(m: int, n: int, k: int) -> int:
+    """Split-K factor for an activation GEMM: only when its 128x128 tiles cannot fill
+    the 256 CUs (the encoder's 2048-token GEMMs); the epilogue then runs in the
+    split-K reduce."""
+    tiles = ((m + 127) // 128) * ((n + 127) // 128)
+    if tiles >= 192 or k < 1024:
+        return 1
+    return max(1, min(8, 512 // tiles, k // 512))
 
 
 class Arena:
@@ -235,19 +246,19 @@ class TTSEngine:
     def _lin(self, x, w, out, m, n, k, bias=None, act=ACT_NONE, drop=NO_DROP, res=None, ldx=None, ldo=None,
              a_conv=None, beta=0.0):
         ops.gemm(x, w, out, m, n, k, ldx or k, k, ldo or n, bias=bias, res=res, ldr=ldo or n, act=act, drop=drop,
-                 a_conv=a_conv, beta=beta, ws=self.ws)
+                 a_conv=a_conv, beta=beta, ws=self.ws, splits=act_splits(m, n, k))
 
     def _dgrad(self, dy, w, out, m, n_in, n_out, res=None, gate=None, gate_scale=1.0, ldy=None, ldo=None,
                a_conv=None, beta=0.0):
         """out[m, n_in] = dy[m, n_out] @ W[n_out, n_in] (+res) (*gate)"""
         ops.gemm(dy, w, out, m, n_in, n_out, ldy or n_out, n_in, ldo or n_in, trans_b=True, res=res,
                  ldr=ldo or n_in, gate=gate, ldg=ldo or n_in, gate_scale=gate_scale, a_conv=a_conv, beta=beta,
-                 ws=self.ws)
+                 ws=self.ws, splits=act_splits(m, n_in, n_out))
 
     def _conv_dgrad(self, dy, wflip, out, m, cin, cout, K, T, ldo=None, beta=0.0):
         """out[m, cin] = conv1d(dy, flipped W): implicit im2col of dy x wflip[cin][tap][cout]"""
         ops.gemm(dy, wflip, out, m, cin, K * cout, cout, K * cout, ldo or cin, a_conv=(T, cout, (K - 1) // 2),
-                 beta=beta, ws=self.ws)
+                 beta=beta, ws=self.ws, splits=act_splits(m, cin, K * cout))
 
     def _wgrad(self, dy, x, gw, n_out, n_in, m, ldy=None, ldx=None, b_conv=None):
         """gw[n_out, n_in] (f32) = dy[m, n_out]^T @ x[m, n_in]"""
@@ -455,9 +466,8 @@ class TTSEngine:
             # LN3 + FFN
             ops.layernorm_bwd(gx, h2, A[f"df2{l}"], self.P(p + "ln3.g"), A[f"dln3m{l}"], A[f"dln3r{l}"], A["g_res"],
                               A["g_br"], self.G(p + "ln3.g"), self.G(p + "ln3.b"), Md,
-                              drop=self.drop(base + 3, c.dropout), ws=self.ws)
+                              drop=self.drop(base + 3, c.dropout), ws=self.ws, dbias=self.G(p + "ffn2.b"))
             self._wgrad(A["g_br"], A[f"df1{l}"], self.G(p + "ffn2.w"), d, F, Md)
-            self._bias(A["g_br"], d, Md, d, self.G(p + "ffn2.b"))
             self._dgrad(A["g_br"], self.W(p + "ffn2.w"), A["g_f1"], Md, F, d, gate=A[f"df1{l}"],
                         gate_scale=gs(c.dropout))
             self._wgrad(A["g_f1"], h2, self.G(p + "ffn1.w"), F, d, Md)
@@ -467,9 +477,8 @@ class TTSEngine:
             # LN2 + cross attention
             ops.layernorm_bwd(gx, h1, A[f"dco{l}"], self.P(p + "ln2.g"), A[f"dln2m{l}"], A[f"dln2r{l}"], A["g_res"],
                               A["g_br"], self.G(p + "ln2.g"), self.G(p + "ln2.b"), Md,
-                              drop=self.drop(base + 1, c.dropout), ws=self.ws)
+                              drop=self.drop(base + 1, c.dropout), ws=self.ws, dbias=self.G(p + "co.b"))
             self._wgrad(A["g_br"], A[f"dcatt{l}"], self.G(p + "co.w"), d, d, Md)
-            self._bias(A["g_br"], d, Md, d, self.G(p + "co.b"))
             self._dgrad(A["g_br"], self.W(p + "co.w"), A["g_att"], Md, d, d)
             ko = 2 * d * l
             g_cq = A["g_qkv"][:, :d]
@@ -483,9 +492,8 @@ class TTSEngine:
             # LN1 + self attention
             ops.layernorm_bwd(gx, x_in, A[f"do{l}"], self.P(p + "ln1.g"), A[f"dln1m{l}"], A[f"dln1r{l}"],
                               A["g_res"], A["g_br"], self.G(p + "ln1.g"), self.G(p + "ln1.b"), Md,
-                              drop=self.drop(base, c.dropout), ws=self.ws)
+                              drop=self.drop(base, c.dropout), ws=self.ws, dbias=self.G(p + "o.b"))
             self._wgrad(A["g_br"], A[f"datt{l}"], self.G(p + "o.w"), d, d, Md)
-            self._bias(A["g_br"], d, Md, d, self.G(p + "o.b"))
             self._dgrad(A["g_br"], self.W(p + "o.w"), A["g_att"], Md, d, d)
             qkv, gq = A[f"dqkv{l}"], A["g_qkv"]
             ops.attn_bwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"datt{l}"], A["g_att"], A[f"dlse{l}"], A["delta"],
@@ -529,9 +537,8 @@ class TTSEngine:
             x_in, h1 = A[f"ex{l}"], A[f"eh1{l}"]
             ops.layernorm_bwd(gxe, h1, A[f"ef2{l}"], self.P(p + "ln2.g"), A[f"eln2m{l}"], A[f"eln2r{l}"], gres, gbr,
                               self.G(p + "ln2.g"), self.G(p + "ln2.b"), Me, drop=self.drop(base + 2, c.dropout),
-                              ws=self.ws)
+                              ws=self.ws, dbias=self.G(p + "ffn2.b"))
             self._wgrad(gbr, A[f"ef1{l}"], self.G(p + "ffn2.w"), d, F, Me)
-            self._bias(gbr, d, Me, d, self.G(p + "ffn2.b"))
             self._dgrad(gbr, self.W(p + "ffn2.w"), gf1, Me, F, d, gate=A[f"ef1{l}"], gate_scale=gs(c.dropout))
             self._wgrad(gf1, h1, self.G(p + "ffn1.w"), F, d, Me)
             self._bias(gf1, F, Me, F, self.G(p + "ffn1.b"))
@@ -539,9 +546,8 @@ class TTSEngine:
             gxe, gxe2 = gxe2, gxe
             ops.layernorm_bwd(gxe, x_in, A[f"eo{l}"], self.P(p + "ln1.g"), A[f"eln1m{l}"], A[f"eln1r{l}"], gres, gbr,
                               self.G(p + "ln1.g"), self.G(p + "ln1.b"), Me, drop=self.drop(base, c.dropout),
-                              ws=self.ws)
+                              ws=self.ws, dbias=self.G(p + "o.b"))
             self._wgrad(gbr, A[f"eatt{l}"], self.G(p + "o.w"), d, d, Me)
-            self._bias(gbr, d, Me, d, self.G(p + "o.b"))
             self._dgrad(gbr, self.W(p + "o.w"), gatt, Me, d, d)
             qkv = A[f"eqkv{l}"]
             ops.attn_bwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"eatt{l}"], gatt, A[f"else{l}"], A["delta"],

@@ -220,11 +220,14 @@ def layernorm_fwd(x, branch, gamma, beta, y, mean, rstd, m, eps=1e-5, drop: Drop
 
 
 def layernorm_bwd(dy, x, branch, gamma, mean, rstd, dx, dbranch, dgamma, dbeta, m, drop: Drop = NO_DROP,
-                  ws: Workspace | None = None):
+                  ws: Workspace | None = None, dbias=None):
+    """dx = d(LN)/ds, dbranch = drop-masked dx, gamma/beta grads, and optionally
+    dbias = column sums of dbranch (the producing linear layer's bias gradient)."""
     L = lib()
     a = _lib.LnArgs()
     a.dy, a.x, a.branch = dy.data_ptr(), x.data_ptr(), ptr(branch)
     a.dx, a.dbranch = dx.data_ptr(), ptr(dbranch)
+    a.dbias = ptr(dbias)
     a.gamma, a.mean, a.rstd = gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr()
     a.dgamma, a.dbeta = dgamma.data_ptr(), dbeta.data_ptr()
     a.m, a.c, a.dtype = m, x.shape[-1], dt(x)
