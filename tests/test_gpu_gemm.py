@@ -120,3 +120,23 @@ def test_conv_implicit_gemm(dtype, variant, cin, cout):
     (yq * dyr.transpose(1, 2)).sum().backward()
     ref_w = wq.grad.permute(0, 2, 1).reshape(cout, KS * cin)
     assert rel(dw, ref_w) < 1e-5
+
+
+@pytest.mark.parametrize("splits", [1, 4])
+@pytest.mark.parametrize("conv", [False, True])
+def test_wgrad_fused_bias_ksum(splits, conv):
+    """Weight-gradient GEMM with the bias gradient (row sums of A = dY^T over k) fused."""
+    Bsz, T, cin, cout, KS, pad = 3, 150, 64, 200, 5, 2
+    M = Bsz * T
+    g = torch.Generator().manual_seed(11 + splits + conv)
+    dy = torch.randn(M, cout, generator=g).bfloat16().cuda()
+    x = torch.randn(M, cin, generator=g).bfloat16().cuda()
+    kin = KS * cin if conv else cin
+    dw = torch.empty(cout, kin, device="cuda")
+    gb = torch.full((cout,), 3.0, device="cuda")
+    ops.gemm(dy, x, dw, cout, kin, M, cout, cin, kin, trans_a=True, trans_b=True, splits=splits,
+             b_conv=(T, cin, pad) if conv else None, a_ksum=gb, a_ksum_beta=0.5)
+    ref_b = 1.5 + dy.double().sum(0)
+    assert rel(gb, ref_b) < 1e-6
+    if not conv:
+        assert rel(dw, dy.double().t() @ x.double()) < 1e-5

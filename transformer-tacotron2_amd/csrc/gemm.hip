@@ -38,6 +38,7 @@ struct EpiParams {
   DropDesc drop;
   int n_log;  // logical N for dropout index (m * n_log + n)
   int vec;    // every row of C/res/gate/bias is 16-B aligned at 8-column boundaries
+  float* ksum; float ksum_beta;   // fused row sums of op(A) over k (v2, M-contiguous A)
 };
 
 TT2_DEV float ld_any(const void* p, int64_t i, int dt) {
@@ -210,6 +211,14 @@ __global__ __launch_bounds__(NT) void gemm_kernel(OpDesc A, OpDesc B, EpiParams 
 __global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int M, int N) {
   const int64_t total = (int64_t)M * N;
   const uint32_t seed = E.drop.thr ? *E.drop.seed : 0u;
+  if (E.ksum) {   // [splits][M] k-sum partials after the C slabs, fixed split order
+    const float* kp = ws + splits * total;
+    for (int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; m < M; m += (int64_t)gridDim.x * blockDim.x) {
+      float v = 0.f;
+      for (int z = 0; z < splits; ++z) v += kp[z * (int64_t)M + m];
+      E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + v : v;
+    }
+  }
   if ((N & 3) == 0) {
     // 4 consecutive columns per thread (16-B partial-slab loads), fixed split order
     const int64_t t4 = total / 4;
@@ -415,6 +424,8 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
   if (AK) A.inner_max = ke; else A.outer_max = ke;
   if (BKC) B.inner_max = ke; else B.outer_max = ke;
   const int nkt = (ke - kb + BK2 - 1) / BK2;
+  const bool do_ks = !AK && E.ksum && (tile % ntn) == 0;   // one n-tile per m-tile sums A over k
+  float ks[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -454,7 +465,41 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
         for (int j = 0; j < 4; ++j) mma16(fa[i], fb[j], acc[i][j]);
 #endif
     }
+    if (!AK && do_ks) {
+      // rows 4*(tid>>4) .. +3 of the [64 k][128 m] A image, m-chunk tid & 15
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kr = 4 * (tid >> 4) + r;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(sa + kr * 256 + (((tid & 15) ^ mc_swz(kr)) << 4));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ks[j] += (float)v[j];
+      }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (!AK && do_ks) {
+    // reduce over the 16 k-groups: lanes l, l^16, l^32, l^48, then the 4 waves via LDS
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ks[j] += __shfl_xor(ks[j], 16, 64);
+      ks[j] += __shfl_xor(ks[j], 32, 64);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[(wave * 16 + lane) * 8 + j] = ks[j];
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int cc = tid >> 3, j = tid & 7, m = m0 + tid;
+      const float v = (red[(0 * 16 + cc) * 8 + j] + red[(1 * 16 + cc) * 8 + j]) +
+                      (red[(2 * 16 + cc) * 8 + j] + red[(3 * 16 + cc) * 8 + j]);
+      if (m < M) {
+        if (ws) ws[(int64_t)gridDim.y * M * N + (int64_t)blockIdx.y * M + m] = v;
+        else E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + v : v;
+      }
+    }
     __syncthreads();
   }
 #ifdef TT2_ABL_NO_EPI
@@ -815,7 +860,7 @@ hipError_t launch2(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
 
 extern "C" size_t tt2_gemm_workspace_size(const tt2_gemm_args* a) {
   if (a->splits <= 1) return 0;
-  return (size_t)a->splits * a->m * a->n * sizeof(float);
+  return (size_t)a->splits * a->m * (a->n + (a->a_ksum ? 1 : 0)) * sizeof(float);
 }
 
 extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
@@ -850,6 +895,8 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   ep.drop = DropDesc{a->drop_seed, a->drop_site, a->drop_thr, a->drop_scale};
   if (ep.drop.thr && !ep.drop.seed) return tt2_set_error(TT2_E_INVALID, "tt2_gemm: dropout without seed");
   ep.n_log = a->n;
+  ep.ksum = a->a_ksum;
+  ep.ksum_beta = a->a_ksum_beta;
   {
     // vectorised epilogue: rows of C / res / gate start 16-B aligned at every 8th column
     auto ok = [](const void* p, int64_t ld, int dt) {
@@ -877,6 +924,8 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   const bool v2 = a->dtype_in == TT2_BF16 && a->kernel_variant != 1 &&
                   A.inner_max % 8 == 0 && B.inner_max % 8 == 0;
   const int var = a->kernel_variant;
+  if (a->a_ksum && !(v2 && var < 4 && a->trans_a && a->a_conv_t == 0))
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ksum needs bf16, trans_a, no conv A, the LDS-DMA kernel");
   if (v2 && var >= 4) {
     // v3 configurations: 4 = BM128/2 stages, 5 = BM128/3, 6 = BM256/3 (K-contiguous A), 7 = BM128/4
 #define TT2_G3(AK_, BK_)                                                                              \

@@ -38,6 +38,7 @@ class GemmArgs(C.Structure):
         ("a_conv_t", i32), ("a_conv_c", i32), ("a_conv_pad", i32),
         ("b_conv_t", i32), ("b_conv_c", i32), ("b_conv_pad", i32),
         ("kernel_variant", i32),
+        ("a_ksum", vp), ("a_ksum_beta", f32),
     ]
 
 

@@ -260,10 +260,15 @@ class TTSEngine:
         ops.gemm(dy, wflip, out, m, cin, K * cout, cout, K * cout, ldo or cin, a_conv=(T, cout, (K - 1) // 2),
                  beta=beta, ws=self.ws, splits=act_splits(m, cin, K * cout))
 
-    def _wgrad(self, dy, x, gw, n_out, n_in, m, ldy=None, ldx=None, b_conv=None):
-        """gw[n_out, n_in] (f32) = dy[m, n_out]^T @ x[m, n_in]"""
+    def _wgrad(self, dy, x, gw, n_out, n_in, m, ldy=None, ldx=None, b_conv=None, gb=None):
+        """gw[n_out, n_in] (f32) = dy[m, n_out]^T @ x[m, n_in]; gb (optional) = the
+        bias gradient sum_m dy[m, :], fused into the GEMM's A-tile pass for bf16."""
+        # the fused path rides on the LDS-DMA kernel: bf16 with 8-aligned M and N
+        fused = gb is not None and dy.dtype == torch.bfloat16 and n_out % 8 == 0 and n_in % 8 == 0
         ops.gemm(dy, x, gw, n_out, n_in, m, ldy or n_out, ldx or n_in, n_in, trans_a=True, trans_b=True,
-                 splits=auto_splits(n_out, n_in, m), b_conv=b_conv, ws=self.ws)
+                 splits=auto_splits(n_out, n_in, m), b_conv=b_conv, ws=self.ws, a_ksum=gb if fused else None)
+        if gb is not None and not fused:
+            self._bias(dy, ldy or n_out, m, n_out, gb)
 
     def _bias(self, dy, ld, m, n, gb):
         ops.colsum(dy, ld, m, n, gb, ws=self.ws)
@@ -435,8 +440,7 @@ class TTSEngine:
                               drop=self.drop(SITE_POSTNET + i, c.postnet_dropout), ws=self.ws)
             x_in = A[f"pcv_o{i - 1}"] if i > 0 else A["pin"]
             self._wgrad(dyv, x_in, self.G(f"post.conv{i}.w").view(cout, K * cin), cout, K * cin, Md, ldx=cin,
-                        b_conv=(Ty, cin, pad))
-            self._bias(dyv, cout, Md, cout, self.G(f"post.conv{i}.b"))
+                        b_conv=(Ty, cin, pad), gb=self.G(f"post.conv{i}.b"))
             wflip = self._wflip(f"post.conv{i}.w", cout, cin, K)
             if i > 0:
                 gn = scratch[(i + 1) % 2].view(-1)[:Md * cin].view(Md, cin)
@@ -450,8 +454,7 @@ class TTSEngine:
         nh = c.n_mels + 1
         ops.cast2d(A["g_heads"], A.heads_ld, A["gh_cd"], A.heads_ld, Md, nh)
         x_top = A[f"dx{c.n_dec}"]
-        self._wgrad(A["gh_cd"], x_top, self.G("heads.w"), nh, d, Md, ldy=A.heads_ld)
-        self._bias(A["gh_cd"], A.heads_ld, Md, nh, self.G("heads.b"))
+        self._wgrad(A["gh_cd"], x_top, self.G("heads.w"), nh, d, Md, ldy=A.heads_ld, gb=self.G("heads.b"))
         gx, gx2 = A["g_xa"], A["g_xb"]
         self._dgrad(A["gh_cd"], self.W("heads.w"), gx, Md, d, nh, ldy=A.heads_ld)
         self._ready("heads.w")
@@ -470,8 +473,7 @@ class TTSEngine:
             self._wgrad(A["g_br"], A[f"df1{l}"], self.G(p + "ffn2.w"), d, F, Md)
             self._dgrad(A["g_br"], self.W(p + "ffn2.w"), A["g_f1"], Md, F, d, gate=A[f"df1{l}"],
                         gate_scale=gs(c.dropout))
-            self._wgrad(A["g_f1"], h2, self.G(p + "ffn1.w"), F, d, Md)
-            self._bias(A["g_f1"], F, Md, F, self.G(p + "ffn1.b"))
+            self._wgrad(A["g_f1"], h2, self.G(p + "ffn1.w"), F, d, Md, gb=self.G(p + "ffn1.b"))
             self._dgrad(A["g_f1"], self.W(p + "ffn1.w"), gx2, Md, d, F, res=A["g_res"])
             gx, gx2 = gx2, gx
             # LN2 + cross attention
@@ -485,8 +487,7 @@ class TTSEngine:
             ops.attn_bwd(A[f"dcq{l}"], mkv[:, ko:], mkv[:, ko + d:], A[f"dcatt{l}"], A["g_att"], A[f"dclse{l}"],
                          A["delta"], g_cq, g_mkv[:, ko:], g_mkv[:, ko + d:], d, kvld, kvld, d, d, 3 * d, kvld, kvld,
                          B, H, Ty, Tx, A["text_len"], False, scale)
-            self._wgrad(g_cq, h1, self.G(p + "cq.w"), d, d, Md, ldy=3 * d)
-            self._bias(g_cq, 3 * d, Md, d, self.G(p + "cq.b"))
+            self._wgrad(g_cq, h1, self.G(p + "cq.w"), d, d, Md, ldy=3 * d, gb=self.G(p + "cq.b"))
             self._dgrad(g_cq, self.W(p + "cq.w"), gx2, Md, d, d, ldy=3 * d, res=A["g_res"])
             gx, gx2 = gx2, gx
             # LN1 + self attention
@@ -499,8 +500,7 @@ class TTSEngine:
             ops.attn_bwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"datt{l}"], A["g_att"], A[f"dlse{l}"], A["delta"],
                          gq, gq[:, d:], gq[:, 2 * d:], 3 * d, 3 * d, 3 * d, d, d, 3 * d, 3 * d, 3 * d,
                          B, H, Ty, Ty, A["mel_len"], True, scale)
-            self._wgrad(gq, x_in, self.G(p + "qkv.w"), 3 * d, d, Md)
-            self._bias(gq, 3 * d, Md, 3 * d, self.G(p + "qkv.b"))
+            self._wgrad(gq, x_in, self.G(p + "qkv.w"), 3 * d, d, Md, gb=self.G(p + "qkv.b"))
             self._dgrad(gq, self.W(p + "qkv.w"), gx2, Md, d, 3 * d, res=A["g_res"])
             gx, gx2 = gx2, gx
             self._ready(p + "qkv.w")
@@ -508,20 +508,18 @@ class TTSEngine:
         g_proj = A["g_br"]
         ops.posenc_bwd(gx, self.pe, g_proj, self.G("dec.alpha"), Md, Ty, drop=self.drop(SITE_DEC_PE, c.dropout),
                        ws=self.ws)
-        self._wgrad(g_proj, A["dp2"], self.G("dec.proj.w"), d, c.dec_prenet, Md)
-        self._bias(g_proj, d, Md, d, self.G("dec.proj.b"))
+        self._wgrad(g_proj, A["dp2"], self.G("dec.proj.w"), d, c.dec_prenet, Md, gb=self.G("dec.proj.b"))
         self._dgrad(g_proj, self.W("dec.proj.w"), A["g_p2"], Md, c.dec_prenet, d, gate=A["dp2"],
                     gate_scale=gs(c.prenet_dropout))
-        self._wgrad(A["g_p2"], A["dp1"], self.G("dec.fc2.w"), c.dec_prenet, c.dec_prenet, Md)
-        self._bias(A["g_p2"], c.dec_prenet, Md, c.dec_prenet, self.G("dec.fc2.b"))
+        self._wgrad(A["g_p2"], A["dp1"], self.G("dec.fc2.w"), c.dec_prenet, c.dec_prenet, Md,
+                    gb=self.G("dec.fc2.b"))
         self._dgrad(A["g_p2"], self.W("dec.fc2.w"), A["g_p1"], Md, c.dec_prenet, c.dec_prenet, gate=A["dp1"],
                     gate_scale=gs(c.prenet_dropout))
-        self._wgrad(A["g_p1"], A["din"], self.G("dec.fc1.w"), c.dec_prenet, c.n_mels, Md)
-        self._bias(A["g_p1"], c.dec_prenet, Md, c.dec_prenet, self.G("dec.fc1.b"))
+        self._wgrad(A["g_p1"], A["din"], self.G("dec.fc1.w"), c.dec_prenet, c.n_mels, Md,
+                    gb=self.G("dec.fc1.b"))
         # ---------------- memory (all layers' cross K/V)
         mem = A[f"ex{c.n_enc}"]
-        self._wgrad(g_mkv, mem, self.G("dec.kv.w"), kvld, d, Me)
-        self._bias(g_mkv, kvld, Me, kvld, self.G("dec.kv.b"))
+        self._wgrad(g_mkv, mem, self.G("dec.kv.w"), kvld, d, Me, gb=self.G("dec.kv.b"))
         self._ready("dec.fc1.w")
         gxe = A["g_xa"].view(-1)[:Me * d].view(Me, d)
         gxe2 = A["g_xb"].view(-1)[:Me * d].view(Me, d)
@@ -540,8 +538,7 @@ class TTSEngine:
                               ws=self.ws, dbias=self.G(p + "ffn2.b"))
             self._wgrad(gbr, A[f"ef1{l}"], self.G(p + "ffn2.w"), d, F, Me)
             self._dgrad(gbr, self.W(p + "ffn2.w"), gf1, Me, F, d, gate=A[f"ef1{l}"], gate_scale=gs(c.dropout))
-            self._wgrad(gf1, h1, self.G(p + "ffn1.w"), F, d, Me)
-            self._bias(gf1, F, Me, F, self.G(p + "ffn1.b"))
+            self._wgrad(gf1, h1, self.G(p + "ffn1.w"), F, d, Me, gb=self.G(p + "ffn1.b"))
             self._dgrad(gf1, self.W(p + "ffn1.w"), gxe2, Me, d, F, res=gres)
             gxe, gxe2 = gxe2, gxe
             ops.layernorm_bwd(gxe, x_in, A[f"eo{l}"], self.P(p + "ln1.g"), A[f"eln1m{l}"], A[f"eln1r{l}"], gres, gbr,
@@ -553,16 +550,15 @@ class TTSEngine:
             ops.attn_bwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"eatt{l}"], gatt, A[f"else{l}"], A["delta"],
                          gq, gq[:, d:], gq[:, 2 * d:], 3 * d, 3 * d, 3 * d, d, d, 3 * d, 3 * d, 3 * d,
                          B, H, Tx, Tx, A["text_len"], False, scale)
-            self._wgrad(gq, x_in, self.G(p + "qkv.w"), 3 * d, d, Me)
-            self._bias(gq, 3 * d, Me, 3 * d, self.G(p + "qkv.b"))
+            self._wgrad(gq, x_in, self.G(p + "qkv.w"), 3 * d, d, Me, gb=self.G(p + "qkv.b"))
             self._dgrad(gq, self.W(p + "qkv.w"), gxe2, Me, d, 3 * d, res=gres)
             gxe, gxe2 = gxe2, gxe
             self._ready(p + "qkv.w")
         # ---------------- encoder pre-net
         ops.posenc_bwd(gxe, self.pe, gbr, self.G("enc.alpha"), Me, Tx, drop=self.drop(SITE_ENC_PE, c.dropout),
                        ws=self.ws)
-        self._wgrad(gbr, A[f"ecv_o{c.enc_conv_layers - 1}"], self.G("enc.proj.w"), d, d, Me)
-        self._bias(gbr, d, Me, d, self.G("enc.proj.b"))
+        self._wgrad(gbr, A[f"ecv_o{c.enc_conv_layers - 1}"], self.G("enc.proj.w"), d, d, Me,
+                    gb=self.G("enc.proj.b"))
         gc = gxe2
         self._dgrad(gbr, self.W("enc.proj.w"), gc, Me, d, d)
         gdy = gres
@@ -572,8 +568,7 @@ class TTSEngine:
                               ACT_RELU, drop=self.drop(SITE_ENC_CONV + i, c.prenet_dropout), ws=self.ws)
             x_in = A[f"ecv_o{i - 1}"] if i > 0 else A["emb"]
             self._wgrad(gdy, x_in, self.G(f"enc.conv{i}.w").view(d, K * d), d, K * d, Me, ldx=d,
-                        b_conv=(Tx, d, pad))
-            self._bias(gdy, d, Me, d, self.G(f"enc.conv{i}.b"))
+                        b_conv=(Tx, d, pad), gb=self.G(f"enc.conv{i}.b"))
             wflip = self._wflip(f"enc.conv{i}.w", d, d, K)
             self._conv_dgrad(gdy, wflip, gc, Me, d, d, K, Tx)
         ops.embedding_bwd(A["text"], gc, self.G("enc.embed"), Me, c.vocab, pad_idx=0)

@@ -59,8 +59,9 @@ _WS = Workspace()
 
 def gemm(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=None, res=None, ldr=0,
          gate=None, ldg=0, gate_scale=1.0, alpha=1.0, beta=0.0, act=0, drop: Drop = NO_DROP, splits=1,
-         a_conv=None, b_conv=None, ws: Workspace | None = None, variant: int = 0):
-    """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see tt2_capi.h tt2_gemm_args."""
+         a_conv=None, b_conv=None, ws: Workspace | None = None, variant: int = 0, a_ksum=None, a_ksum_beta=0.0):
+    """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see tt2_capi.h tt2_gemm_args.
+    a_ksum (f32 [m], bf16 trans_a only): a_ksum = a_ksum_beta * a_ksum + sum_k A(m,k)."""
     L = lib()
     g = GemmArgs()
     g.a, g.b, g.c = a.data_ptr(), b.data_ptr(), c.data_ptr()
@@ -84,6 +85,7 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=Non
     if b_conv is not None:
         g.b_conv_t, g.b_conv_c, g.b_conv_pad = b_conv
     g.kernel_variant = variant
+    g.a_ksum, g.a_ksum_beta = ptr(a_ksum), a_ksum_beta
     g.splits = max(1, splits)
     if g.splits > 1:
         need = L.tt2_gemm_workspace_size(C.byref(g))
