@@ -22,12 +22,13 @@ def _mk(shape, dtype, gen):
 
 
 VARIANTS = [(torch.float32, 1), (torch.bfloat16, 1), (torch.bfloat16, 2), (torch.bfloat16, 4), (torch.bfloat16, 5),
-            (torch.bfloat16, 6), (torch.bfloat16, 7)]
+            (torch.bfloat16, 6), (torch.bfloat16, 7), (torch.bfloat16, 8)]
 
 
 @pytest.mark.parametrize("dtype,variant", VARIANTS)
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
-@pytest.mark.parametrize("mnk", [(200, 136, 72), (128, 128, 32), (40, 264, 520), (256, 384, 1000), (96, 80, 46)])
+@pytest.mark.parametrize("mnk", [(200, 136, 72), (128, 128, 32), (40, 264, 520), (256, 384, 1000), (96, 80, 46),
+                                 (600, 520, 1000)])
 def test_gemm_layouts(dtype, variant, ta, tb, mnk):
     m, n, k = mnk
     if (ta and m % 8) or (tb and n % 8) or (not ta and k % 8) or (not tb and k % 8):

@@ -280,15 +280,19 @@ typedef __attribute__((address_space(3))) void lvoid_t;
 // swizzle of the 16-B chunk index for an M/N-contiguous tile row k (256-B rows)
 TT2_DEV int mc_swz(int k) { return ((k & 3) << 1) ^ (((k >> 3) & 1) << 3); }
 
+// Per-lane LDS-DMA source: the chunk's address, or the zero page when the chunk is out
+// of range (or reads conv padding).  Branch-free per lane (a select), so the DMA issue
+// is not wrapped in exec-mask branches; the conv test is behind a uniform branch.
 TT2_DEV const void* chunk_src(const OpDesc& d, int outer, int inner) {
-  if (outer >= d.outer_max || inner >= d.inner_max) return g_zero_page;
-  const bf16* base = reinterpret_cast<const bf16*>(d.p);
+  bool ok = (outer < d.outer_max) & (inner < d.inner_max);
+  int64_t off = (int64_t)outer * d.ld + inner;
   if (d.conv_t > 0) {
     const int ts = outer % d.conv_t + inner / d.conv_c - d.conv_pad;
-    if (ts < 0 || ts >= d.conv_t) return g_zero_page;
-    return base + (int64_t)outer * d.ld + inner - (int64_t)d.conv_pad * d.conv_c;
+    ok = ok & (ts >= 0) & (ts < d.conv_t);
+    off -= (int64_t)d.conv_pad * d.conv_c;
   }
-  return base + (int64_t)outer * d.ld + inner;
+  const void* p = reinterpret_cast<const bf16*>(d.p) + off;
+  return ok ? p : (const void*)g_zero_page;
 }
 
 // issue this wave's 4 of the 16 LDS-DMA instructions of one 128 x 64 operand tile
@@ -856,6 +860,193 @@ hipError_t launch2(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   return hipGetLastError();
 }
 
+
+// =====================================================================================
+// v4 (bf16, K-contiguous A): 256 x 256 output tile, 512 threads = 8 waves (2 M x 4 N),
+// each wave 128 x 64 = 8 x 4 MFMA 16x16x32 blocks.  At 64 MFMA FLOP per staged byte
+// x 2 this halves the L2 -> CU bytes per FLOP of the 128^2 tile, which is what bounds
+// the 128^2 kernel (~70 GB/s per CU served from L2).  K runs in 32-deep "k-halves"
+// through a 4-slot LDS ring (slot = A 256x32 + B 256x32 bf16 = 32 KB), filled by
+// LDS-DMA three k-halves ahead of the one being multiplied; per k-half: counted
+// vmcnt for this thread's copies of the current slot, one barrier, re-issue into the
+// slot the previous k-half released, 12 fragment reads, 32 MFMAs.
+// LDS images (swizzle on the per-lane global source, image lane-linear):
+//   K-contiguous operand: [256 rows][4 chunks of 16 B], chunk c of row r at c ^ ((r>>1)&3)
+//   N-contiguous B      : [32 k rows][32 chunks], chunk c of row k at c ^ mc_swz(k)
+// both bank-conflict-free for their ds_read_b128 / ds_read_b64_tr_b16 patterns.
+// =====================================================================================
+constexpr int G4_NT = 512;
+constexpr int G4_OPB = 256 * 32 * 2;               // 16 KB: one operand's k-half
+constexpr int G4_SLOT = 2 * G4_OPB;                // 32 KB
+constexpr int G4_SLOTS = 4;
+constexpr int G4_EPI_LD = 260;                     // f32 words per staged C row
+constexpr int G4_SMEM = (G4_SLOTS * G4_SLOT > 128 * G4_EPI_LD * 4) ? G4_SLOTS * G4_SLOT : 128 * G4_EPI_LD * 4;
+
+// this wave's 2 of the 16 LDS-DMA instructions of one operand k-half
+template <bool KC>
+TT2_DEV void g4_issue(const OpDesc& d, char* lds, int r0, int k0, int lane, int wave) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int inst = wave * 2 + i;
+    const void* src;
+    if (KC) {
+      const int row = inst * 16 + (lane >> 2);
+      const int lc = (lane & 3) ^ ((row >> 1) & 3);
+      src = chunk_src(d, r0 + row, k0 + lc * 8);
+    } else {
+      const int kr = inst * 2 + (lane >> 5);
+      const int lc = (lane & 31) ^ mc_swz(kr);
+      src = chunk_src(d, k0 + kr, r0 + lc * 8);
+    }
+    __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(lds + inst * 1024), 16, 0, 0);
+  }
+}
+
+// 16 x 32 fragment (rows r0 + (lane&15)) of a k-half image
+template <bool KC>
+TT2_DEV bf16x8 g4_frag(const char* img, int r0, int lane) {
+  if (KC) {
+    const int row = r0 + (lane & 15);
+    return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((((lane >> 4) ^ (row >> 1)) & 3) << 4));
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int c = (r0 + 4 * p) >> 3;
+    const int k_lo = 8 * g + q, k_hi = k_lo + 4;
+    typedef __attribute__((address_space(3))) short4v lds_s4;
+    const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s4*)(img + k_lo * 512 + ((c ^ mc_swz(k_lo)) << 4) + ((p & 1) << 3)));
+    const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s4*)(img + k_hi * 512 + ((c ^ mc_swz(k_hi)) << 4) + ((p & 1) << 3)));
+    union { short4v s[2]; bf16x8 v; } u;
+    u.s[0] = lo;
+    u.s[1] = hi;
+    return u.v;
+  }
+}
+
+TT2_DEV void g4_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+template <bool BKC>
+__global__ __launch_bounds__(G4_NT, 1) void gemm4_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
+                                                         int k_split, float* ws, int ntm, int ntn) {
+  __shared__ __attribute__((aligned(1024))) char smem[G4_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nt = ntm * ntn;
+  const int bid = blockIdx.x;
+  const int q8 = nt / 8, rr = nt % 8, x = bid % 8;
+  const int tile = (x < rr ? x * (q8 + 1) : rr * (q8 + 1) + (x - rr) * q8) + bid / 8;
+  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
+  const int kb = blockIdx.y * k_split;
+  const int ke = min(K, kb + k_split);
+  A.inner_max = ke;
+  if (BKC) B.inner_max = ke; else B.outer_max = ke;
+  const int nkh = (ke - kb + 31) / 32;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int h = 0; h < 3; ++h)
+    if (h < nkh) {
+      g4_issue<true>(A, smem + h * G4_SLOT, m0, kb + 32 * h, lane, wave);
+      g4_issue<BKC>(B, smem + h * G4_SLOT + G4_OPB, n0, kb + 32 * h, lane, wave);
+    }
+  for (int h = 0; h < nkh; ++h) {
+    // this thread's copies of k-half h are done when at most the later ones are pending
+    if (h + 2 < nkh) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (h + 1 < nkh) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    g4_barrier();   // everyone's copies of h landed; everyone finished reading k-half h-1
+    if (h + 3 < nkh) {
+      char* s3 = smem + ((h + 3) & 3) * G4_SLOT;
+      g4_issue<true>(A, s3, m0, kb + 32 * (h + 3), lane, wave);
+      g4_issue<BKC>(B, s3 + G4_OPB, n0, kb + 32 * (h + 3), lane, wave);
+    }
+    const char* sa = smem + (h & 3) * G4_SLOT;
+    const char* sb = sa + G4_OPB;
+    bf16x8 fb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = g4_frag<BKC>(sb, wc * 64 + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      Frag8<bf16> fa;
+      fa.v = g4_frag<true>(sa, wr * 128 + 16 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        Frag8<bf16> fbj;
+        fbj.v = fb[j];
+        mma16(fa, fbj, acc[i][j]);
+      }
+    }
+  }
+  g4_barrier();   // all waves done with the ring before it becomes the C staging area
+
+  // C through LDS in two 128-row passes (pass q: the waves with wr == q)
+  float* cs = reinterpret_cast<float*>(smem);
+  const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (wr == q) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            cs[(16 * i + 4 * (lane >> 4) + r) * G4_EPI_LD + wc * 64 + 16 * j + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+      const int id = tid + G4_NT * it;   // 128 rows x 32 chunks of 8
+      const int row = id >> 5, c8 = (id & 31) * 8;
+      const int m = m0 + 128 * q + row, n = n0 + c8;
+      if (m >= M || n >= N) continue;
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + row * G4_EPI_LD + c8);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * G4_EPI_LD + c8 + 4);
+      if (ws) {
+        float* w = ws + ((int64_t)blockIdx.y * M + m) * N + n;
+        if (n + 8 <= N && (N % 4) == 0) {
+          *reinterpret_cast<f32x4*>(w) = lo;
+          *reinterpret_cast<f32x4*>(w + 4) = hi;
+        } else {
+          const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          for (int j = 0; j < 8; ++j)
+            if (n + j < N) w[j] = v[j];
+        }
+      } else {
+        const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        epi_store8(E, seed, m, n, N, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <bool BKC>
+hipError_t launch4(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
+                   hipStream_t s) {
+  int k_split = K;
+  if (splits > 1) {
+    k_split = ((K + splits - 1) / splits + 31) / 32 * 32;
+    splits = (K + k_split - 1) / k_split;
+  }
+  const int ntm = (M + 255) / 256, ntn = (N + 255) / 256;
+  hipLaunchKernelGGL((gemm4_kernel<BKC>), dim3(ntm * ntn, splits), dim3(G4_NT), 0, s, A, B, E, M, N, K, k_split,
+                     splits > 1 ? ws : nullptr, ntm, ntn);
+  if (splits > 1) {
+    const int64_t total = (int64_t)M * N;
+    int64_t nb = (total + 255) / 256;
+    int blocks = (int)(nb < 4096 ? nb : 4096);
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, splits, E, M, N);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" size_t tt2_gemm_workspace_size(const tt2_gemm_args* a) {
@@ -926,6 +1117,15 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   const int var = a->kernel_variant;
   if (a->a_ksum && !(v2 && var < 4 && a->trans_a && a->a_conv_t == 0))
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ksum needs bf16, trans_a, no conv A, the LDS-DMA kernel");
+  // v4: 256^2 tiles (K-contiguous A).  Auto only for GEMMs with a full chip of such
+  // tiles and a long K (4096^3: +20 % over v2); the training step's d_model = 512
+  // shapes measure faster on v2 (more CUs pulling operands), or variant 8 forces it.
+  const bool big = (int64_t)((a->m + 255) / 256) * ((a->n + 255) / 256) >= 256 && a->k >= 1024;
+  if (v2 && !a->trans_a && !a->a_ksum && (var == 8 || (var == 0 && big))) {
+    if (!a->trans_b) err = launch4<true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    else err = launch4<false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    return tt2_check_launch(err, "tt2_gemm(v4)");
+  }
   if (v2 && var >= 4) {
     // v3 configurations: 4 = BM128/2 stages, 5 = BM128/3, 6 = BM256/3 (K-contiguous A), 7 = BM128/4
 #define TT2_G3(AK_, BK_)                                                                              \

@@ -141,20 +141,46 @@ __global__ void pe_fwd_kernel(const T* x, const float* alpha, const float* pe, T
   }
 }
 // dx = drop'(dout); part[block] = sum dx * pe
+// dx = drop(dout) and a per-block partial of dalpha = sum(dx * pe[t]).  8-element
+// chunks (C % 8 == 0): 16-B loads, 32-bit chunk indexing.
 template <typename T>
 __global__ __launch_bounds__(NT) void pe_bwd_kernel(const T* dout, const float* pe, T* dx, float* part, int M, int C,
                                                     int Tlen, DropDesc drop) {
   __shared__ float red[NT / 64];
-  const int64_t total = (int64_t)M * C;
+  const int cpr = C >> 3, nchunk = M * cpr;
   const uint32_t seed = drop.thr ? *drop.seed : 0u;
   float s = 0.f;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
-    const int m = (int)(i / C), c = (int)(i % C);
+  for (int q = blockIdx.x * NT + threadIdx.x; q < nchunk; q += gridDim.x * NT) {
+    const int m = q / cpr, c0 = (q - m * cpr) * 8;
     const int t = m % Tlen;
-    float g = to_f32(dout[i]);
-    if (drop.thr) g = drop_apply(drop, seed, (uint32_t)i, g);
-    dx[i] = from_f32<T>(g);
-    s += g * pe[(int64_t)t * C + c];
+    const int64_t i0 = (int64_t)m * C + c0;
+    float g[8];
+    if constexpr (sizeof(T) == 2) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(dout + i0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = (float)v[j];
+    } else {
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(dout + i0), hi = *reinterpret_cast<const f32x4*>(dout + i0 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { g[j] = lo[j]; g[4 + j] = hi[j]; }
+    }
+    if (drop.thr) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = drop_apply(drop, seed, (uint32_t)(i0 + j), g[j]);
+    }
+    const f32x4 p0 = *reinterpret_cast<const f32x4*>(pe + (int64_t)t * C + c0);
+    const f32x4 p1 = *reinterpret_cast<const f32x4*>(pe + (int64_t)t * C + c0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += g[j] * p0[j] + g[4 + j] * p1[j];
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)g[j];
+      *reinterpret_cast<bf16x8*>(dx + i0) = o;
+    } else {
+      *reinterpret_cast<f32x4*>(dx + i0) = f32x4{g[0], g[1], g[2], g[3]};
+      *reinterpret_cast<f32x4*>(dx + i0 + 4) = f32x4{g[4], g[5], g[6], g[7]};
+    }
   }
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -446,6 +472,8 @@ extern "C" size_t tt2_posenc_bwd_workspace_size(void) { return TT2_PE_BWD_BLOCKS
 extern "C" int tt2_posenc_bwd(const tt2_pe_args* p, hipStream_t s) {
   if (!p->workspace || p->ws_bytes < tt2_posenc_bwd_workspace_size())
     return tt2_set_error(TT2_E_INVALID, "tt2_posenc_bwd: workspace");
+  if (p->c % 8 || (int64_t)p->m * p->c >= (1ll << 31))
+    return tt2_set_error(TT2_E_INVALID, "tt2_posenc_bwd: C must be a multiple of 8 and M*C < 2^31");
   DropDesc d{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
   float* part = reinterpret_cast<float*>(p->workspace);
   if (p->dtype == TT2_DT_BF16)

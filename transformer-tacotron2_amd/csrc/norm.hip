@@ -175,19 +175,30 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
   }
 }
 
-// grid (C / 64, 3): column block x of partial array y; 4 row groups of 64 lanes.
+// grid (C / 16, 3): 16 columns of partial array y per block, 16 row groups of 16
+// lanes; each lane sums nb/16 partial rows with independent loads in flight.
 __global__ __launch_bounds__(256) void ln_bwd_finalize(LnArgs a, int nb) {
-  __shared__ float sm[4][64];
+  __shared__ float sm[16][17];
   const int which = blockIdx.y;
   float* dst = which == 0 ? a.dgamma : (which == 1 ? a.dbeta : a.dbias);
   if (!dst) return;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
-  float acc = 0.f;
-  for (int r = rg; r < nb; r += 4) acc += a.part[((int64_t)r * 3 + which) * a.C + c];
-  sm[rg][threadIdx.x & 63] = acc;
+  const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  const float* src = a.part + (int64_t)which * a.C + c;
+  const int64_t rs = 3 * (int64_t)a.C;   // stride between partial rows
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int r = rg;
+  for (; r + 48 < nb; r += 64) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] += src[(r + 16 * u) * rs];
+  }
+  for (; r < nb; r += 16) acc[0] += src[r * rs];
+  sm[rg][cl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
   if (rg == 0) {
-    const float v = (sm[0][threadIdx.x] + sm[1][threadIdx.x]) + (sm[2][threadIdx.x] + sm[3][threadIdx.x]);
+    float v = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) v += sm[g][cl];
     dst[c] = a.grad_beta != 0.f ? a.grad_beta * dst[c] + v : v;
   }
 }
@@ -397,7 +408,7 @@ extern "C" int tt2_layernorm_bwd(const tt2_ln_args* p, hipStream_t s) {
   const int nb = TT2_LN_BWD_BLOCKS;
   if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(LNB_NT), 0, s, a);
   else hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nb), dim3(LNB_NT), 0, s, a);
-  hipLaunchKernelGGL(ln_bwd_finalize, dim3(p->c / 64, 3), dim3(256), 0, s, a, nb);
+  hipLaunchKernelGGL(ln_bwd_finalize, dim3(p->c / 16, 3), dim3(256), 0, s, a, nb);
   return tt2_check_launch(hipGetLastError(), "tt2_layernorm_bwd");
 }
 
