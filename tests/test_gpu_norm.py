@@ -58,3 +58,47 @@ def test_layernorm_fwd_bwd_dbias(dtype, m, p):
     assert rel(dgamma, ref_g.detach()) < tol_b
     assert rel(dbeta, dy.to(dtype).double().sum(0)) < tol_b
     assert rel(dbias, brr.grad.sum(0)) < tol_b
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("m,c,act,res", [(1000, 512, 1, False), (333, 80, 0, True), (64, 512, 2, False)])
+def test_batchnorm_train_fwd_bwd(dtype, m, c, act, res):
+    """Training-mode BatchNorm1d over rows + act + dropout (+ residual): forward, running
+    statistics and backward vs float64 torch."""
+    g = torch.Generator().manual_seed(m + c + act)
+    y = (torch.randn(m, c, generator=g) * 3 + 1.5)
+    gamma = 1 + 0.1 * torch.randn(c, generator=g)
+    beta = 0.1 * torch.randn(c, generator=g)
+    dout = torch.randn(m, c, generator=g)
+    r = torch.randn(m, 96, generator=g) if res else None
+    p = 0.2
+    seed = torch.tensor([7], dtype=torch.int32).cuda()
+    drop = ops.Drop(seed, 33, p)
+    yd, dd = y.to(dtype).cuda(), dout.to(dtype).cuda()
+    mean = torch.empty(c, device="cuda")
+    rstd = torch.empty(c, device="cuda")
+    rm, rv = torch.zeros(c, device="cuda"), torch.ones(c, device="cuda")
+    out = torch.empty(m, c, dtype=dtype, device="cuda")
+    ops.batchnorm_fwd(yd, gamma.cuda(), beta.cuda(), mean, rstd, rm, rv, out, m, c, act, True, drop=drop,
+                      res=r.cuda() if res else None, res_ld=96)
+    keep = torch.from_numpy(dropout_keep(7, 33, m * c, p)).view(m, c).double()
+    yr = y.to(dtype).double().requires_grad_(True)
+    gr, br = gamma.double().requires_grad_(True), beta.double().requires_grad_(True)
+    z = torch.nn.functional.batch_norm(yr, None, None, gr, br, training=True, eps=1e-5)
+    z = z.relu() if act == 1 else (z.tanh() if act == 2 else z)
+    o = z * keep / (1 - p)
+    if res:
+        o = o + r[:, :c].double()
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel(out, o) < tol
+    yv = y.to(dtype).double()
+    assert rel(rm, 0.1 * yv.mean(0)) < 1e-5
+    assert rel(rv, 0.9 + 0.1 * yv.var(0, unbiased=True)) < 1e-5
+    o.backward(dout.to(dtype).double())
+    dy = torch.empty(m, c, dtype=dtype, device="cuda")
+    dg, db = torch.empty(c, device="cuda"), torch.empty(c, device="cuda")
+    ops.batchnorm_bwd(yd, dd, gamma.cuda(), beta.cuda(), mean, rstd, dy, dg, db, m, c, act, drop=drop)
+    tol_b = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel(dy, yr.grad) < tol_b
+    assert rel(dg, gr.grad) < tol_b
+    assert rel(db, br.grad) < tol_b

@@ -225,24 +225,56 @@ TT2_DEV float act_grad_from_out(int act, float z) {
   return act == ACT_RELU ? (z > 0.f ? 1.f : 0.f) : (act == ACT_TANH ? 1.f - z * z : 1.f);
 }
 
-// grid (ceil(C/256), R): thread = column, chunk = rows [r*rows_per, ...)
-template <typename T>
-__global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
-  const int c = blockIdx.x * NT + threadIdx.x;
-  if (c >= a.C) return;
-  const int r0 = blockIdx.y * a.rows_per, r1 = min(a.M, r0 + a.rows_per);
-  const T* y = reinterpret_cast<const T*>(a.y);
-  float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += to_f32(y[(int64_t)r * a.C + c]);
-  const int n = r1 - r0;
-  const float mu = n > 0 ? s / n : 0.f;
-  float m2 = 0.f;
-  for (int r = r0; r < r1; ++r) { const float d = to_f32(y[(int64_t)r * a.C + c]) - mu; m2 += d * d; }
-  a.part[((int64_t)blockIdx.y * 2 + 0) * a.C + c] = mu;
-  a.part[((int64_t)blockIdx.y * 2 + 1) * a.C + c] = m2;
+// All BatchNorm kernels work on 8-column groups (16-B loads/stores; C % 8 == 0).
+// Statistics: one workgroup per chunk of rows_per rows; CG = C/8 column groups x
+// (256/CG) row lanes.  Chunk moments use a per-column shift (the chunk's first row)
+// so sum / sum-of-squares keep full precision; chunks are Chan-combined in double.
+
+TT2_DEV void ld8v(const void* p, int64_t off, int dt, float (&v)[8]) {
+  if (dt == TT2_BF16) ld8(reinterpret_cast<const bf16*>(p) + off, v);
+  else ld8(reinterpret_cast<const float*>(p) + off, v);
 }
 
-// Chan/Welford combine of per-chunk (mean, M2); 64 columns x 4 chunk groups per block.
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
+  __shared__ float red[2][NT][8];
+  const int CG = a.C >> 3, nrl = NT / CG;
+  const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
+  const int r0 = blockIdx.x * a.rows_per, r1 = min(a.M, r0 + a.rows_per);
+  const T* y = reinterpret_cast<const T*>(a.y);
+  float k[8], s1[8], s2[8];
+  ld8(y + (int64_t)r0 * a.C + cg * 8, k);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  if (rl < nrl) {
+    for (int r = r0 + rl; r < r1; r += nrl) {
+      float v[8];
+      ld8(y + (int64_t)r * a.C + cg * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[j] - k[j];
+        s1[j] += d;
+        s2[j] += d * d;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[0][threadIdx.x][j] = s1[j]; red[1][threadIdx.x][j] = s2[j]; }
+  __syncthreads();
+  if (threadIdx.x < CG) {
+    const float n = (float)(r1 - r0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float S1 = 0.f, S2 = 0.f;
+      for (int l = 0; l < nrl; ++l) { S1 += red[0][l * CG + cg][j]; S2 += red[1][l * CG + cg][j]; }
+      const int c = cg * 8 + j;
+      a.part[((int64_t)blockIdx.x * 2 + 0) * a.C + c] = k[j] + S1 / n;
+      a.part[((int64_t)blockIdx.x * 2 + 1) * a.C + c] = fmaxf(S2 - S1 * S1 / n, 0.f);
+    }
+  }
+}
+
+// Chan/Welford combine of per-chunk (mean, M2)
 TT2_DEV void chan_add(double& n, double& mu, double& m2, double nb, double mb, double m2b) {
   if (nb <= 0) return;
   const double nn = n + nb;
@@ -252,10 +284,11 @@ TT2_DEV void chan_add(double& n, double& mu, double& m2, double nb, double mb, d
   n = nn;
 }
 
+// grid ceil(C/16): 16 columns x 16 chunk groups per block
 __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
-  __shared__ double red[3][4][64];
-  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ double red[3][16][17];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   if (!a.training) {
     if (g == 0 && c < a.C) {
       a.mean[c] = a.run_mean[c];
@@ -265,7 +298,7 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
   }
   double n = 0.0, mu = 0.0, m2 = 0.0;
   if (c < a.C)
-    for (int r = g; r < a.R; r += 4) {
+    for (int r = g; r < a.R; r += 16) {
       const int nb = min(a.rows_per, a.M - r * a.rows_per);
       chan_add(n, mu, m2, nb, a.part[((int64_t)r * 2 + 0) * a.C + c], a.part[((int64_t)r * 2 + 1) * a.C + c]);
     }
@@ -273,7 +306,7 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
   __syncthreads();
   if (g != 0 || c >= a.C) return;
   n = 0.0; mu = 0.0; m2 = 0.0;
-  for (int k = 0; k < 4; ++k) chan_add(n, mu, m2, red[0][k][cl], red[1][k][cl], red[2][k][cl]);
+  for (int k = 0; k < 16; ++k) chan_add(n, mu, m2, red[0][k][cl], red[1][k][cl], red[2][k][cl]);
   const double var = n > 0 ? m2 / n : 0.0;
   a.mean[c] = (float)mu;
   a.rstd[c] = (float)(1.0 / sqrt(var + a.eps));
@@ -284,60 +317,99 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
   }
 }
 
+// per-column constants of 8 consecutive columns
+TT2_DEV void col8(const float* p, int c0, float (&v)[8]) {
+  const f32x4 lo = *reinterpret_cast<const f32x4*>(p + c0), hi = *reinterpret_cast<const f32x4*>(p + c0 + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
-  const int64_t total = (int64_t)a.M * a.C;
+  const int CG = a.C >> 3;
+  const int nq = a.M * CG;
   const T* y = reinterpret_cast<const T*>(a.y);
   const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
-    const int c = (int)(i % a.C);
-    float z = act_f(a.act, (to_f32(y[i]) - a.mean[c]) * a.rstd[c] * a.gamma[c] + a.beta[c]);
-    if (a.drop.thr) z = drop_apply(a.drop, seed, (uint32_t)i, z);
-    if (a.res) {
-      const int64_t ri = (i / a.C) * a.res_ld + c;
-      z += a.res_dt == TT2_BF16 ? (float)reinterpret_cast<const bf16*>(a.res)[ri]
-                                : reinterpret_cast<const float*>(a.res)[ri];
+  for (int q = blockIdx.x * NT + threadIdx.x; q < nq; q += gridDim.x * NT) {
+    const int m = q / CG, c0 = (q - m * CG) * 8;
+    const int64_t i0 = (int64_t)m * a.C + c0;
+    float v[8], mu[8], rs[8], g[8], b[8];
+    ld8(y + i0, v);
+    col8(a.mean, c0, mu); col8(a.rstd, c0, rs); col8(a.gamma, c0, g); col8(a.beta, c0, b);
+    float z[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      z[j] = act_f(a.act, (v[j] - mu[j]) * rs[j] * g[j] + b[j]);
+      if (a.drop.thr) z[j] = drop_apply(a.drop, seed, (uint32_t)(i0 + j), z[j]);
     }
-    if (a.out_dt == TT2_BF16) reinterpret_cast<bf16*>(a.out)[i] = (bf16)z;
-    else reinterpret_cast<float*>(a.out)[i] = z;
+    if (a.res) {
+      float r[8];
+      ld8v(a.res, (int64_t)m * a.res_ld + c0, a.res_dt, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] += r[j];
+    }
+    if (a.out_dt == TT2_BF16) st8(reinterpret_cast<bf16*>(a.out) + i0, z);
+    else st8(reinterpret_cast<float*>(a.out) + i0, z);
   }
 }
 
 // dpre = d(pre-activation BN output): recompute z from y.
-TT2_DEV float bn_dpre(const BnArgs& a, uint32_t seed, int64_t i, int c, float yv, float doutv, float& xh) {
-  xh = (yv - a.mean[c]) * a.rstd[c];
-  const float z = act_f(a.act, xh * a.gamma[c] + a.beta[c]);
-  float g = a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)i, doutv) : doutv;
-  return g * act_grad_from_out(a.act, z);
+TT2_DEV float bn_dpre(const BnArgs& a, uint32_t seed, uint32_t i, float xh, float g, float b, float doutv) {
+  const float z = act_f(a.act, xh * g + b);
+  const float d = a.drop.thr ? drop_apply(a.drop, seed, i, doutv) : doutv;
+  return d * act_grad_from_out(a.act, z);
 }
 
 template <typename T, typename TD>
 __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
-  const int c = blockIdx.x * NT + threadIdx.x;
-  if (c >= a.C) return;
-  const int r0 = blockIdx.y * a.rows_per, r1 = min(a.M, r0 + a.rows_per);
+  __shared__ float red[2][NT][8];
+  const int CG = a.C >> 3, nrl = NT / CG;
+  const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
+  const int c0 = cg * 8;
+  const int r0 = blockIdx.x * a.rows_per, r1 = min(a.M, r0 + a.rows_per);
   const T* y = reinterpret_cast<const T*>(a.y);
   const TD* dout = reinterpret_cast<const TD*>(a.dout);
   const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
-  float s1 = 0.f, s2 = 0.f;
-  for (int r = r0; r < r1; ++r) {
-    const int64_t i = (int64_t)r * a.C + c;
-    float xh;
-    const float dp = bn_dpre(a, seed, i, c, to_f32(y[i]), to_f32(dout[i]), xh);
-    s1 += dp;
-    s2 += dp * xh;
+  float s1[8], s2[8], mu[8], rs[8], g[8], b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  col8(a.mean, c0, mu); col8(a.rstd, c0, rs); col8(a.gamma, c0, g); col8(a.beta, c0, b);
+  if (rl < nrl) {
+    for (int r = r0 + rl; r < r1; r += nrl) {
+      const int64_t i0 = (int64_t)r * a.C + c0;
+      float v[8], d[8];
+      ld8(y + i0, v);
+      ld8(dout + i0, d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (v[j] - mu[j]) * rs[j];
+        const float dp = bn_dpre(a, seed, (uint32_t)(i0 + j), xh, g[j], b[j], d[j]);
+        s1[j] += dp;
+        s2[j] += dp * xh;
+      }
+    }
   }
-  a.part[((int64_t)blockIdx.y * 2 + 0) * a.C + c] = s1;
-  a.part[((int64_t)blockIdx.y * 2 + 1) * a.C + c] = s2;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[0][threadIdx.x][j] = s1[j]; red[1][threadIdx.x][j] = s2[j]; }
+  __syncthreads();
+  if (threadIdx.x < CG) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float S1 = 0.f, S2 = 0.f;
+      for (int l = 0; l < nrl; ++l) { S1 += red[0][l * CG + cg][j]; S2 += red[1][l * CG + cg][j]; }
+      a.part[((int64_t)blockIdx.x * 2 + 0) * a.C + c0 + j] = S1;
+      a.part[((int64_t)blockIdx.x * 2 + 1) * a.C + c0 + j] = S2;
+    }
+  }
 }
 
 __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(BnArgs a) {
-  __shared__ float red[2][4][64];
-  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ float red[2][16][17];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float s1 = 0.f, s2 = 0.f;
   if (c < a.C)
-    for (int r = g; r < a.R; r += 4) {
+    for (int r = g; r < a.R; r += 16) {
       s1 += a.part[((int64_t)r * 2 + 0) * a.C + c];
       s2 += a.part[((int64_t)r * 2 + 1) * a.C + c];
     }
@@ -345,25 +417,35 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(BnArgs a) {
   red[1][g][cl] = s2;
   __syncthreads();
   if (g != 0 || c >= a.C) return;
-  a.dbeta[c] = (red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]);
-  a.dgamma[c] = (red[1][0][cl] + red[1][1][cl]) + (red[1][2][cl] + red[1][3][cl]);
+  float t1 = 0.f, t2 = 0.f;
+  for (int k = 0; k < 16; ++k) { t1 += red[0][k][cl]; t2 += red[1][k][cl]; }
+  a.dbeta[c] = t1;
+  a.dgamma[c] = t2;
 }
 
 template <typename T, typename TD>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
-  const int64_t total = (int64_t)a.M * a.C;
+  const int CG = a.C >> 3;
+  const int nq = a.M * CG;
   const T* y = reinterpret_cast<const T*>(a.y);
   const TD* dout = reinterpret_cast<const TD*>(a.dout);
   const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
   const float invM = 1.f / a.M;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
-    const int c = (int)(i % a.C);
-    float xh;
-    const float dp = bn_dpre(a, seed, i, c, to_f32(y[i]), to_f32(dout[i]), xh);
-    float g;
-    if (a.training) g = a.gamma[c] * a.rstd[c] * (dp - a.dbeta[c] * invM - xh * a.dgamma[c] * invM);
-    else g = a.gamma[c] * a.rstd[c] * dp;
-    reinterpret_cast<T*>(a.dy)[i] = from_f32<T>(g);
+  for (int q = blockIdx.x * NT + threadIdx.x; q < nq; q += gridDim.x * NT) {
+    const int m = q / CG, c0 = (q - m * CG) * 8;
+    const int64_t i0 = (int64_t)m * a.C + c0;
+    float v[8], d[8], mu[8], rs[8], g[8], b[8], db[8], dg[8], o[8];
+    ld8(y + i0, v);
+    ld8(dout + i0, d);
+    col8(a.mean, c0, mu); col8(a.rstd, c0, rs); col8(a.gamma, c0, g); col8(a.beta, c0, b);
+    if (a.training) { col8(a.dbeta, c0, db); col8(a.dgamma, c0, dg); }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (v[j] - mu[j]) * rs[j];
+      const float dp = bn_dpre(a, seed, (uint32_t)(i0 + j), xh, g[j], b[j], d[j]);
+      o[j] = a.training ? g[j] * rs[j] * (dp - db[j] * invM - xh * dg[j] * invM) : g[j] * rs[j] * dp;
+    }
+    st8(reinterpret_cast<T*>(a.dy) + i0, o);
   }
 }
 
@@ -434,19 +516,30 @@ extern "C" size_t tt2_batchnorm_workspace_size(const tt2_bn_args* p) {
   return R * 2 * p->c * sizeof(float);
 }
 
+static int bn_check(const tt2_bn_args* p, const char* what) {
+  auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (p->c % 8 || p->c / 8 > NT) return tt2_set_error(TT2_E_INVALID, what);
+  if (p->res && p->res_ld % 8) return tt2_set_error(TT2_E_INVALID, what);
+  if (!al(p->y) || !al(p->out) || !al(p->res) || !al(p->dout) || !al(p->dy) || !al(p->gamma) || !al(p->beta) ||
+      !al(p->mean) || !al(p->rstd) || !al(p->dgamma) || !al(p->dbeta))
+    return tt2_set_error(TT2_E_INVALID, what);
+  return TT2_OK;
+}
+
 extern "C" int tt2_batchnorm_fwd(const tt2_bn_args* p, hipStream_t s) {
   if (p->m <= 0) return TT2_OK;
   if (p->training && (!p->workspace || p->ws_bytes < tt2_batchnorm_workspace_size(p)))
     return tt2_set_error(TT2_E_INVALID, "tt2_batchnorm_fwd: workspace too small");
+  if (bn_check(p, "tt2_batchnorm_fwd: C % 8, C <= 2048, res_ld % 8 and 16-B aligned buffers required"))
+    return TT2_E_INVALID;
   BnArgs a = bn_args(p);
   const bool bf = p->dtype == TT2_DT_BF16;
   if (p->training) {
-    dim3 g((p->c + NT - 1) / NT, a.R);
-    if (bf) hipLaunchKernelGGL(bn_stats_kernel<bf16>, g, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL(bn_stats_kernel<float>, g, dim3(NT), 0, s, a);
+    if (bf) hipLaunchKernelGGL(bn_stats_kernel<bf16>, dim3(a.R), dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(a.R), dim3(NT), 0, s, a);
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + 63) / 64), dim3(NT), 0, s, a);
-  const int g = grid_for((int64_t)p->m * p->c);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + 15) / 16), dim3(NT), 0, s, a);
+  const int g = grid_for((int64_t)p->m * p->c / 8);
   if (bf) hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(g), dim3(NT), 0, s, a);
   else hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(g), dim3(NT), 0, s, a);
   return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_fwd");
@@ -456,18 +549,18 @@ extern "C" int tt2_batchnorm_bwd(const tt2_bn_args* p, hipStream_t s) {
   if (p->m <= 0) return TT2_OK;
   if (!p->workspace || p->ws_bytes < tt2_batchnorm_workspace_size(p))
     return tt2_set_error(TT2_E_INVALID, "tt2_batchnorm_bwd: workspace too small");
+  if (bn_check(p, "tt2_batchnorm_bwd: C % 8, C <= 2048 and 16-B aligned buffers required")) return TT2_E_INVALID;
   BnArgs a = bn_args(p);
   const bool bf = p->dtype == TT2_DT_BF16;
   const bool dbf = p->dout_dtype == TT2_DT_BF16;
-  dim3 g((p->c + NT - 1) / NT, a.R);
 #define TT2_BN_DISPATCH(KER, grid)                                                              \
   if (bf && dbf) hipLaunchKernelGGL((KER<bf16, bf16>), grid, dim3(NT), 0, s, a);                \
   else if (bf) hipLaunchKernelGGL((KER<bf16, float>), grid, dim3(NT), 0, s, a);                 \
   else if (dbf) hipLaunchKernelGGL((KER<float, bf16>), grid, dim3(NT), 0, s, a);                \
   else hipLaunchKernelGGL((KER<float, float>), grid, dim3(NT), 0, s, a);
-  TT2_BN_DISPATCH(bn_bwd_stats_kernel, g)
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + 63) / 64), dim3(NT), 0, s, a);
-  const int ga = grid_for((int64_t)p->m * p->c);
+  TT2_BN_DISPATCH(bn_bwd_stats_kernel, dim3(a.R))
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + 15) / 16), dim3(NT), 0, s, a);
+  const int ga = grid_for((int64_t)p->m * p->c / 8);
   TT2_BN_DISPATCH(bn_bwd_apply_kernel, dim3(ga))
 #undef TT2_BN_DISPATCH
   return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_bwd");
