@@ -22,7 +22,8 @@ def _mk(shape, dtype, gen):
 
 
 VARIANTS = [(torch.float32, 1), (torch.bfloat16, 1), (torch.bfloat16, 2), (torch.bfloat16, 4), (torch.bfloat16, 5),
-            (torch.bfloat16, 6), (torch.bfloat16, 7), (torch.bfloat16, 8)]
+            (torch.bfloat16, 6), (torch.bfloat16, 7), (torch.bfloat16, 8), (torch.bfloat16, 9),
+            (torch.bfloat16, 10)]
 
 
 @pytest.mark.parametrize("dtype,variant", VARIANTS)

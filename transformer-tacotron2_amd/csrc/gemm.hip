@@ -223,8 +223,19 @@ __global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int
     // 4 consecutive columns per thread (16-B partial-slab loads), fixed split order
     const int64_t t4 = total / 4;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < t4; i += (int64_t)gridDim.x * blockDim.x) {
-      f32x4 v = reinterpret_cast<const f32x4*>(ws)[i];
-      for (int z = 1; z < splits; ++z) v += reinterpret_cast<const f32x4*>(ws + z * total)[i];
+      // two accumulators, 4 slab loads in flight per step (fixed order per element)
+      f32x4 v = reinterpret_cast<const f32x4*>(ws)[i], w = f32x4{0.f, 0.f, 0.f, 0.f};
+      int z = 1;
+      for (; z + 3 < splits; z += 4) {
+        const f32x4 a0 = reinterpret_cast<const f32x4*>(ws + z * total)[i];
+        const f32x4 a1 = reinterpret_cast<const f32x4*>(ws + (z + 1) * total)[i];
+        const f32x4 a2 = reinterpret_cast<const f32x4*>(ws + (z + 2) * total)[i];
+        const f32x4 a3 = reinterpret_cast<const f32x4*>(ws + (z + 3) * total)[i];
+        v += a0 + a2;
+        w += a1 + a3;
+      }
+      for (; z < splits; ++z) v += reinterpret_cast<const f32x4*>(ws + z * total)[i];
+      v += w;
       const int m = (int)(4 * i / N), n = (int)(4 * i % N);
 #pragma unroll
       for (int j = 0; j < 4; ++j) st_any(E.c, (int64_t)m * E.ldc + n + j, E.c_dt, epi_value(E, seed, m, n + j, v[j]));
@@ -463,10 +474,16 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
 #pragma unroll
       for (int i = 0; i < 4; ++i) { asm volatile("" :: "v"(fa[i].v)); asm volatile("" :: "v"(fb[i].v)); }
 #else
+#ifdef TT2_G2_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) mma16(fa[i], fb[j], acc[i][j]);
+#ifdef TT2_G2_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
 #endif
     }
     if (!AK && do_ks) {
@@ -1047,6 +1064,204 @@ hipError_t launch4(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   return hipGetLastError();
 }
 
+
+// =====================================================================================
+// v5 (bf16): the v2 tile (128 x 128, 4 waves of 64 x 64) with BK = 32 and a 3-slot
+// LDS ring (16 KB per slot, two K steps in flight), and the C staging split in two
+// 64-row passes: 48 KB of LDS per workgroup, so three workgroups share a CU (v2: two).
+// More resident workgroups is what hides the per-K-step load latency of this tile
+// (measured: every v2 GEMM of the step runs faster with more workgroups per CU).
+// Images: K-contiguous [128 rows][4 chunks], chunk c of row r at c ^ ((r >> 1) & 3);
+// M/N-contiguous [32 k][16 chunks], chunk c of row k at c ^ mc_swz(k).
+// =====================================================================================
+constexpr int G5_OPB = 128 * 32 * 2;     // 8 KB per operand per slot
+constexpr int G5_SLOT = 2 * G5_OPB;       // 16 KB
+constexpr int G5_EPI = 64 * EPI_LD * 4;   // 33.8 KB of C staging per pass
+template <int SLOTS> struct G5 {
+  static constexpr int SMEM = SLOTS * G5_SLOT > G5_EPI ? SLOTS * G5_SLOT : G5_EPI;
+  static constexpr int WG_PER_CU = SLOTS == 3 ? 3 : 4;
+};
+
+template <bool KC>
+TT2_DEV void g5_issue(const OpDesc& d, char* lds, int r0, int k0, int lane, int wave) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int inst = wave * 2 + i;
+    const void* src;
+    if (KC) {
+      const int row = inst * 16 + (lane >> 2);
+      const int lc = (lane & 3) ^ ((row >> 1) & 3);
+      src = chunk_src(d, r0 + row, k0 + lc * 8);
+    } else {
+      const int kr = inst * 4 + (lane >> 4);
+      const int lc = (lane & 15) ^ mc_swz(kr);
+      src = chunk_src(d, k0 + kr, r0 + lc * 8);
+    }
+    __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(lds + inst * 1024), 16, 0, 0);
+  }
+}
+
+template <bool KC>
+TT2_DEV void g5_frag(Frag8<bf16>& f, const char* img, int r0, int lane) {
+  if (KC) {
+    const int row = r0 + (lane & 15);
+    f.v = *reinterpret_cast<const bf16x8*>(img + row * 64 + ((((lane >> 4) ^ (row >> 1)) & 3) << 4));
+  } else {
+    frag2<false>(f, img, r0, 0, lane);   // 256-B k rows, k 0..31
+  }
+}
+
+template <bool AK, bool BKC, int SLOTS>
+__global__ __launch_bounds__(NT, G5<SLOTS>::WG_PER_CU) void gemm5_kernel(OpDesc A, OpDesc B, EpiParams E, int M,
+                                                                         int N, int K, int k_split, float* ws,
+                                                                         int ntm, int ntn) {
+  __shared__ __attribute__((aligned(1024))) char smem[G5<SLOTS>::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nt = ntm * ntn;
+  const int bid = blockIdx.x;
+  const int q8 = nt / 8, rr = nt % 8, x = bid % 8;
+  const int tile = (x < rr ? x * (q8 + 1) : rr * (q8 + 1) + (x - rr) * q8) + bid / 8;
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+  const int kb = blockIdx.y * k_split;
+  const int ke = min(K, kb + k_split);
+  if (AK) A.inner_max = ke; else A.outer_max = ke;
+  if (BKC) B.inner_max = ke; else B.outer_max = ke;
+  const int nkt = (ke - kb + 31) / 32;
+  const bool do_ks = !AK && E.ksum && (tile % ntn) == 0;
+  float ks[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int t = 0; t < SLOTS - 1; ++t)
+    if (t < nkt) {
+      g5_issue<AK>(A, smem + t * G5_SLOT, m0, kb + 32 * t, lane, wave);
+      g5_issue<BKC>(B, smem + t * G5_SLOT + G5_OPB, n0, kb + 32 * t, lane, wave);
+    }
+  int slot = 0;
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (SLOTS == 3 && kt + 1 < nkt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");   // step kt landed everywhere; step kt-1's slot is free
+    if (kt + SLOTS - 1 < nkt) {
+      const int s2 = slot == 0 ? SLOTS - 1 : slot - 1;
+      g5_issue<AK>(A, smem + s2 * G5_SLOT, m0, kb + 32 * (kt + SLOTS - 1), lane, wave);
+      g5_issue<BKC>(B, smem + s2 * G5_SLOT + G5_OPB, n0, kb + 32 * (kt + SLOTS - 1), lane, wave);
+    }
+    const char* sa = smem + slot * G5_SLOT;
+    const char* sb = sa + G5_OPB;
+    Frag8<bf16> fa[4], fb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g5_frag<AK>(fa[i], sa, wm * 64 + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g5_frag<BKC>(fb[j], sb, wn * 64 + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mma16(fa[i], fb[j], acc[i][j]);
+    if (!AK && do_ks) {
+      // k rows 2*(tid>>4), +1 of the [32 k][128 m] A image, m-chunk tid & 15
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int kr = 2 * (tid >> 4) + r;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(sa + kr * 256 + (((tid & 15) ^ mc_swz(kr)) << 4));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ks[j] += (float)v[j];
+      }
+    }
+    slot = slot == SLOTS - 1 ? 0 : slot + 1;
+  }
+  asm volatile("s_barrier" ::: "memory");   // ring free for the epilogue
+
+  if (!AK && do_ks) {
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ks[j] += __shfl_xor(ks[j], 16, 64);
+      ks[j] += __shfl_xor(ks[j], 32, 64);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[(wave * 16 + lane) * 8 + j] = ks[j];
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int cc = tid >> 3, j = tid & 7, m = m0 + tid;
+      const float v = (red[(0 * 16 + cc) * 8 + j] + red[(1 * 16 + cc) * 8 + j]) +
+                      (red[(2 * 16 + cc) * 8 + j] + red[(3 * 16 + cc) * 8 + j]);
+      if (m < M) {
+        if (ws) ws[(int64_t)gridDim.y * M * N + (int64_t)blockIdx.y * M + m] = v;
+        else E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + v : v;
+      }
+    }
+    __syncthreads();
+  }
+
+  float* cs = reinterpret_cast<float*>(smem);
+  const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (wm == q) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            cs[(16 * i + 4 * (lane >> 4) + r) * EPI_LD + wn * 64 + 16 * j + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int it = 0; it < 4; ++it) {
+      const int id = tid + NT * it;   // 64 rows x 16 chunks of 8
+      const int row = id >> 4, c8 = (id & 15) * 8;
+      const int m = m0 + 64 * q + row, n = n0 + c8;
+      if (m >= M || n >= N) continue;
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + row * EPI_LD + c8);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * EPI_LD + c8 + 4);
+      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if (ws) {
+        float* w = ws + ((int64_t)blockIdx.y * M + m) * N + n;
+        if (n + 8 <= N && (N % 4) == 0) {
+          *reinterpret_cast<f32x4*>(w) = lo;
+          *reinterpret_cast<f32x4*>(w + 4) = hi;
+        } else {
+          for (int j = 0; j < 8; ++j)
+            if (n + j < N) w[j] = v[j];
+        }
+      } else {
+        epi_store8(E, seed, m, n, N, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <bool AK, bool BKC, int SLOTS>
+hipError_t launch5(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
+                   hipStream_t s) {
+  int k_split = K;
+  if (splits > 1) {
+    k_split = ((K + splits - 1) / splits + 31) / 32 * 32;
+    splits = (K + k_split - 1) / k_split;
+  }
+  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm5_kernel<AK, BKC, SLOTS>), dim3(ntm * ntn, splits), dim3(NT), 0, s, A, B, E, M, N, K, k_split,
+                     splits > 1 ? ws : nullptr, ntm, ntn);
+  if (splits > 1) {
+    const int64_t total = (int64_t)M * N;
+    int64_t nb = (total + 255) / 256;
+    int blocks = (int)(nb < 4096 ? nb : 4096);
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, splits, E, M, N);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" size_t tt2_gemm_workspace_size(const tt2_gemm_args* a) {
@@ -1115,7 +1330,7 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   const bool v2 = a->dtype_in == TT2_BF16 && a->kernel_variant != 1 &&
                   A.inner_max % 8 == 0 && B.inner_max % 8 == 0;
   const int var = a->kernel_variant;
-  if (a->a_ksum && !(v2 && var < 4 && a->trans_a && a->a_conv_t == 0))
+  if (a->a_ksum && !(v2 && (var < 4 || var == 9 || var == 10) && a->trans_a && a->a_conv_t == 0))
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ksum needs bf16, trans_a, no conv A, the LDS-DMA kernel");
   // v4: 256^2 tiles (K-contiguous A).  Auto only for GEMMs with a full chip of such
   // tiles and a long K (4096^3: +20 % over v2); the training step's d_model = 512
@@ -1125,6 +1340,21 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
     if (!a->trans_b) err = launch4<true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
     else err = launch4<false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
     return tt2_check_launch(err, "tt2_gemm(v4)");
+  }
+  // auto: the BK=32 / 2-slot / 4-workgroups-per-CU form for activation GEMMs with enough
+  // 128^2 tiles to give every CU four (e.g. 12800 x 2048 x 512: +15 % fwd, +25 % dgrad);
+  // fewer tiles pile four workgroups onto a fraction of the CUs, so those stay on v2
+  const int64_t tiles128 = (int64_t)((a->m + 127) / 128) * ((a->n + 127) / 128);
+  const bool v5auto = var == 0 && !a->trans_a && !a->a_ksum && tiles128 >= 1024 && a->k <= 1024;
+  if (v2 && (var == 9 || var == 10 || v5auto)) {
+#define TT2_G5(S)                                                                                            \
+    if (!a->trans_a && !a->trans_b) err = launch5<true, true, S>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);   \
+    else if (!a->trans_a && a->trans_b) err = launch5<true, false, S>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
+    else if (a->trans_a && !a->trans_b) err = launch5<false, true, S>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
+    else err = launch5<false, false, S>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    if (var == 9) { TT2_G5(3) } else { TT2_G5(2) }   // 10 and auto: 2 slots
+#undef TT2_G5
+    return tt2_check_launch(err, "tt2_gemm(v5)");
   }
   if (v2 && var >= 4) {
     // v3 configurations: 4 = BM128/2 stages, 5 = BM128/3, 6 = BM256/3 (K-contiguous A), 7 = BM128/4

@@ -228,7 +228,7 @@ TT2_DEV float act_grad_from_out(int act, float z) {
 // All BatchNorm kernels work on 8-column groups (16-B loads/stores; C % 8 == 0).
 // Statistics: one workgroup per chunk of rows_per rows; CG = C/8 column groups x
 // (256/CG) row lanes.  Chunk moments use a per-column shift (the chunk's first row)
-// so sum / sum-of-squares keep full precision; chunks are Chan-combined in double.
+// so sum / sum-of-squares keep full precision; chunks are combined exactly in double.
 
 TT2_DEV void ld8v(const void* p, int64_t off, int dt, float (&v)[8]) {
   if (dt == TT2_BF16) ld8(reinterpret_cast<const bf16*>(p) + off, v);
@@ -274,19 +274,12 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
   }
 }
 
-// Chan/Welford combine of per-chunk (mean, M2)
-TT2_DEV void chan_add(double& n, double& mu, double& m2, double nb, double mb, double m2b) {
-  if (nb <= 0) return;
-  const double nn = n + nb;
-  const double d = mb - mu;
-  mu += d * nb / nn;
-  m2 += m2b + d * d * n * nb / nn;
-  n = nn;
-}
-
-// grid ceil(C/16): 16 columns x 16 chunk groups per block
+// grid ceil(C/16): 16 columns x 16 chunk groups per block.  Exact two-pass combine of
+// the chunk moments (no per-chunk division): mean = sum n_c mean_c / n, then
+// M2 = sum M2_c + n_c (mean_c - mean)^2, accumulated in double.
 __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
-  __shared__ double red[3][16][17];
+  __shared__ double red[16][17];
+  __shared__ double smean[16];
   const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   if (!a.training) {
@@ -296,18 +289,35 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
     }
     return;
   }
-  double n = 0.0, mu = 0.0, m2 = 0.0;
-  if (c < a.C)
-    for (int r = g; r < a.R; r += 16) {
-      const int nb = min(a.rows_per, a.M - r * a.rows_per);
-      chan_add(n, mu, m2, nb, a.part[((int64_t)r * 2 + 0) * a.C + c], a.part[((int64_t)r * 2 + 1) * a.C + c]);
-    }
-  red[0][g][cl] = n; red[1][g][cl] = mu; red[2][g][cl] = m2;
+  const bool ok = c < a.C;
+  double acc = 0.0;
+  if (ok)
+    for (int r = g; r < a.R; r += 16)
+      acc += (double)min(a.rows_per, a.M - r * a.rows_per) * a.part[((int64_t)r * 2 + 0) * a.C + c];
+  red[g][cl] = acc;
   __syncthreads();
-  if (g != 0 || c >= a.C) return;
-  n = 0.0; mu = 0.0; m2 = 0.0;
-  for (int k = 0; k < 16; ++k) chan_add(n, mu, m2, red[0][k][cl], red[1][k][cl], red[2][k][cl]);
-  const double var = n > 0 ? m2 / n : 0.0;
+  if (g == 0) {
+    double t = 0.0;
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    smean[cl] = t / a.M;
+  }
+  __syncthreads();
+  const double mu = smean[cl];
+  acc = 0.0;
+  if (ok)
+    for (int r = g; r < a.R; r += 16) {
+      const double nb = min(a.rows_per, a.M - r * a.rows_per);
+      const double d = a.part[((int64_t)r * 2 + 0) * a.C + c] - mu;
+      acc += a.part[((int64_t)r * 2 + 1) * a.C + c] + nb * d * d;
+    }
+  __syncthreads();
+  red[g][cl] = acc;
+  __syncthreads();
+  if (g != 0 || !ok) return;
+  double m2 = 0.0;
+  for (int k = 0; k < 16; ++k) m2 += red[k][cl];
+  const double n = a.M;
+  const double var = m2 / n;
   a.mean[c] = (float)mu;
   a.rstd[c] = (float)(1.0 / sqrt(var + a.eps));
   if (a.run_mean) {
@@ -470,8 +480,10 @@ extern "C" int tt2_layernorm_fwd(const tt2_ln_args* p, hipStream_t s) {
   return tt2_check_launch(hipGetLastError(), "tt2_layernorm_fwd");
 }
 
+static int ln_bwd_blocks(int m) { return min(256, (m + 15) / 16); }
+
 extern "C" size_t tt2_layernorm_bwd_workspace_size(const tt2_ln_args* p) {
-  return (size_t)TT2_LN_BWD_BLOCKS * 3 * p->c * sizeof(float);
+  return (size_t)ln_bwd_blocks(p->m) * 3 * p->c * sizeof(float);
 }
 
 extern "C" int tt2_layernorm_bwd(const tt2_ln_args* p, hipStream_t s) {
@@ -487,11 +499,19 @@ extern "C" int tt2_layernorm_bwd(const tt2_ln_args* p, hipStream_t s) {
   a.M = p->m; a.C = p->c; a.eps = p->eps;
   a.drop = DropDesc{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
   if (p->m == 0) return TT2_OK;
-  const int nb = TT2_LN_BWD_BLOCKS;
+  const int nb = ln_bwd_blocks(p->m);
   if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(LNB_NT), 0, s, a);
   else hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nb), dim3(LNB_NT), 0, s, a);
   hipLaunchKernelGGL(ln_bwd_finalize, dim3(p->c / 16, 3), dim3(256), 0, s, a, nb);
   return tt2_check_launch(hipGetLastError(), "tt2_layernorm_bwd");
+}
+
+// rows per statistics chunk: at most TT2_BN_ROWS_PER_CHUNK, fewer for short inputs
+// so there are >= ~256 chunk workgroups (one per CU) when the rows allow it
+static int bn_rows_per(int m) {
+  int rp = TT2_BN_ROWS_PER_CHUNK;
+  while (rp > 8 && (m + rp - 1) / rp < 256) rp >>= 1;
+  return rp;
 }
 
 static BnArgs bn_args(const tt2_bn_args* p) {
@@ -505,14 +525,15 @@ static BnArgs bn_args(const tt2_bn_args* p) {
   a.res_ld = p->res_ld > 0 ? p->res_ld : p->c;
   a.training = p->training;
   a.eps = p->eps; a.momentum = p->momentum;
-  a.rows_per = TT2_BN_ROWS_PER_CHUNK;
+  a.rows_per = bn_rows_per(p->m);
   a.R = (p->m + a.rows_per - 1) / a.rows_per;
   a.drop = DropDesc{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
   return a;
 }
 
 extern "C" size_t tt2_batchnorm_workspace_size(const tt2_bn_args* p) {
-  const size_t R = (p->m + TT2_BN_ROWS_PER_CHUNK - 1) / TT2_BN_ROWS_PER_CHUNK;
+  const int rp = bn_rows_per(p->m);
+  const size_t R = (p->m + rp - 1) / rp;
   return R * 2 * p->c * sizeof(float);
 }
 
