@@ -72,6 +72,21 @@ typedef struct tt2_gemm_args {
    * A tiles already staged in LDS.  Requires bf16, trans_a, no conv on A. */
   float* a_ksum;
   float a_ksum_beta;
+  /* decode-step fusions, skinny path only (bf16, m <= 32, A and B K-contiguous):
+   * - LayerNorm prologue on A: when a_ln_gamma != NULL the GEMM multiplies
+   *   h = LN(A + a_ln_branch) (row-wise over the k = 512 columns, eps a_ln_eps) instead of A,
+   *   and writes h to a_ln_out [m, k] (ld k);
+   * - KV-cache scatter epilogue: when kv_cache != NULL, output columns n >= kv_col0 are also
+   *   stored to kv_cache[m * kv_bstride + (*kv_t) * kv_ld + (n - kv_col0)] (bf16). */
+  const void* a_ln_branch;
+  const float* a_ln_gamma;
+  const float* a_ln_beta;
+  void* a_ln_out;
+  float a_ln_eps;
+  void* kv_cache;
+  const int32_t* kv_t;
+  int32_t kv_col0;
+  int64_t kv_bstride, kv_ld;
 } tt2_gemm_args;
 
 size_t tt2_gemm_workspace_size(const tt2_gemm_args* a);
@@ -129,7 +144,6 @@ int tt2_decode_emit(const float* heads, int64_t heads_ld, int batch, int n_mels,
 
 /* ------------------------------------------------------------- reductions */
 #define TT2_COLSUM_ROWS 128
-#define TT2_LN_BWD_BLOCKS 256
 #define TT2_BN_ROWS_PER_CHUNK 64
 #define TT2_PE_BWD_BLOCKS 1024
 #define TT2_LOSS_BLOCKS 256

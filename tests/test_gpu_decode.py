@@ -52,6 +52,22 @@ def test_graph_replay_equals_eager():
     assert torch.equal(a1, a2)
 
 
+@pytest.mark.parametrize("fuse", [0, 2])
+def test_decode_fusion_levels_match(fuse):
+    """bf16 decode with the KV scatter (default level 1) vs no fusion / also the fused
+    LayerNorm prologues: same frames within bf16 rounding of the LN output."""
+    _, model, text, tl = setup(torch.bfloat16)
+    T = 10
+    model.eval()
+    ref = Decoder(model.engine, 3, 17, T)
+    ref.fuse = 1
+    out = Decoder(model.engine, 3, 17, T)
+    out.fuse = fuse
+    a, _ = ref.run(text.cuda(), tl.cuda(), T, stop_threshold=None)
+    b, _ = out.run(text.cuda(), tl.cuda(), T, stop_threshold=None)
+    assert rel(b, a) < (1e-6 if fuse == 0 else 2e-2)
+
+
 def test_stop_token_early_exit():
     _, model, text, tl = setup(torch.bfloat16)
     e = model.engine

@@ -1,0 +1,35 @@
+"""Decode throughput A/B (dev tool, GPU): fused vs unfused decode step, cfg3 shape."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "transformer-tacotron2_amd"))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from tt2.config import TTSConfig  # noqa: E402
+from tt2.infer import Decoder  # noqa: E402
+from tt2.model import TransformerTTS  # noqa: E402
+
+torch.manual_seed(0)
+model = TransformerTTS(TTSConfig(), dtype=torch.bfloat16)
+model.eval()
+g = torch.Generator().manual_seed(1)
+text = torch.randint(1, 80, (bench.DEC_B, bench.TX), generator=g).cuda()
+tl = torch.full((bench.DEC_B,), bench.TX, dtype=torch.int32, device="cuda")
+for fuse in (0, 1, 2, 0, 1, 2):
+    dec = Decoder(model.engine, bench.DEC_B, bench.TX, bench.DEC_T)
+    dec.fuse = fuse
+    dec.encode(text, tl)
+    dec.capture()
+    dec.reset()
+    dec.decode_loop(32)
+    torch.cuda.synchronize()
+    dec.reset()
+    t0 = time.perf_counter()
+    dec.decode_loop(400, stop_threshold=None)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(f"fuse={fuse}: {dt / 400 * 1e6:.1f} us/step")

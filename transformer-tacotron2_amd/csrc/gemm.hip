@@ -813,11 +813,55 @@ hipError_t launch3(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
 // =====================================================================================
 constexpr int SK_COLS = 16;
 
+// Decode-step fusions carried by the skinny kernel (tt2_gemm_args a_ln_* / kv_*).
+struct SkinnyFuse {
+  const bf16* br; const float* gamma; const float* beta; bf16* h_out; float eps;   // LN prologue (gamma != 0)
+  bf16* kv; const int32_t* kv_t; int kv_col0; int64_t kv_bstride, kv_ld;           // KV scatter (kv != 0)
+};
+
+constexpr int SK_LN_LD = 512 + 8;   // bf16 per LDS row of the normalised A (16-B pad)
+
 __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t ldx, const bf16* W, int64_t ldw,
-                                                         EpiParams E, int M, int N, int K) {
+                                                         EpiParams E, int M, int N, int K, SkinnyFuse F) {
   __shared__ float red[4][32][SK_COLS + 1];
+  extern __shared__ __attribute__((aligned(16))) bf16 s_h[];   // [32][SK_LN_LD] when F.gamma (K == 512)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * SK_COLS;
+  if (F.gamma) {
+    // h = LN(x + br) for the (<= 32) rows: rows wave, wave + 4, ... with every load issued
+    // before the first reduction; h goes to LDS (the A operand below) and, from one
+    // workgroup, to F.h_out (the next residual)
+    const int c0 = lane * 8;
+    union U { uint4 u; bf16x8 v; } a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int row = min(wave + 4 * u, M - 1);
+      a[u].u = *reinterpret_cast<const uint4*>(X + (int64_t)row * ldx + c0);
+      b[u].u = *reinterpret_cast<const uint4*>(F.br + (int64_t)row * ldx + c0);
+    }
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(F.gamma + c0), g1 = *reinterpret_cast<const f32x4*>(F.gamma + c0 + 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(F.beta + c0), b1 = *reinterpret_cast<const f32x4*>(F.beta + c0 + 4);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int row = wave + 4 * u;
+      if (row >= M) break;
+      float v[8], sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { v[j] = (float)a[u].v[j] + (float)b[u].v[j]; sum += v[j]; }
+      const float mu = wave_sum(sum) / K;
+      float sq = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[j] - mu; sq += d * d; }
+      const float rs = rsqrtf(wave_sum(sq) / K + F.eps);
+      bf16x8 h;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        h[j] = (bf16)((v[j] - mu) * rs * (j < 4 ? g0[j] : g1[j - 4]) + (j < 4 ? b0[j] : b1[j - 4]));
+      *reinterpret_cast<bf16x8*>(s_h + row * SK_LN_LD + c0) = h;
+      if (blockIdx.x == 0) *reinterpret_cast<bf16x8*>(F.h_out + (int64_t)row * K + c0) = h;
+    }
+    __syncthreads();
+  }
   const int kq = ((K + 127) / 128) * 32;                 // per-wave K slice, multiple of 32
   const int kb = wave * kq, ke = min(K, kb + kq);
   const int r = lane & 15, g = lane >> 4;
@@ -833,8 +877,13 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t 
     const bool kok = kk < ke;
     U w, a0, a1;
     w.u = (nok && kok) ? *reinterpret_cast<const uint4*>(wrow + kk) : make_uint4(0, 0, 0, 0);
-    a0.u = (r0ok && kok) ? *reinterpret_cast<const uint4*>(x0 + kk) : make_uint4(0, 0, 0, 0);
-    a1.u = (r1ok && kok) ? *reinterpret_cast<const uint4*>(x1 + kk) : make_uint4(0, 0, 0, 0);
+    if (F.gamma) {
+      a0.u = (r0ok && kok) ? *reinterpret_cast<const uint4*>(s_h + r * SK_LN_LD + kk) : make_uint4(0, 0, 0, 0);
+      a1.u = (r1ok && kok) ? *reinterpret_cast<const uint4*>(s_h + (r + 16) * SK_LN_LD + kk) : make_uint4(0, 0, 0, 0);
+    } else {
+      a0.u = (r0ok && kok) ? *reinterpret_cast<const uint4*>(x0 + kk) : make_uint4(0, 0, 0, 0);
+      a1.u = (r1ok && kok) ? *reinterpret_cast<const uint4*>(x1 + kk) : make_uint4(0, 0, 0, 0);
+    }
     acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0.v, w.v, acc0, 0, 0, 0);
     acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1.v, w.v, acc1, 0, 0, 0);
   }
@@ -851,7 +900,10 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t 
     const int m = row, nn = n0 + col;
     if (m < M && nn < N) {
       const float v = (red[0][row][col] + red[1][row][col]) + (red[2][row][col] + red[3][row][col]);
-      st_any(E.c, (int64_t)m * E.ldc + nn, E.c_dt, epi_value(E, seed, m, nn, v));
+      const float o = epi_value(E, seed, m, nn, v);
+      st_any(E.c, (int64_t)m * E.ldc + nn, E.c_dt, o);
+      if (F.kv && nn >= F.kv_col0)
+        F.kv[(int64_t)m * F.kv_bstride + (int64_t)(*F.kv_t) * F.kv_ld + (nn - F.kv_col0)] = (bf16)o;
     }
   }
 }
@@ -1320,10 +1372,21 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   // skinny-M weight-streaming path (decode step)
   const bool skinny = a->dtype_in == TT2_BF16 && a->m <= 32 && !a->trans_a && !a->trans_b && a->k % 8 == 0 &&
                       a->a_conv_t == 0 && a->splits <= 1 && (a->kernel_variant == 0 || a->kernel_variant == 3);
+  const bool fused = a->a_ln_gamma || a->kv_cache;
+  if (fused && !skinny)
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln / kv fusions need the skinny path (bf16, m <= 32, NT)");
+  if (a->a_ln_gamma && (a->k != 512 || a->lda != a->k || !a->a_ln_branch || !a->a_ln_beta || !a->a_ln_out))
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln needs k == lda == 512, branch, beta and out");
+  if (a->kv_cache && (!a->kv_t || a->dtype_out != TT2_BF16))
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: kv scatter needs kv_t and a bf16 output");
   if (skinny) {
-    hipLaunchKernelGGL(gemm_skinny_kernel, dim3((a->n + SK_COLS - 1) / SK_COLS), dim3(NT), 0, stream,
+    SkinnyFuse F{reinterpret_cast<const bf16*>(a->a_ln_branch), a->a_ln_gamma, a->a_ln_beta,
+                 reinterpret_cast<bf16*>(a->a_ln_out), a->a_ln_eps, reinterpret_cast<bf16*>(a->kv_cache), a->kv_t,
+                 a->kv_col0, a->kv_bstride, a->kv_ld};
+    const size_t lds = a->a_ln_gamma ? 32 * SK_LN_LD * sizeof(bf16) : 0;
+    hipLaunchKernelGGL(gemm_skinny_kernel, dim3((a->n + SK_COLS - 1) / SK_COLS), dim3(NT), lds, stream,
                        reinterpret_cast<const bf16*>(a->a), a->lda, reinterpret_cast<const bf16*>(a->b), a->ldb, ep,
-                       a->m, a->n, a->k);
+                       a->m, a->n, a->k, F);
     return tt2_check_launch(hipGetLastError(), "tt2_gemm(skinny)");
   }
   // v2 (LDS-DMA) path: bf16, every chunk either fully inside or fully outside its row

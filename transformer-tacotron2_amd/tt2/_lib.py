@@ -39,6 +39,8 @@ class GemmArgs(C.Structure):
         ("b_conv_t", i32), ("b_conv_c", i32), ("b_conv_pad", i32),
         ("kernel_variant", i32),
         ("a_ksum", vp), ("a_ksum_beta", f32),
+        ("a_ln_branch", vp), ("a_ln_gamma", vp), ("a_ln_beta", vp), ("a_ln_out", vp), ("a_ln_eps", f32),
+        ("kv_cache", vp), ("kv_t", vp), ("kv_col0", i32), ("kv_bstride", i64), ("kv_ld", i64),
     ]
 
 

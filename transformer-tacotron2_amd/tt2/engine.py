@@ -50,7 +50,7 @@ def act_splits(m: int, n: int, k: int) -> int:
     the 256 CUs (the encoder's 2048-token GEMMs); the epilogue then runs in the
     split-K reduce."""
     tiles = ((m + 127) // 128) * ((n + 127) // 128)
-    if tiles >= 192 or k < 1024:
+    if tiles >= 192 or k < 1024 or m <= 32:   # m <= 32: the decode step's skinny weight-streaming GEMM
         return 1
     return max(1, min(8, 512 // tiles, k // 512))
 
@@ -244,9 +244,9 @@ class TTSEngine:
 
     # ------------------------------------------------------------ GEMM helpers
     def _lin(self, x, w, out, m, n, k, bias=None, act=ACT_NONE, drop=NO_DROP, res=None, ldx=None, ldo=None,
-             a_conv=None, beta=0.0):
+             a_conv=None, beta=0.0, **fuse):
         ops.gemm(x, w, out, m, n, k, ldx or k, k, ldo or n, bias=bias, res=res, ldr=ldo or n, act=act, drop=drop,
-                 a_conv=a_conv, beta=beta, ws=self.ws, splits=act_splits(m, n, k))
+                 a_conv=a_conv, beta=beta, ws=self.ws, splits=act_splits(m, n, k), **fuse)
 
     def _dgrad(self, dy, w, out, m, n_in, n_out, res=None, gate=None, gate_scale=1.0, ldy=None, ldo=None,
                a_conv=None, beta=0.0):

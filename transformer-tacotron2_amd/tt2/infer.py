@@ -55,6 +55,10 @@ class Decoder:
         self.t = torch.zeros(1, dtype=torch.int32, device=dev)
         self.seed = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graph = None
+        # bf16 decode-step fusions in the skinny GEMM: 0 none, 1 KV-cache scatter in the
+        # QKV epilogue, 2 also the LayerNorms as GEMM prologues (measured slower: every
+        # workgroup recomputes the 32-row statistics on its critical path)
+        self.fuse = 1
 
     # ----------------------------------------------------------------- one step
     def step(self):
@@ -73,14 +77,67 @@ class Decoder:
             drop=d2)
         lin(self.p2, e.W("dec.proj.w"), self.proj, B, d, c.dec_prenet, bias=e.P("dec.proj.b"))
         ops.posenc_fwd(self.proj, e.P("dec.alpha"), e.pe, self.x0, B, 1, t_ptr=self.t)
+        mkv = A["mkv"]
+        kvld = c.n_dec * 2 * d
+        eps = c.ln_eps
+        # Each post-LN is fused into the GEMM that consumes it (the skinny kernel
+        # normalises its A rows and publishes the LN output for the residual path), and
+        # the K/V columns of the QKV projection go straight into the KV cache: 8 kernels
+        # per layer instead of 12.
+        if e.cd != torch.bfloat16 or self.fuse < 2:
+            return self._step_layers_unfused(lin, B, d, F, H, scale, kv_fused=e.cd == torch.bfloat16 and self.fuse == 1)
+        x, ln_prev = self.x0, None          # ln_prev: (branch, gamma, beta, out) pending on x
+        xs = (self.xa, self.xb)
+        for l in range(c.n_dec):
+            p = f"dec{l}."
+            cache = self.cache[l]
+            kv = (cache, self.t, d, self.Tmax * 2 * d, 2 * d)
+            if ln_prev is None:
+                lin(x, e.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"), kv=kv)
+            else:
+                lin(x, e.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"), kv=kv, a_ln=ln_prev + (eps,))
+                x = ln_prev[3]
+            ops.attn_decode(self.qkv, cache, cache[:, :, d:], self.att, 3 * d, self.Tmax * 2 * d, 2 * d,
+                            self.Tmax * 2 * d, 2 * d, d, B, H, self.Tmax, t_ptr=self.t, scale=scale)
+            lin(self.att, e.W(p + "o.w"), self.o, B, d, d, bias=e.P(p + "o.b"))
+            # h1 = LN1(x + o), fused into the cross-attention query projection
+            lin(x, e.W(p + "cq.w"), self.cq, B, d, d, bias=e.P(p + "cq.b"),
+                a_ln=(self.o, e.P(p + "ln1.g"), e.P(p + "ln1.b"), self.h1, eps))
+            ko = 2 * d * l
+            ops.attn_decode(self.cq, mkv[:, ko:], mkv[:, ko + d:], self.catt, d, self.Tx * kvld, kvld,
+                            self.Tx * kvld, kvld, d, B, H, self.Tx, key_len=A["text_len"], scale=scale)
+            lin(self.catt, e.W(p + "co.w"), self.co, B, d, d, bias=e.P(p + "co.b"))
+            # h2 = LN2(h1 + co), fused into FFN1
+            lin(self.h1, e.W(p + "ffn1.w"), self.f1, B, F, d, bias=e.P(p + "ffn1.b"), act=ACT_RELU,
+                a_ln=(self.co, e.P(p + "ln2.g"), e.P(p + "ln2.b"), self.h2, eps))
+            lin(self.f1, e.W(p + "ffn2.w"), self.f2, B, d, F, bias=e.P(p + "ffn2.b"))
+            # LN3(h2 + f2) is fused into the next consumer (next layer's QKV, or the heads)
+            x, ln_prev = self.h2, (self.f2, e.P(p + "ln3.g"), e.P(p + "ln3.b"), xs[l % 2])
+        lin(x, e.W("heads.w"), self.heads, B, c.n_mels + 1, d, bias=e.P("heads.b"), ldo=96,
+            a_ln=ln_prev + (eps,))
+        self._emit()
+
+    def _emit(self):
+        c = self.e.cfg
+        ops.decode_emit(self.heads, 96, self.B, c.n_mels, self.Tmax, self.mel_seq, self.stop_seq, self.prev, self.t,
+                        self.seed)
+
+    def _step_layers_unfused(self, lin, B, d, F, H, scale, kv_fused=False):
+        """Decoder layers + heads with separate LayerNorm kernels; the K/V append is a
+        separate kernel too unless kv_fused (bf16 skinny-GEMM epilogue scatter)."""
+        e, c, A = self.e, self.e.cfg, self.A
         x, xn = self.x0, self.xa
         mkv = A["mkv"]
         kvld = c.n_dec * 2 * d
         for l in range(c.n_dec):
             p = f"dec{l}."
-            lin(x, e.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"))
             cache = self.cache[l]
-            ops.kv_append(self.qkv[:, d:], 3 * d, cache, self.Tmax * 2 * d, 2 * d, 2 * d, B, self.t)
+            if kv_fused:
+                lin(x, e.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"),
+                    kv=(cache, self.t, d, self.Tmax * 2 * d, 2 * d))
+            else:
+                lin(x, e.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"))
+                ops.kv_append(self.qkv[:, d:], 3 * d, cache, self.Tmax * 2 * d, 2 * d, 2 * d, B, self.t)
             ops.attn_decode(self.qkv, cache, cache[:, :, d:], self.att, 3 * d, self.Tmax * 2 * d, 2 * d,
                             self.Tmax * 2 * d, 2 * d, d, B, H, self.Tmax, t_ptr=self.t, scale=scale)
             lin(self.att, e.W(p + "o.w"), self.o, B, d, d, bias=e.P(p + "o.b"))
@@ -96,8 +153,7 @@ class Decoder:
             ops.layernorm_fwd(self.h2, self.f2, e.P(p + "ln3.g"), e.P(p + "ln3.b"), xn, None, None, B, c.ln_eps)
             x, xn = xn, (self.xb if xn is self.xa else self.xa)
         lin(x, e.W("heads.w"), self.heads, B, c.n_mels + 1, d, bias=e.P("heads.b"), ldo=96)
-        ops.decode_emit(self.heads, 96, B, c.n_mels, self.Tmax, self.mel_seq, self.stop_seq, self.prev, self.t,
-                        self.seed)
+        self._emit()
 
     # ----------------------------------------------------------------- driver
     def reset(self):

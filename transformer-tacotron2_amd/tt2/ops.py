@@ -59,9 +59,12 @@ _WS = Workspace()
 
 def gemm(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=None, res=None, ldr=0,
          gate=None, ldg=0, gate_scale=1.0, alpha=1.0, beta=0.0, act=0, drop: Drop = NO_DROP, splits=1,
-         a_conv=None, b_conv=None, ws: Workspace | None = None, variant: int = 0, a_ksum=None, a_ksum_beta=0.0):
+         a_conv=None, b_conv=None, ws: Workspace | None = None, variant: int = 0, a_ksum=None, a_ksum_beta=0.0,
+         a_ln=None, kv=None):
     """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see tt2_capi.h tt2_gemm_args.
-    a_ksum (f32 [m], bf16 trans_a only): a_ksum = a_ksum_beta * a_ksum + sum_k A(m,k)."""
+    a_ksum (f32 [m], bf16 trans_a only): a_ksum = a_ksum_beta * a_ksum + sum_k A(m,k).
+    a_ln = (branch, gamma, beta, out, eps): multiply LN(A + branch), writing it to out (skinny path).
+    kv = (cache, t_ptr, col0, bstride, ld): also store columns >= col0 to the KV cache at step *t_ptr."""
     L = lib()
     g = GemmArgs()
     g.a, g.b, g.c = a.data_ptr(), b.data_ptr(), c.data_ptr()
@@ -86,6 +89,12 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=Non
         g.b_conv_t, g.b_conv_c, g.b_conv_pad = b_conv
     g.kernel_variant = variant
     g.a_ksum, g.a_ksum_beta = ptr(a_ksum), a_ksum_beta
+    if a_ln is not None:
+        br, gam, bet, out, eps = a_ln
+        g.a_ln_branch, g.a_ln_gamma, g.a_ln_beta, g.a_ln_out, g.a_ln_eps = ptr(br), ptr(gam), ptr(bet), ptr(out), eps
+    if kv is not None:
+        cache, t_ptr, col0, bstride, ld = kv
+        g.kv_cache, g.kv_t, g.kv_col0, g.kv_bstride, g.kv_ld = ptr(cache), ptr(t_ptr), col0, bstride, ld
     g.splits = max(1, splits)
     if g.splits > 1:
         need = L.tt2_gemm_workspace_size(C.byref(g))
