@@ -21,6 +21,8 @@
 // attn_bwd_prep.
 #include <math.h>
 
+#include <type_traits>
+
 #include "tt2_capi.h"
 #include "tt2_internal.h"
 #include "tt2_common.h"
@@ -623,15 +625,17 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
     r2s3<NTH>(rv, sV[0], tid);
   }
   __syncthreads();
-  for (int t = 0; t < ntile; ++t) {
+  // one 64-key tile; BUF is compile-time so every LDS address is lane base + immediate
+  auto tile = [&](auto BUFC, int t) {
+    constexpr int BUF = decltype(BUFC)::value;
     const int k0 = 64 * t;
     const bool more = t + 1 < ntile;
     if (more) {
       g2r3<NTH>(rk, K, ABL_ROW(k0 + 64), tid);
       g2r3<NTH>(rv, V, ABL_ROW(k0 + 64), tid);
     }
-    const bf16* cK = sK[t & 1];
-    const bf16* cV = sV[t & 1];
+    const bf16* cK = sK[BUF];
+    const bf16* cV = sV[BUF];
     if (!(a.causal && k0 > qw + 31)) {   // wave-uniform: some key of the tile is visible
       f32x16 s[2];
 #pragma unroll
@@ -682,10 +686,14 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
           for (int db = 0; db < 2; ++db) mma32(trfrag(cV, 32 * kb + 16 * hh, db, lane), pf[kb][hh], o[db]);
     }
     if (more) {
-      r2s3<NTH>(rk, sK[(t + 1) & 1], tid);
-      r2s3<NTH>(rv, sV[(t + 1) & 1], tid);
+      r2s3<NTH>(rk, sK[BUF ^ 1], tid);
+      r2s3<NTH>(rv, sV[BUF ^ 1], tid);
     }
     ABL_SYNC();
+  };
+  for (int t = 0; t < ntile; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntile) tile(std::integral_constant<int, 1>{}, t + 1);
   }
   const float l = xor32_sum(l_r);
   if (qv < a.Tq) {
@@ -736,15 +744,16 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
     r2s3<NTH>(rv, sV[0], tid);
   }
   __syncthreads();
-  for (int t = 0; t < ntile; ++t) {
+  auto tile = [&](auto BUFC, int t) {
+    constexpr int BUF = decltype(BUFC)::value;
     const int k0 = 64 * t;
     const bool more = t + 1 < ntile;
     if (more) {
       g2r3<NTH>(rk, K, ABL_ROW(k0 + 64), tid);
       g2r3<NTH>(rv, V, ABL_ROW(k0 + 64), tid);
     }
-    const bf16* cK = sK[t & 1];
-    const bf16* cV = sV[t & 1];
+    const bf16* cK = sK[BUF];
+    const bf16* cV = sV[BUF];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       const int kb0 = k0 + 32 * kb;
@@ -757,25 +766,31 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
         mma32(rowfrag(cK, 32 * kb + ql, 2 * st + hi), fq[st], s);
         mma32(rowfrag(cV, 32 * kb + ql, 2 * st + hi), fdo[st], dp);
       }
-      const bool edge = kb0 + 32 > klim || (a.causal && kb0 + 31 > qw);
-      const int lim = edge ? (a.causal ? min(klim - 1, qv) : klim - 1) - kb0 - 4 * hi : 64;
+      float p[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p[r] = fast_exp2(fmaf(s[r], c, -lse));
+      if (kb0 + 32 > klim || (a.causal && kb0 + 31 > qw)) {   // wave-uniform: mask edge tiles only
+        const int lim = (a.causal ? min(klim - 1, qv) : klim - 1) - kb0 - 4 * hi;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) p[r] = crow(r, 0) > lim ? 0.f : p[r];
+      }
       bf16x8 dsf[2];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float p = fast_exp2(fmaf(s[r], c, -lse));
-        p = crow(r, 0) > lim ? 0.f : p;
-        dsf[r >> 3][r & 7] = (bf16)(p * (dp[r] - dl));
-      }
+      for (int r = 0; r < 16; ++r) dsf[r >> 3][r & 7] = (bf16)(p[r] * (dp[r] - dl));
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
         for (int db = 0; db < 2; ++db) mma32(trfrag(cK, 32 * kb + 16 * hh, db, lane), dsf[hh], dq[db]);
     }
     if (more) {
-      r2s3<NTH>(rk, sK[(t + 1) & 1], tid);
-      r2s3<NTH>(rv, sV[(t + 1) & 1], tid);
+      r2s3<NTH>(rk, sK[BUF ^ 1], tid);
+      r2s3<NTH>(rv, sV[BUF ^ 1], tid);
     }
     ABL_SYNC();
+  };
+  for (int t = 0; t < ntile; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntile) tile(std::integral_constant<int, 1>{}, t + 1);
   }
   if (qok) store_rowT(dQ + (int64_t)qv * a.dq_ld, dq, a.scale, hi);
 }
@@ -831,17 +846,18 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
     stats(0, qstart);
   }
   __syncthreads();
-  for (int t = 0; t < ntile; ++t) {
+  auto tile = [&](auto BUFC, int t) {
+    constexpr int BUF = decltype(BUFC)::value;
     const int q0 = qstart + 64 * t;
     const bool more = t + 1 < ntile;
     if (more) {
       g2r3<NTH>(rq, Q, ABL_ROW(q0 + 64), tid);
       g2r3<NTH>(rd, dO, ABL_ROW(q0 + 64), tid);
     }
-    const bf16* cQ = sQ[t & 1];
-    const bf16* cD = sdO[t & 1];
-    const float* cL = sL[t & 1];
-    const float* cDl = sDl[t & 1];
+    const bf16* cQ = sQ[BUF];
+    const bf16* cD = sdO[BUF];
+    const float* cL = sL[BUF];
+    const float* cDl = sDl[BUF];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
       const int qb0 = q0 + 32 * qb;
@@ -854,9 +870,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
         mma32(rowfrag(cQ, 32 * qb + kl, 2 * st + hi), fk[st], s);
         mma32(rowfrag(cD, 32 * qb + kl, 2 * st + hi), fv[st], dp);
       }
-      // masked: query q < kv (causal) or every query when kv >= klim
-      const int qlo = (kv >= klim ? 1 << 20 : (a.causal ? kv - qb0 : -1)) - 4 * hi;   // visible iff crow >= qlo
-      bf16x8 pf[2], dsf[2];
+      float p[16], dl[16];
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int qi = 32 * qb + 8 * rr + 4 * hi;
@@ -864,12 +878,21 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
         const f32x4 Dl = *reinterpret_cast<const f32x4*>(cDl + qi);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int r = 4 * rr + i;
-          float p = fast_exp2(fmaf(s[r], c, -L[i]));
-          p = crow(r, 0) < qlo ? 0.f : p;
-          pf[r >> 3][r & 7] = (bf16)p;
-          dsf[r >> 3][r & 7] = (bf16)(p * (dp[r] - Dl[i]));
+          p[4 * rr + i] = fast_exp2(fmaf(s[4 * rr + i], c, -L[i]));
+          dl[4 * rr + i] = Dl[i];
         }
+      }
+      if (kw + 32 > klim || (a.causal && qb0 < kw + 31)) {   // wave-uniform: mask edge tiles only
+        // masked: query q < kv (causal) or every query when kv >= klim
+        const int qlo = (kv >= klim ? 1 << 20 : (a.causal ? kv - qb0 : -1)) - 4 * hi;   // visible iff crow >= qlo
+#pragma unroll
+        for (int r = 0; r < 16; ++r) p[r] = crow(r, 0) < qlo ? 0.f : p[r];
+      }
+      bf16x8 pf[2], dsf[2];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        pf[r >> 3][r & 7] = (bf16)p[r];
+        dsf[r >> 3][r & 7] = (bf16)(p[r] * (dp[r] - dl[r]));
       }
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
@@ -880,11 +903,15 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
         }
     }
     if (more) {
-      r2s3<NTH>(rq, sQ[(t + 1) & 1], tid);
-      r2s3<NTH>(rd, sdO[(t + 1) & 1], tid);
-      stats((t + 1) & 1, q0 + 64);
+      r2s3<NTH>(rq, sQ[BUF ^ 1], tid);
+      r2s3<NTH>(rd, sdO[BUF ^ 1], tid);
+      stats(BUF ^ 1, q0 + 64);
     }
     ABL_SYNC();
+  };
+  for (int t = 0; t < ntile; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntile) tile(std::integral_constant<int, 1>{}, t + 1);
   }
   if (kv < a.Tk) {
     store_rowT(dK + (int64_t)kv * a.dk_ld, dk, a.scale, hi);
@@ -925,10 +952,10 @@ int v3_waves(const tt2_attn_args* p, int rows, bool fwd) {
   if (p->variant == 2) return 2;
   if (p->variant == 3) return 4;
   // auto: the forward shares each K/V tile across 4 waves (128 queries) while that
-  // still gives two workgroups per CU; the backward kernels (more registers, 2 waves
-  // per SIMD) measure faster with 2-wave workgroups at every shape of the workload.
+  // still gives two workgroups per CU; the backward kernels (buffer-unrolled loops)
+  // measure fastest with 4-wave workgroups at every shape of the workload.
   const int64_t wg4 = (int64_t)((rows + 127) / 128) * p->batch * p->heads;
-  return fwd && wg4 >= 512 ? 4 : 2;
+  return !fwd || wg4 >= 512 ? 4 : 2;
 }
 
 extern "C" int tt2_attn_fwd(const tt2_attn_args* p, hipStream_t s) {

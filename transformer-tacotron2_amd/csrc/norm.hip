@@ -14,6 +14,7 @@
 //   z = act((y - mean) * rstd * gamma + beta); out = drop(z) (+ res)
 // The backward recomputes z from y (saved) and the statistics.
 #include <math.h>
+#include <stdlib.h>
 
 #include "tt2_capi.h"
 #include "tt2_internal.h"
@@ -90,72 +91,101 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(LnArgs a) {
   if (lane == 0 && a.mean) { a.mean[row] = mean; a.rstd[row] = rstd; }
 }
 
-// Backward: 8 waves per workgroup, one 512-wide row per wave and two rows in
-// flight (both rows' x / branch / dy loads issued before either is reduced), so
-// the ~1-row-per-wave latency chain of a plain loop is halved.  Per-workgroup
-// (dgamma, dbeta, dbias) column partials go to part[block][3][C]; ln_bwd_finalize
-// sums them (fixed order: bitwise reproducible).
+// Backward: 8 waves per workgroup, one 512-wide row per wave at a time, software-
+// pipelined: the raw x / branch / dy chunks of the wave's next row are loaded before the
+// current row is reduced, so every wave always has a row of loads in flight.  The
+// dropout keep-mask of an element is hashed once and used for both s = x + drop(br)
+// and dbranch = drop(ds).  Per-workgroup (dgamma, dbeta, dbias) column partials go to
+// part[block][3][C]; ln_bwd_finalize sums them (fixed order: bitwise reproducible).
 constexpr int LNB_NT = 512;
+template <typename T> struct LnRow { uint4 x[sizeof(T) / 2], dy[sizeof(T) / 2], br[sizeof(T) / 2]; float mean, rstd; };
+
+template <typename T>
+TT2_DEV void ln_row_load(LnRow<T>& r, const LnArgs& a, int row, int c0) {
+  constexpr int NV = sizeof(T) / 2;   // 16-B vectors per 8 elements
+  const int64_t off = (int64_t)row * a.C + c0;
+  const uint4* X = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.x) + off);
+  const uint4* DY = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.dy) + off);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) { r.x[v] = X[v]; r.dy[v] = DY[v]; }
+  if (a.branch) {
+    const uint4* BR = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.branch) + off);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) r.br[v] = BR[v];
+  }
+  r.mean = a.mean[row];
+  r.rstd = a.rstd[row];
+}
+
+template <typename T> TT2_DEV void unpack8(const uint4 (&u)[sizeof(T) / 2], float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    union { uint4 q; bf16x8 b; } c;
+    c.q = u[0];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)c.b[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = __uint_as_float((&u[0].x)[j]); v[4 + j] = __uint_as_float((&u[1].x)[j]); }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
   __shared__ float red[3][4][512];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c0 = lane * 8;
   float g[8];
+  {
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(a.gamma + c0), g1 = *reinterpret_cast<const f32x4*>(a.gamma + c0 + 4);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) g[j] = a.gamma[c0 + j];
+    for (int j = 0; j < 4; ++j) { g[j] = g0[j]; g[4 + j] = g1[j]; }
+  }
   float pg[8], pb[8], pd[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) pg[j] = pb[j] = pd[j] = 0.f;
   const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
-  const T* X = reinterpret_cast<const T*>(a.x);
-  const T* BR = reinterpret_cast<const T*>(a.branch);
-  const T* DY = reinterpret_cast<const T*>(a.dy);
   const int stride = gridDim.x * 8;
-  for (int r0 = blockIdx.x * 8 + w; r0 < a.M; r0 += 2 * stride) {
-    const int rows[2] = {r0, r0 + stride};
-    float s[2][8], dy[2][8], br[2][8], mean[2], rstd[2];
+  int row = blockIdx.x * 8 + w;
+  LnRow<T> cur, nxt;
+  if (row < a.M) ln_row_load<T>(cur, a, row, c0);
+  for (; row < a.M; row += stride) {
+    if (row + stride < a.M) ln_row_load<T>(nxt, a, row + stride, c0);
+    const int64_t off = (int64_t)row * a.C + c0;
+    float s[8], dy[8], keep[8];
+    unpack8<T>(cur.x, s);
+    unpack8<T>(cur.dy, dy);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int row = rows[u] < a.M ? rows[u] : r0;   // duplicate row: loaded, never stored
-      const int64_t off = (int64_t)row * a.C + c0;
-      ld8(X + off, s[u]);
-      ld8(DY + off, dy[u]);
-      if (BR) ld8(BR + off, br[u]);
-      mean[u] = a.mean[row];
-      rstd[u] = a.rstd[row];
+    for (int j = 0; j < 8; ++j)
+      keep[j] = a.drop.thr ? (drop_hash(seed, a.drop.site, (uint32_t)(off + j)) >= a.drop.thr ? a.drop.scale : 0.f)
+                           : 1.f;
+    if (a.branch) {
+      float br[8];
+      unpack8<T>(cur.br, br);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += br[j] * keep[j];
     }
+    float c1 = 0.f, c2 = 0.f, xh[8], gd[8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (rows[u] >= a.M) break;
-      const int64_t off = (int64_t)rows[u] * a.C + c0;
-      if (BR) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          s[u][j] += a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)(off + j), br[u][j]) : br[u][j];
-      }
-      float c1 = 0.f, c2 = 0.f, xh[8], gd[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        xh[j] = (s[u][j] - mean[u]) * rstd[u];
-        gd[j] = g[j] * dy[u][j];
-        c1 += gd[j];
-        c2 += gd[j] * xh[j];
-        pg[j] += dy[u][j] * xh[j];
-        pb[j] += dy[u][j];
-      }
-      c1 = wave_sum(c1) / a.C;
-      c2 = wave_sum(c2) / a.C;
-      float ds[8], db[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        ds[j] = rstd[u] * (gd[j] - c1 - xh[j] * c2);
-        db[j] = a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)(off + j), ds[j]) : ds[j];
-        pd[j] += db[j];
-      }
-      st8(reinterpret_cast<T*>(a.dx) + off, ds);
-      if (a.dbranch) st8(reinterpret_cast<T*>(a.dbranch) + off, db);
+    for (int j = 0; j < 8; ++j) {
+      xh[j] = (s[j] - cur.mean) * cur.rstd;
+      gd[j] = g[j] * dy[j];
+      c1 += gd[j];
+      c2 += gd[j] * xh[j];
+      pg[j] += dy[j] * xh[j];
+      pb[j] += dy[j];
     }
+    c1 = wave_sum(c1) / a.C;
+    c2 = wave_sum(c2) / a.C;
+    float ds[8], db[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ds[j] = cur.rstd * (gd[j] - c1 - xh[j] * c2);
+      db[j] = ds[j] * keep[j];
+      pd[j] += db[j];
+    }
+    st8(reinterpret_cast<T*>(a.dx) + off, ds);
+    if (a.dbranch) st8(reinterpret_cast<T*>(a.dbranch) + off, db);
+    cur = nxt;
   }
   // 8 waves -> 4 rows of LDS partials -> 1
   if (w >= 4) {
@@ -480,7 +510,10 @@ extern "C" int tt2_layernorm_fwd(const tt2_ln_args* p, hipStream_t s) {
   return tt2_check_launch(hipGetLastError(), "tt2_layernorm_fwd");
 }
 
-static int ln_bwd_blocks(int m) { return min(256, (m + 15) / 16); }
+static int ln_bwd_blocks(int m) {
+  static const int cap = getenv("TT2_LNB_CAP") ? atoi(getenv("TT2_LNB_CAP")) : 256;   // dev A/B knob
+  return min(cap, (m + 15) / 16);
+}
 
 extern "C" size_t tt2_layernorm_bwd_workspace_size(const tt2_ln_args* p) {
   return (size_t)ln_bwd_blocks(p->m) * 3 * p->c * sizeof(float);

@@ -113,10 +113,21 @@ TT2_DEV float drop_apply(const DropDesc& d, uint32_t seed, uint32_t idx, float v
 }
 
 // ---------------------------------------------------------------- reductions
+// Full-wave sum without LDS: DPP within 16-lane rows (quad xor 1, quad xor 2,
+// half-row mirror, row mirror), then v_permlane16_swap / v_permlane32_swap across
+// rows.  Every lane ends with the total (same value in all lanes).
+template <int CTRL> TT2_DEV float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 TT2_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f32<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f32<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f32<0x141>(v);   // row_half_mirror
+  v += dpp_f32<0x140>(v);   // row_mirror
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 TT2_DEV float wave_max(float v) {
 #pragma unroll
