@@ -123,6 +123,21 @@ def decode_bench(model, reps: int = 3):
                          "note": "whole-run algorithmic bytes / wall time (launch-bound: ~80 kernels per step)"}}
 
 
+def gemm_kernel_name(plan: int, ta: int, tb: int) -> str:
+    """rocprofv3's (demangled) name of the kernel tt2_gemm_plan selected."""
+    t = lambda b: "true" if b else "false"  # noqa: E731
+    ak, bk = t(not ta), t(not tb)
+    if plan == 2:
+        return f"gemm2_kernel<{ak}, {bk}>"
+    if plan in (9, 10):
+        return f"gemm5_kernel<{ak}, {bk}, {3 if plan == 9 else 2}>"
+    if plan == 8:
+        return f"gemm4_kernel<{bk}>"
+    if plan == 3:
+        return "gemm_skinny_kernel"
+    return f"gemm plan {plan}"
+
+
 def roofline(model, text, tl, mel, ml):
     """Live per-launch timing of the dominant kernel family in one eager step."""
     from tt2 import ops
@@ -138,18 +153,16 @@ def roofline(model, text, tl, mel, ml):
     tot_t = sum(v[2] for v in summ.values())
     tot_f = sum(v[1] for v in summ.values())
     achieved = flops / secs / 1e12
-    names = {(1, 0, 0): "gemm2_kernel<true, true> (bf16 forward linear/conv: A, B K-contiguous)",
-             (1, 0, 1): "gemm2_kernel<true, false> (bf16 dgrad)",
-             (1, 1, 1): "gemm2_kernel<false, false> (bf16 wgrad)"}
+    kname = gemm_kernel_name(*key[1:4])
     traffic, tsrc = None, None
     prof = os.path.join(ROOT, "profiles")
     tfiles = sorted(f for f in os.listdir(prof) if f.endswith("_traffic.json")) if os.path.isdir(prof) else []
     if tfiles:
         t = json.load(open(os.path.join(prof, tfiles[-1])))
-        if t.get("kernel", "") in names.get(key[1:4], ""):
+        if t.get("kernel", "") == kname:
             traffic, tsrc = round(t["hbm_bytes_per_launch"]), "profiles/" + tfiles[-1]
     return {
-        "kernel": names.get(key[1:4], str(key)) + (" +split-K reduce" if key[4] else ""),
+        "kernel": kname,
         "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_source": tsrc,
         "algo_bytes_per_launch": round(abytes / n), "launches_per_step": n, "flops_per_launch": flops / n,

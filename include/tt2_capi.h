@@ -87,10 +87,17 @@ typedef struct tt2_gemm_args {
   const int32_t* kv_t;
   int32_t kv_col0;
   int64_t kv_bstride, kv_ld;
+  /* measurement hook: with splits > 1, launch only the main kernel (partials stay in
+   * the workspace, C is not written), so a per-kernel timing excludes the reduce */
+  int32_t main_only;
 } tt2_gemm_args;
 
 size_t tt2_gemm_workspace_size(const tt2_gemm_args* a);
 int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream);
+/* Kernel tt2_gemm would launch for these args (no device work): 1 register-staged
+ * 128x128 (any dtype), 2 LDS-DMA 128x128 (bf16), 3 skinny decode (m <= 32),
+ * 4-7 deeper LDS pipelines, 8 256x256, 9/10 BK=32 LDS ring; -1 invalid. */
+int tt2_gemm_plan(const tt2_gemm_args* a);
 
 /* ---------------------------------------------------------------- attention
  * Scaled dot-product attention over heads of width 64, read in place from

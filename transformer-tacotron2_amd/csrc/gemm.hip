@@ -39,6 +39,7 @@ struct EpiParams {
   int n_log;  // logical N for dropout index (m * n_log + n)
   int vec;    // every row of C/res/gate/bias is 16-B aligned at 8-column boundaries
   float* ksum; float ksum_beta;   // fused row sums of op(A) over k (v2, M-contiguous A)
+  int main_only;                  // split-K: skip the reduce launch (measurement hook)
 };
 
 TT2_DEV float ld_any(const void* p, int64_t i, int dt) {
@@ -261,7 +262,7 @@ hipError_t launch_t(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M,
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, splits);
   hipLaunchKernelGGL((gemm_kernel<T, AK, BKC>), grid, dim3(NT), 0, s, A, B, E, M, N, K, k_split,
                      splits > 1 ? ws : nullptr);
-  if (splits > 1) {
+  if (splits > 1 && !E.main_only) {
     const int64_t total = (int64_t)M * N;
     int64_t nb = (total + 255) / 256; int blocks = (int)(nb < 4096 ? nb : 4096);
     hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, splits, E, M, N);
@@ -796,7 +797,7 @@ hipError_t launch3(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   dim3 grid(ntm * ntn, splits);
   hipLaunchKernelGGL((gemm3_kernel<AK, BKC, BM_, STAGES>), grid, dim3(G::THREADS), G::SMEM, s, A, B, E, M, N, K,
                      k_split, splits > 1 ? ws : nullptr, ntm, ntn);
-  if (splits > 1) {
+  if (splits > 1 && !E.main_only) {
     const int64_t total = (int64_t)M * N;
     int64_t nb = (total + 255) / 256;
     int blocks = (int)(nb < 4096 ? nb : 4096);
@@ -920,7 +921,7 @@ hipError_t launch2(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   dim3 grid(ntm * ntn, splits);
   hipLaunchKernelGGL((gemm2_kernel<AK, BKC>), grid, dim3(NT), 0, s, A, B, E, M, N, K, k_split,
                      splits > 1 ? ws : nullptr, ntm, ntn);
-  if (splits > 1) {
+  if (splits > 1 && !E.main_only) {
     const int64_t total = (int64_t)M * N;
     int64_t nb = (total + 255) / 256;
     int blocks = (int)(nb < 4096 ? nb : 4096);
@@ -1107,7 +1108,7 @@ hipError_t launch4(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   const int ntm = (M + 255) / 256, ntn = (N + 255) / 256;
   hipLaunchKernelGGL((gemm4_kernel<BKC>), dim3(ntm * ntn, splits), dim3(G4_NT), 0, s, A, B, E, M, N, K, k_split,
                      splits > 1 ? ws : nullptr, ntm, ntn);
-  if (splits > 1) {
+  if (splits > 1 && !E.main_only) {
     const int64_t total = (int64_t)M * N;
     int64_t nb = (total + 255) / 256;
     int blocks = (int)(nb < 4096 ? nb : 4096);
@@ -1305,7 +1306,7 @@ hipError_t launch5(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
   hipLaunchKernelGGL((gemm5_kernel<AK, BKC, SLOTS>), dim3(ntm * ntn, splits), dim3(NT), 0, s, A, B, E, M, N, K, k_split,
                      splits > 1 ? ws : nullptr, ntm, ntn);
-  if (splits > 1) {
+  if (splits > 1 && !E.main_only) {
     const int64_t total = (int64_t)M * N;
     int64_t nb = (total + 255) / 256;
     int blocks = (int)(nb < 4096 ? nb : 4096);
@@ -1320,6 +1321,43 @@ extern "C" size_t tt2_gemm_workspace_size(const tt2_gemm_args* a) {
   if (a->splits <= 1) return 0;
   return (size_t)a->splits * a->m * (a->n + (a->a_ksum ? 1 : 0)) * sizeof(float);
 }
+
+// Kernel selection (also exported as tt2_gemm_plan): 1 v1 register-staged, 2 v2
+// LDS-DMA 128^2, 3 skinny (M <= 32), 4-7 v3 pipelines, 8 v4 256^2, 9/10 v5 BK=32 ring
+// (3 / 2 slots).  Returns -1 (error set) for an unsupported fusion request.
+static int gemm_plan(const tt2_gemm_args* a) {
+  const int var = a->kernel_variant;
+  const int64_t a_inner = a->trans_a ? a->m : a->k, b_inner = a->trans_b ? a->n : a->k;
+  const bool skinny = a->dtype_in == TT2_BF16 && a->m <= 32 && !a->trans_a && !a->trans_b && a->k % 8 == 0 &&
+                      a->a_conv_t == 0 && a->splits <= 1 && (var == 0 || var == 3);
+  if ((a->a_ln_gamma || a->kv_cache) && !skinny)
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln / kv fusions need the skinny path (bf16, m <= 32, NT)"), -1;
+  if (a->a_ln_gamma && (a->k != 512 || a->lda != a->k || !a->a_ln_branch || !a->a_ln_beta || !a->a_ln_out))
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln needs k == lda == 512, branch, beta and out"), -1;
+  if (a->kv_cache && (!a->kv_t || a->dtype_out != TT2_BF16))
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: kv scatter needs kv_t and a bf16 output"), -1;
+  if (skinny) return 3;
+  // LDS-DMA kernels: bf16, every 16-B chunk either fully inside or fully outside its row
+  const bool v2 = a->dtype_in == TT2_BF16 && var != 1 && a_inner % 8 == 0 && b_inner % 8 == 0;
+  if (a->a_ksum && !(v2 && (var < 4 || var == 9 || var == 10) && a->trans_a && a->a_conv_t == 0))
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ksum needs bf16, trans_a, no conv A, the LDS-DMA kernel"), -1;
+  if (!v2) return 1;
+  // v4: 256^2 tiles (K-contiguous A).  Auto only for GEMMs with a full chip of such
+  // tiles and a long K (4096^3: +20 % over v2); the training step's d_model = 512
+  // shapes measure faster on v2 (more CUs pulling operands), or variant 8 forces it.
+  const bool big = (int64_t)((a->m + 255) / 256) * ((a->n + 255) / 256) >= 256 && a->k >= 1024;
+  if (!a->trans_a && !a->a_ksum && (var == 8 || (var == 0 && big))) return 8;
+  // v5 auto: the BK=32 / 2-slot / 4-workgroups-per-CU form for activation GEMMs with
+  // enough 128^2 tiles to give every CU four (e.g. 12800 x 2048 x 512: +15 % fwd, +25 %
+  // dgrad); fewer tiles pile four workgroups onto a fraction of the CUs: those stay on v2
+  const int64_t tiles128 = (int64_t)((a->m + 127) / 128) * ((a->n + 127) / 128);
+  if (var == 9) return 9;
+  if (var == 10 || (var == 0 && !a->trans_a && !a->a_ksum && tiles128 >= 1024 && a->k <= 1024)) return 10;
+  if (var >= 4 && var <= 7) return var;
+  return 2;
+}
+
+extern "C" int tt2_gemm_plan(const tt2_gemm_args* a) { return gemm_plan(a); }
 
 extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   if (a->m <= 0 || a->n <= 0) return TT2_OK;
@@ -1355,6 +1393,7 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   ep.n_log = a->n;
   ep.ksum = a->a_ksum;
   ep.ksum_beta = a->a_ksum_beta;
+  ep.main_only = a->main_only;
   {
     // vectorised epilogue: rows of C / res / gate start 16-B aligned at every 8th column
     auto ok = [](const void* p, int64_t ld, int dt) {
@@ -1369,17 +1408,9 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   const int sp = a->splits > 1 ? a->splits : 1;
 
   hipError_t err;
-  // skinny-M weight-streaming path (decode step)
-  const bool skinny = a->dtype_in == TT2_BF16 && a->m <= 32 && !a->trans_a && !a->trans_b && a->k % 8 == 0 &&
-                      a->a_conv_t == 0 && a->splits <= 1 && (a->kernel_variant == 0 || a->kernel_variant == 3);
-  const bool fused = a->a_ln_gamma || a->kv_cache;
-  if (fused && !skinny)
-    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln / kv fusions need the skinny path (bf16, m <= 32, NT)");
-  if (a->a_ln_gamma && (a->k != 512 || a->lda != a->k || !a->a_ln_branch || !a->a_ln_beta || !a->a_ln_out))
-    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln needs k == lda == 512, branch, beta and out");
-  if (a->kv_cache && (!a->kv_t || a->dtype_out != TT2_BF16))
-    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: kv scatter needs kv_t and a bf16 output");
-  if (skinny) {
+  const int plan = gemm_plan(a);
+  if (plan < 0) return TT2_E_INVALID;   // message already set
+  if (plan == 3) {   // skinny-M weight-streaming path (decode step)
     SkinnyFuse F{reinterpret_cast<const bf16*>(a->a_ln_branch), a->a_ln_gamma, a->a_ln_beta,
                  reinterpret_cast<bf16*>(a->a_ln_out), a->a_ln_eps, reinterpret_cast<bf16*>(a->kv_cache), a->kv_t,
                  a->kv_col0, a->kv_bstride, a->kv_ld};
@@ -1389,38 +1420,24 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
                        a->m, a->n, a->k, F);
     return tt2_check_launch(hipGetLastError(), "tt2_gemm(skinny)");
   }
-  // v2 (LDS-DMA) path: bf16, every chunk either fully inside or fully outside its row
-  const bool v2 = a->dtype_in == TT2_BF16 && a->kernel_variant != 1 &&
-                  A.inner_max % 8 == 0 && B.inner_max % 8 == 0;
-  const int var = a->kernel_variant;
-  if (a->a_ksum && !(v2 && (var < 4 || var == 9 || var == 10) && a->trans_a && a->a_conv_t == 0))
-    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ksum needs bf16, trans_a, no conv A, the LDS-DMA kernel");
-  // v4: 256^2 tiles (K-contiguous A).  Auto only for GEMMs with a full chip of such
-  // tiles and a long K (4096^3: +20 % over v2); the training step's d_model = 512
-  // shapes measure faster on v2 (more CUs pulling operands), or variant 8 forces it.
-  const bool big = (int64_t)((a->m + 255) / 256) * ((a->n + 255) / 256) >= 256 && a->k >= 1024;
-  if (v2 && !a->trans_a && !a->a_ksum && (var == 8 || (var == 0 && big))) {
+  if (plan == 8) {
     if (!a->trans_b) err = launch4<true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
     else err = launch4<false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
     return tt2_check_launch(err, "tt2_gemm(v4)");
   }
-  // auto: the BK=32 / 2-slot / 4-workgroups-per-CU form for activation GEMMs with enough
-  // 128^2 tiles to give every CU four (e.g. 12800 x 2048 x 512: +15 % fwd, +25 % dgrad);
-  // fewer tiles pile four workgroups onto a fraction of the CUs, so those stay on v2
-  const int64_t tiles128 = (int64_t)((a->m + 127) / 128) * ((a->n + 127) / 128);
-  const bool v5auto = var == 0 && !a->trans_a && !a->a_ksum && tiles128 >= 1024 && a->k <= 1024;
-  if (v2 && (var == 9 || var == 10 || v5auto)) {
+  if (plan == 9 || plan == 10) {
 #define TT2_G5(S)                                                                                            \
     if (!a->trans_a && !a->trans_b) err = launch5<true, true, S>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);   \
     else if (!a->trans_a && a->trans_b) err = launch5<true, false, S>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
     else if (a->trans_a && !a->trans_b) err = launch5<false, true, S>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
     else err = launch5<false, false, S>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
-    if (var == 9) { TT2_G5(3) } else { TT2_G5(2) }   // 10 and auto: 2 slots
+    if (plan == 9) { TT2_G5(3) } else { TT2_G5(2) }
 #undef TT2_G5
     return tt2_check_launch(err, "tt2_gemm(v5)");
   }
-  if (v2 && var >= 4) {
+  if (plan >= 4 && plan <= 7) {
     // v3 configurations: 4 = BM128/2 stages, 5 = BM128/3, 6 = BM256/3 (K-contiguous A), 7 = BM128/4
+    const int var = plan;
 #define TT2_G3(AK_, BK_)                                                                              \
     if (var == 6 && AK_) err = launch3<AK_, BK_, 256, 3>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
     else if (var == 5 || var == 6) err = launch3<AK_, BK_, 128, 3>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
@@ -1433,7 +1450,7 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
 #undef TT2_G3
     return tt2_check_launch(err, "tt2_gemm(v3)");
   }
-  if (v2) {
+  if (plan == 2) {
     if (!a->trans_a && !a->trans_b) err = launch2<true, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
     else if (!a->trans_a && a->trans_b) err = launch2<true, false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
     else if (a->trans_a && !a->trans_b) err = launch2<false, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);

@@ -41,6 +41,7 @@ class GemmArgs(C.Structure):
         ("a_ksum", vp), ("a_ksum_beta", f32),
         ("a_ln_branch", vp), ("a_ln_gamma", vp), ("a_ln_beta", vp), ("a_ln_out", vp), ("a_ln_eps", f32),
         ("kv_cache", vp), ("kv_t", vp), ("kv_col0", i32), ("kv_bstride", i64), ("kv_ld", i64),
+        ("main_only", i32),
     ]
 
 
@@ -51,6 +52,7 @@ SIGNATURES: dict[str, tuple[list, object]] = {
     "tt2_init": ([C.c_int], C.c_int),
     "tt2_gemm_workspace_size": ([C.POINTER(GemmArgs)], sz),
     "tt2_gemm": ([C.POINTER(GemmArgs), vp], C.c_int),
+    "tt2_gemm_plan": ([C.POINTER(GemmArgs)], C.c_int),
 }
 
 _lib = None

@@ -101,7 +101,7 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=Non
         buf = (ws or _WS).get(need)
         g.workspace, g.ws_bytes = buf.data_ptr(), buf.numel()
     if PROBE is not None:
-        key = ("gemm", g.dtype_in, int(trans_a), int(trans_b), g.splits > 1)
+        key = ("gemm", L.tt2_gemm_plan(C.byref(g)), int(trans_a), int(trans_b))
         esz = 2 if g.dtype_in == _lib.DT_BF16 else 4
         algo_bytes = esz * (m * k + n * k) + (2 if g.dtype_out == _lib.DT_BF16 else 4) * m * n
         PROBE.begin()
@@ -154,6 +154,7 @@ class LaunchProbe:
             if k != key or saved is None:
                 continue
             torch.cuda.synchronize()
+            saved.main_only = 1      # the kernel alone (a split-K reduce is a different kernel)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(reps):
