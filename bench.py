@@ -135,6 +135,10 @@ def gemm_kernel_name(plan: int, ta: int, tb: int) -> str:
         return f"gemm4_kernel<{bk}>"
     if plan == 3:
         return "gemm_skinny_kernel"
+    if plan == 13:
+        return f"gemm7_kernel<{ak}, {bk}>"
+    if plan in (11, 12):
+        return f"gemm6_kernel<{ak}, {bk}, {256 if plan == 11 else 128}>"
     return f"gemm plan {plan}"
 
 

@@ -66,7 +66,9 @@ typedef struct tt2_gemm_args {
   float drop_scale;
   int32_t a_conv_t, a_conv_c, a_conv_pad;
   int32_t b_conv_t, b_conv_c, b_conv_pad;
-  int32_t kernel_variant;  /* 0 auto, 1 register-staged (any shape), 2 LDS-DMA (bf16, 8-aligned inner dims) */
+  int32_t kernel_variant;  /* 0 auto, 1 register-staged (any shape), 2 LDS-DMA 128x128 (bf16, 8-aligned inner
+                              dims), 11 / 12 LDS-DMA 256x256 / 256x128 (same, no conv operands), 13 warp-
+                              specialised 256x128 (same, conv C, T >= 64; the auto choice when eligible) */
   /* optional fused row sums of op(A) over k: a_ksum[m] = a_ksum_beta * a_ksum[m] + sum_k A(m, k)
    * (f32).  With A = dY^T of a weight-gradient GEMM this is the bias gradient, taken from the
    * A tiles already staged in LDS.  Requires bf16, trans_a, no conv on A. */

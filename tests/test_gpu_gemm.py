@@ -21,9 +21,8 @@ def _mk(shape, dtype, gen):
     return torch.randn(shape, generator=gen, dtype=torch.float32).to(dtype).cuda()
 
 
-VARIANTS = [(torch.float32, 1), (torch.bfloat16, 1), (torch.bfloat16, 2), (torch.bfloat16, 4), (torch.bfloat16, 5),
-            (torch.bfloat16, 6), (torch.bfloat16, 7), (torch.bfloat16, 8), (torch.bfloat16, 9),
-            (torch.bfloat16, 10)]
+VARIANTS = [(torch.float32, 1), (torch.bfloat16, 1), (torch.bfloat16, 2), (torch.bfloat16, 11),
+            (torch.bfloat16, 12), (torch.bfloat16, 13)]
 
 
 @pytest.mark.parametrize("dtype,variant", VARIANTS)
@@ -85,9 +84,11 @@ def test_gemm_splitk_tanh_beta(dtype, variant):
 
 @pytest.mark.parametrize("dtype,variant", VARIANTS)
 @pytest.mark.parametrize("cin,cout", [(80, 136), (64, 80)])
-def test_conv_implicit_gemm(dtype, variant, cin, cout):
-    """Conv1d(k5, pad2) fwd / dgrad / wgrad as implicit GEMMs, channels-last."""
-    Bsz, T, KS, pad = 3, 37, 5, 2
+@pytest.mark.parametrize("T", [37, 100])
+def test_conv_implicit_gemm(dtype, variant, cin, cout, T):
+    """Conv1d(k5, pad2) fwd / dgrad / wgrad as implicit GEMMs, channels-last (T >= 64
+    and C >= 64 also run the v7 loaders' conv tracking)."""
+    Bsz, KS, pad = 3, 5, 2
     g = torch.Generator().manual_seed(cin + cout)
     x = torch.randn(Bsz, T, cin, generator=g)
     w = torch.randn(cout, cin, KS, generator=g) / math.sqrt(cin * KS)
@@ -126,7 +127,8 @@ def test_conv_implicit_gemm(dtype, variant, cin, cout):
 
 @pytest.mark.parametrize("splits", [1, 4])
 @pytest.mark.parametrize("conv", [False, True])
-def test_wgrad_fused_bias_ksum(splits, conv):
+@pytest.mark.parametrize("variant", [0, 2, 11, 12, 13])
+def test_wgrad_fused_bias_ksum(splits, conv, variant):
     """Weight-gradient GEMM with the bias gradient (row sums of A = dY^T over k) fused."""
     Bsz, T, cin, cout, KS, pad = 3, 150, 64, 200, 5, 2
     M = Bsz * T
@@ -137,7 +139,7 @@ def test_wgrad_fused_bias_ksum(splits, conv):
     dw = torch.empty(cout, kin, device="cuda")
     gb = torch.full((cout,), 3.0, device="cuda")
     ops.gemm(dy, x, dw, cout, kin, M, cout, cin, kin, trans_a=True, trans_b=True, splits=splits,
-             b_conv=(T, cin, pad) if conv else None, a_ksum=gb, a_ksum_beta=0.5)
+             b_conv=(T, cin, pad) if conv else None, a_ksum=gb, a_ksum_beta=0.5, variant=variant)
     ref_b = 1.5 + dy.double().sum(0)
     assert rel(gb, ref_b) < 1e-6
     if not conv:

@@ -58,5 +58,5 @@ def gemm_bench(variants):
 
 
 if __name__ == "__main__":
-    vs = [int(x) for x in sys.argv[1:]] or [2, 4, 5, 6, 7]
+    vs = [int(x) for x in sys.argv[1:]] or [2, 13]
     gemm_bench(vs)

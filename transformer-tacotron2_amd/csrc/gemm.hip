@@ -570,243 +570,6 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
 }
 
 // =====================================================================================
-// v3 (bf16): the v2 operand images and swizzles, but a STAGES-deep LDS ring with the
-// next STAGES-1 K tiles in flight across the barrier (counted `s_waitcnt vmcnt` +
-// raw s_barrier, never a full drain inside the loop), BM = 128 or 256 rows
-// (256 = 8 waves, K-contiguous A only), and branch-light per-lane addressing: each
-// lane keeps its chunk pointers / conv tap-time state and advances them by one K
-// tile per iteration instead of recomputing divisions.
-// =====================================================================================
-struct LaneChunk {
-  const bf16* p;   // address of this lane's chunk for the current K tile (unmasked)
-  int outer, inner;
-  int t, tap;      // conv bookkeeping (time of outer, tap of inner)
-};
-
-template <bool KC>
-TT2_DEV void lane_chunk_init(LaneChunk& c, const OpDesc& d, int inst, int lane, int r0, int k0) {
-  if (KC) {
-    const int row = inst * 8 + (lane >> 3);
-    const int gc = (lane & 7) ^ (row & 7);
-    c.outer = r0 + row;
-    c.inner = k0 + gc * 8;
-  } else {
-    const int kr = inst * 4 + (lane >> 4);
-    const int gc = (lane & 15) ^ mc_swz(kr);
-    c.outer = k0 + kr;
-    c.inner = r0 + gc * 8;
-  }
-  c.p = reinterpret_cast<const bf16*>(d.p) + (int64_t)c.outer * d.ld + c.inner;
-  if (d.conv_t > 0) {
-    c.p -= (int64_t)d.conv_pad * d.conv_c;
-    c.t = c.outer % d.conv_t;
-    c.tap = c.inner / d.conv_c;
-  } else {
-    c.t = 0;
-    c.tap = 0;
-  }
-}
-
-template <bool KC>
-TT2_DEV void lane_chunk_advance(LaneChunk& c, const OpDesc& d) {
-  if (KC) {
-    c.inner += BK2;
-    c.p += BK2;
-    if (d.conv_t > 0) {   // inner = tap * C + ci: ci grows by 64 < C (C >= 80 when conv)
-      int ci = c.inner - c.tap * d.conv_c;
-      while (ci >= d.conv_c) { ci -= d.conv_c; ++c.tap; }
-    }
-  } else {
-    c.outer += BK2;
-    c.p += (int64_t)BK2 * d.ld;
-    if (d.conv_t > 0) {
-      c.t += BK2;
-      while (c.t >= d.conv_t) c.t -= d.conv_t;
-    }
-  }
-}
-
-TT2_DEV const void* lane_chunk_src(const LaneChunk& c, const OpDesc& d) {
-  bool ok = c.outer < d.outer_max && c.inner < d.inner_max;
-  if (d.conv_t > 0) {
-    const int ts = c.t + c.tap - d.conv_pad;
-    ok = ok && ts >= 0 && ts < d.conv_t;
-  }
-  return ok ? (const void*)c.p : (const void*)g_zero_page;
-}
-
-template <int N> TT2_DEV void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <int BM_, int STAGES> struct G3 {
-  static constexpr int WAVES = BM_ / 32;                 // 2 (n) x BM/64 (m)
-  static constexpr int THREADS = WAVES * 64;
-  static constexpr int A_BYTES = BM_ * BK2 * 2;
-  static constexpr int B_BYTES = 128 * BK2 * 2;
-  static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int A_INST = A_BYTES / 1024 / WAVES;  // LDS-DMA instructions per wave per tile
-  static constexpr int B_INST = B_BYTES / 1024 / WAVES;
-  static constexpr int INST = A_INST + B_INST;
-  static constexpr int EPI = BM_ * EPI_LD * 4;
-  static constexpr int SMEM = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
-};
-
-template <bool AK, bool BKC, int BM_, int STAGES>
-__global__ __launch_bounds__((BM_ / 32) * 64) void gemm3_kernel(OpDesc A, OpDesc B, EpiParams E, int M,
-                                                                         int N, int K, int k_split, float* ws,
-                                                                         int ntm, int ntn) {
-  using G = G3<BM_, STAGES>;
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nt = ntm * ntn;
-  const int bid = blockIdx.x;
-  const int q = nt / 8, rr = nt % 8, x = bid % 8;
-  const int tile = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + bid / 8;
-  const int m0 = (tile / ntn) * BM_, n0 = (tile % ntn) * BN;
-  const int kb = blockIdx.y * k_split;
-  const int ke = min(K, kb + k_split);
-  if (AK) A.inner_max = ke; else A.outer_max = ke;
-  if (BKC) B.inner_max = ke; else B.outer_max = ke;
-  const int nkt = (ke - kb + BK2 - 1) / BK2;
-
-  LaneChunk ca[G::A_INST], cb[G::B_INST];
-#pragma unroll
-  for (int i = 0; i < G::A_INST; ++i) lane_chunk_init<AK>(ca[i], A, wave * G::A_INST + i, lane, m0, kb);
-#pragma unroll
-  for (int i = 0; i < G::B_INST; ++i) lane_chunk_init<BKC>(cb[i], B, wave * G::B_INST + i, lane, n0, kb);
-
-  auto issue = [&](int stage) {
-    char* sa = smem + stage * G::STAGE;
-    char* sb = sa + G::A_BYTES;
-#pragma unroll
-    for (int i = 0; i < G::A_INST; ++i) {
-      __builtin_amdgcn_global_load_lds((gvoid_t*)lane_chunk_src(ca[i], A),
-                                       (lvoid_t*)(sa + (wave * G::A_INST + i) * 1024), 16, 0, 0);
-      lane_chunk_advance<AK>(ca[i], A);
-    }
-#pragma unroll
-    for (int i = 0; i < G::B_INST; ++i) {
-      __builtin_amdgcn_global_load_lds((gvoid_t*)lane_chunk_src(cb[i], B),
-                                       (lvoid_t*)(sb + (wave * G::B_INST + i) * 1024), 16, 0, 0);
-      lane_chunk_advance<BKC>(cb[i], B);
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: tiles 0 .. STAGES-2 in flight
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nkt) issue(s);
-  if (nkt > STAGES - 2) wait_vmcnt<(STAGES - 2) * G::INST>();
-  else wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();
-
-  for (int kt = 0; kt < nkt; ++kt) {
-    const bool more = kt + STAGES - 1 < nkt;
-    if (more) issue((kt + STAGES - 1) % STAGES);
-    const char* sa = smem + (kt % STAGES) * G::STAGE;
-    const char* sb = sa + G::A_BYTES;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      Frag8<bf16> fa[4], fb[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) frag2<AK>(fa[i], sa, wm * 64 + 16 * i, kk, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) frag2<BKC>(fb[j], sb, wn * 64 + 16 * j, kk, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) mma16(fa[i], fb[j], acc[i][j]);
-    }
-    // tile kt+1 must have landed (this wave's part), and every wave must be done
-    // reading tile kt before the NEXT iteration's issue overwrites its slot.
-    if (more) wait_vmcnt<(STAGES - 2) * G::INST>();
-    else wait_vmcnt<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-
-  float* cs = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        cs[(wm * 64 + 16 * i + 4 * (lane >> 4) + r) * EPI_LD + wn * 64 + 16 * j + (lane & 15)] = acc[i][j][r];
-  __syncthreads();
-  const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
-  constexpr int ITERS = BM_ * 16 / G::THREADS;
-#pragma unroll 2
-  for (int it = 0; it < ITERS; ++it) {
-    const int id = tid + G::THREADS * it;
-    const int row = id >> 4, c8 = (id & 15) * 8;
-    const int m = m0 + row, n = n0 + c8;
-    if (m >= M || n >= N) continue;
-    float v[8];
-    const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + row * EPI_LD + c8);
-    const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * EPI_LD + c8 + 4);
-    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-    v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-    if (ws) {
-      float* w = ws + ((int64_t)blockIdx.y * M + m) * N + n;
-      if (n + 8 <= N && (N % 4) == 0) {
-        *reinterpret_cast<f32x4*>(w) = lo;
-        *reinterpret_cast<f32x4*>(w + 4) = hi;
-      } else {
-        for (int j = 0; j < 8; ++j)
-          if (n + j < N) w[j] = v[j];
-      }
-    } else {
-      epi_store8(E, seed, m, n, N, v);
-    }
-  }
-}
-
-template <bool AK, bool BKC, int BM_, int STAGES>
-hipError_t launch3(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
-                   hipStream_t s) {
-  using G = G3<BM_, STAGES>;
-  int k_split = K;
-  if (splits > 1) {
-    k_split = ((K + splits - 1) / splits + BK2 - 1) / BK2 * BK2;
-    splits = (K + k_split - 1) / k_split;
-  }
-  const int ntm = (M + BM_ - 1) / BM_, ntn = (N + BN - 1) / BN;
-  static bool attr_set = false;   // one-time opt-in to > 64 KB dynamic LDS
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm3_kernel<AK, BKC, BM_, STAGES>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
-    attr_set = true;
-  }
-  dim3 grid(ntm * ntn, splits);
-  hipLaunchKernelGGL((gemm3_kernel<AK, BKC, BM_, STAGES>), grid, dim3(G::THREADS), G::SMEM, s, A, B, E, M, N, K,
-                     k_split, splits > 1 ? ws : nullptr, ntm, ntn);
-  if (splits > 1 && !E.main_only) {
-    const int64_t total = (int64_t)M * N;
-    int64_t nb = (total + 255) / 256;
-    int blocks = (int)(nb < 4096 ? nb : 4096);
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, splits, E, M, N);
-  }
-  return hipGetLastError();
-}
-
-// =====================================================================================
 // skinny-M (decode, M <= 32) bf16: out[M, N] = X[M, K] W[N, K]^T.  The problem is a
 // weight stream: every workgroup owns 16 output columns and streams their W rows
 // straight to registers (no LDS round trip), the 4 waves split K, and one MFMA
@@ -932,321 +695,244 @@ hipError_t launch2(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
 
 
 // =====================================================================================
-// v4 (bf16, K-contiguous A): 256 x 256 output tile, 512 threads = 8 waves (2 M x 4 N),
-// each wave 128 x 64 = 8 x 4 MFMA 16x16x32 blocks.  At 64 MFMA FLOP per staged byte
-// x 2 this halves the L2 -> CU bytes per FLOP of the 128^2 tile, which is what bounds
-// the 128^2 kernel (~70 GB/s per CU served from L2).  K runs in 32-deep "k-halves"
-// through a 4-slot LDS ring (slot = A 256x32 + B 256x32 bf16 = 32 KB), filled by
-// LDS-DMA three k-halves ahead of the one being multiplied; per k-half: counted
-// vmcnt for this thread's copies of the current slot, one barrier, re-issue into the
-// slot the previous k-half released, 12 fragment reads, 32 MFMAs.
-// LDS images (swizzle on the per-lane global source, image lane-linear):
-//   K-contiguous operand: [256 rows][4 chunks of 16 B], chunk c of row r at c ^ ((r>>1)&3)
-//   N-contiguous B      : [32 k rows][32 chunks], chunk c of row k at c ^ mc_swz(k)
-// both bank-conflict-free for their ds_read_b128 / ds_read_b64_tr_b16 patterns.
+// v6 (bf16, plain operands): 256-row tiles.  Every 128^2 kernel above streams operand
+// tiles at ~50 GB/s per CU, and making both operands L2-resident speeds the same launch
+// up by only ~5 %: the L2 -> LDS path, not HBM, bounds them, so FLOPs per staged byte
+// is the lever -- 256 x 256 (128 FLOP/B) or 256 x 128 (85 FLOP/B) against 64.
+// 512 threads = 8 waves.  BN = 256: 2 (M) x 4 (N) waves of 128 x 64, 2 LDS stages;
+// BN = 128: 4 x 2 waves of 64 x 64, 3 stages (counted vmcnt + raw s_barrier).  BK = 64.
+// Each lane's LDS-DMA source is a loop-invariant 32-bit byte offset from a wave-uniform
+// base that advances one K tile per step, so the loop spends no VALU on addresses.
+// Rows / columns past M or N are clamped to the last valid one (they only feed C rows /
+// columns that are never stored); the K tail (the last step when the K range is not a
+// multiple of 64) takes a masked copy that reads the zero page.
+// Images are v2's: K-contiguous [rows][8 chunks], chunk c of row r at c ^ (r & 7);
+// M/N-contiguous as 128-column sub-images [64 k][16 chunks], chunk c of row k at
+// c ^ mc_swz(k).
 // =====================================================================================
-constexpr int G4_NT = 512;
-constexpr int G4_OPB = 256 * 32 * 2;               // 16 KB: one operand's k-half
-constexpr int G4_SLOT = 2 * G4_OPB;                // 32 KB
-constexpr int G4_SLOTS = 4;
-constexpr int G4_EPI_LD = 260;                     // f32 words per staged C row
-constexpr int G4_SMEM = (G4_SLOTS * G4_SLOT > 128 * G4_EPI_LD * 4) ? G4_SLOTS * G4_SLOT : 128 * G4_EPI_LD * 4;
-
-// this wave's 2 of the 16 LDS-DMA instructions of one operand k-half
-template <bool KC>
-TT2_DEV void g4_issue(const OpDesc& d, char* lds, int r0, int k0, int lane, int wave) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int inst = wave * 2 + i;
-    const void* src;
-    if (KC) {
-      const int row = inst * 16 + (lane >> 2);
-      const int lc = (lane & 3) ^ ((row >> 1) & 3);
-      src = chunk_src(d, r0 + row, k0 + lc * 8);
-    } else {
-      const int kr = inst * 2 + (lane >> 5);
-      const int lc = (lane & 31) ^ mc_swz(kr);
-      src = chunk_src(d, k0 + kr, r0 + lc * 8);
-    }
-    __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(lds + inst * 1024), 16, 0, 0);
-  }
-}
-
-// 16 x 32 fragment (rows r0 + (lane&15)) of a k-half image
-template <bool KC>
-TT2_DEV bf16x8 g4_frag(const char* img, int r0, int lane) {
-  if (KC) {
-    const int row = r0 + (lane & 15);
-    return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((((lane >> 4) ^ (row >> 1)) & 3) << 4));
-  } else {
-    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    const int c = (r0 + 4 * p) >> 3;
-    const int k_lo = 8 * g + q, k_hi = k_lo + 4;
-    typedef __attribute__((address_space(3))) short4v lds_s4;
-    const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_s4*)(img + k_lo * 512 + ((c ^ mc_swz(k_lo)) << 4) + ((p & 1) << 3)));
-    const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_s4*)(img + k_hi * 512 + ((c ^ mc_swz(k_hi)) << 4) + ((p & 1) << 3)));
-    union { short4v s[2]; bf16x8 v; } u;
-    u.s[0] = lo;
-    u.s[1] = hi;
-    return u.v;
-  }
-}
-
-TT2_DEV void g4_barrier() { asm volatile("s_barrier" ::: "memory"); }
-
-template <bool BKC>
-__global__ __launch_bounds__(G4_NT, 1) void gemm4_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
-                                                         int k_split, float* ws, int ntm, int ntn) {
-  __shared__ __attribute__((aligned(1024))) char smem[G4_SMEM];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int nt = ntm * ntn;
-  const int bid = blockIdx.x;
-  const int q8 = nt / 8, rr = nt % 8, x = bid % 8;
-  const int tile = (x < rr ? x * (q8 + 1) : rr * (q8 + 1) + (x - rr) * q8) + bid / 8;
-  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
-  const int kb = blockIdx.y * k_split;
-  const int ke = min(K, kb + k_split);
-  A.inner_max = ke;
-  if (BKC) B.inner_max = ke; else B.outer_max = ke;
-  const int nkh = (ke - kb + 31) / 32;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int h = 0; h < 3; ++h)
-    if (h < nkh) {
-      g4_issue<true>(A, smem + h * G4_SLOT, m0, kb + 32 * h, lane, wave);
-      g4_issue<BKC>(B, smem + h * G4_SLOT + G4_OPB, n0, kb + 32 * h, lane, wave);
-    }
-  for (int h = 0; h < nkh; ++h) {
-    // this thread's copies of k-half h are done when at most the later ones are pending
-    if (h + 2 < nkh) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (h + 1 < nkh) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    g4_barrier();   // everyone's copies of h landed; everyone finished reading k-half h-1
-    if (h + 3 < nkh) {
-      char* s3 = smem + ((h + 3) & 3) * G4_SLOT;
-      g4_issue<true>(A, s3, m0, kb + 32 * (h + 3), lane, wave);
-      g4_issue<BKC>(B, s3 + G4_OPB, n0, kb + 32 * (h + 3), lane, wave);
-    }
-    const char* sa = smem + (h & 3) * G4_SLOT;
-    const char* sb = sa + G4_OPB;
-    bf16x8 fb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = g4_frag<BKC>(sb, wc * 64 + 16 * j, lane);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      Frag8<bf16> fa;
-      fa.v = g4_frag<true>(sa, wr * 128 + 16 * i, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        Frag8<bf16> fbj;
-        fbj.v = fb[j];
-        mma16(fa, fbj, acc[i][j]);
-      }
-    }
-  }
-  g4_barrier();   // all waves done with the ring before it becomes the C staging area
-
-  // C through LDS in two 128-row passes (pass q: the waves with wr == q)
-  float* cs = reinterpret_cast<float*>(smem);
-  const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    if (wr == q) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            cs[(16 * i + 4 * (lane >> 4) + r) * G4_EPI_LD + wc * 64 + 16 * j + (lane & 15)] = acc[i][j][r];
-    }
-    __syncthreads();
-#pragma unroll 2
-    for (int it = 0; it < 8; ++it) {
-      const int id = tid + G4_NT * it;   // 128 rows x 32 chunks of 8
-      const int row = id >> 5, c8 = (id & 31) * 8;
-      const int m = m0 + 128 * q + row, n = n0 + c8;
-      if (m >= M || n >= N) continue;
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + row * G4_EPI_LD + c8);
-      const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * G4_EPI_LD + c8 + 4);
-      if (ws) {
-        float* w = ws + ((int64_t)blockIdx.y * M + m) * N + n;
-        if (n + 8 <= N && (N % 4) == 0) {
-          *reinterpret_cast<f32x4*>(w) = lo;
-          *reinterpret_cast<f32x4*>(w + 4) = hi;
-        } else {
-          const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          for (int j = 0; j < 8; ++j)
-            if (n + j < N) w[j] = v[j];
-        }
-      } else {
-        const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        epi_store8(E, seed, m, n, N, v);
-      }
-    }
-    __syncthreads();
-  }
-}
-
-template <bool BKC>
-hipError_t launch4(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
-                   hipStream_t s) {
-  int k_split = K;
-  if (splits > 1) {
-    k_split = ((K + splits - 1) / splits + 31) / 32 * 32;
-    splits = (K + k_split - 1) / k_split;
-  }
-  const int ntm = (M + 255) / 256, ntn = (N + 255) / 256;
-  hipLaunchKernelGGL((gemm4_kernel<BKC>), dim3(ntm * ntn, splits), dim3(G4_NT), 0, s, A, B, E, M, N, K, k_split,
-                     splits > 1 ? ws : nullptr, ntm, ntn);
-  if (splits > 1 && !E.main_only) {
-    const int64_t total = (int64_t)M * N;
-    int64_t nb = (total + 255) / 256;
-    int blocks = (int)(nb < 4096 ? nb : 4096);
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, splits, E, M, N);
-  }
-  return hipGetLastError();
-}
-
-
-// =====================================================================================
-// v5 (bf16): the v2 tile (128 x 128, 4 waves of 64 x 64) with BK = 32 and a 3-slot
-// LDS ring (16 KB per slot, two K steps in flight), and the C staging split in two
-// 64-row passes: 48 KB of LDS per workgroup, so three workgroups share a CU (v2: two).
-// More resident workgroups is what hides the per-K-step load latency of this tile
-// (measured: every v2 GEMM of the step runs faster with more workgroups per CU).
-// Images: K-contiguous [128 rows][4 chunks], chunk c of row r at c ^ ((r >> 1) & 3);
-// M/N-contiguous [32 k][16 chunks], chunk c of row k at c ^ mc_swz(k).
-// =====================================================================================
-constexpr int G5_OPB = 128 * 32 * 2;     // 8 KB per operand per slot
-constexpr int G5_SLOT = 2 * G5_OPB;       // 16 KB
-constexpr int G5_EPI = 64 * EPI_LD * 4;   // 33.8 KB of C staging per pass
-template <int SLOTS> struct G5 {
-  static constexpr int SMEM = SLOTS * G5_SLOT > G5_EPI ? SLOTS * G5_SLOT : G5_EPI;
-  static constexpr int WG_PER_CU = SLOTS == 3 ? 3 : 4;
+constexpr int G6_NT = 512;
+#ifdef TT2_STAMPS   // dev timeline (tools/gemm_stamps.hip): per workgroup and K step, wave 0
+__device__ unsigned long long g_st[4096 * 64 * 4];
+#define G6_STAMP(t, slot)                                                                            \
+  if (tid == 0 && (t) < 64)                                                                          \
+    g_st[((size_t)(blockIdx.x + gridDim.x * blockIdx.y) * 64 + (t)) * 4 + (slot)] = __builtin_amdgcn_s_memtime();
+#else
+#define G6_STAMP(t, slot)
+#endif
+template <int BN_> struct G6 {
+  static constexpr int WM = BN_ == 256 ? 2 : 4, WN = 8 / WM;
+  static constexpr int TM = 256 / WM, TN = BN_ / WN;              // wave tile
+  static constexpr int MI = TM / 16, NJ = TN / 16;
+  static constexpr int A_BYTES = 256 * 128, B_BYTES = BN_ * 128;   // 64 k x 2 B per row
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_INST = A_BYTES / 1024 / 8, B_INST = B_BYTES / 1024 / 8;   // per wave
+  static constexpr int INST = A_INST + B_INST;
+  static constexpr int STAGES = BN_ == 256 ? 2 : 3;
+  static constexpr int EPI_ROWS = BN_ == 256 ? 128 : 256;          // C rows staged per pass
+  static constexpr int EPI_LDW = BN_ + 4;
+  static constexpr int EPI = EPI_ROWS * EPI_LDW * 4;
+  static constexpr int SMEM = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
 };
 
-template <bool KC>
-TT2_DEV void g5_issue(const OpDesc& d, char* lds, int r0, int k0, int lane, int wave) {
+// loop-invariant byte offsets of this lane's NI copies of one operand tile
+template <bool KC, int NI>
+TT2_DEV void g6_offsets(uint32_t (&off)[NI], const OpDesc& d, int r0, int lane, int wave) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int inst = wave * 2 + i;
-    const void* src;
+  for (int i = 0; i < NI; ++i) {
+    const int inst = wave * NI + i;
     if (KC) {
-      const int row = inst * 16 + (lane >> 2);
-      const int lc = (lane & 3) ^ ((row >> 1) & 3);
-      src = chunk_src(d, r0 + row, k0 + lc * 8);
+      const int row = inst * 8 + (lane >> 3);
+      const int gc = (lane & 7) ^ (row & 7);
+      const int r = min(r0 + row, d.outer_max - 1);
+      off[i] = (uint32_t)(((int64_t)r * d.ld + gc * 8) * 2);
     } else {
-      const int kr = inst * 4 + (lane >> 4);
-      const int lc = (lane & 15) ^ mc_swz(kr);
-      src = chunk_src(d, k0 + kr, r0 + lc * 8);
+      const int sub = inst >> 4, kr = (inst & 15) * 4 + (lane >> 4);
+      const int gc = (lane & 15) ^ mc_swz(kr);
+      int col = r0 + sub * 128 + gc * 8;
+      col = col < d.inner_max ? col : d.inner_max - 8;
+      off[i] = (uint32_t)(((int64_t)kr * d.ld + col) * 2);
     }
+  }
+}
+
+template <bool KC, int NI>
+TT2_DEV void g6_issue(const OpDesc& d, const uint32_t (&off)[NI], char* lds, int k0, int wave) {
+  const char* base = reinterpret_cast<const char*>(d.p) + (KC ? (int64_t)k0 * 2 : (int64_t)k0 * d.ld * 2);
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+    __builtin_amdgcn_global_load_lds((gvoid_t*)(base + off[i]), (lvoid_t*)(lds + (wave * NI + i) * 1024), 16, 0, 0);
+}
+
+// the K-tail copy: chunks (KC) or k rows (M/N-contiguous) at k >= ke read the zero page
+template <bool KC, int NI>
+TT2_DEV void g6_issue_tail(const OpDesc& d, const uint32_t (&off)[NI], char* lds, int k0, int ke, int lane,
+                           int wave) {
+  const char* base = reinterpret_cast<const char*>(d.p) + (KC ? (int64_t)k0 * 2 : (int64_t)k0 * d.ld * 2);
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int inst = wave * NI + i;
+    int k;
+    if (KC) {
+      const int row = inst * 8 + (lane >> 3);
+      k = k0 + ((lane & 7) ^ (row & 7)) * 8;
+    } else {
+      k = k0 + (inst & 15) * 4 + (lane >> 4);
+    }
+    const void* src = k < ke ? (const void*)(base + off[i]) : (const void*)g_zero_page;
     __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(lds + inst * 1024), 16, 0, 0);
   }
 }
 
+// one LDS-DMA copy (instruction `inst` of the operand's tile); tl: the K-tail step
 template <bool KC>
-TT2_DEV void g5_frag(Frag8<bf16>& f, const char* img, int r0, int lane) {
-  if (KC) {
-    const int row = r0 + (lane & 15);
-    f.v = *reinterpret_cast<const bf16x8*>(img + row * 64 + ((((lane >> 4) ^ (row >> 1)) & 3) << 4));
-  } else {
-    frag2<false>(f, img, r0, 0, lane);   // 256-B k rows, k 0..31
+TT2_DEV void g6_issue_one(const OpDesc& d, uint32_t off, char* lds, int k0, int ke, int inst, int lane, bool tl) {
+  const char* base = reinterpret_cast<const char*>(d.p) + (KC ? (int64_t)k0 * 2 : (int64_t)k0 * d.ld * 2);
+  const void* src = base + off;
+  if (tl) {
+    int k;
+    if (KC) {
+      const int row = inst * 8 + (lane >> 3);
+      k = k0 + ((lane & 7) ^ (row & 7)) * 8;
+    } else {
+      k = k0 + (inst & 15) * 4 + (lane >> 4);
+    }
+    src = k < ke ? src : (const void*)g_zero_page;
   }
+  __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(lds + inst * 1024), 16, 0, 0);
 }
 
-template <bool AK, bool BKC, int SLOTS>
-__global__ __launch_bounds__(NT, G5<SLOTS>::WG_PER_CU) void gemm5_kernel(OpDesc A, OpDesc B, EpiParams E, int M,
-                                                                         int N, int K, int k_split, float* ws,
-                                                                         int ntm, int ntn) {
-  __shared__ __attribute__((aligned(1024))) char smem[G5<SLOTS>::SMEM];
+template <bool KC>
+TT2_DEV void g6_frag(Frag8<bf16>& f, const char* img, int r0, int kk, int lane) {
+  if (KC) frag2<true>(f, img, r0, kk, lane);
+  else frag2<false>(f, img + (r0 >> 7) * 16384, r0 & 127, kk, lane);
+}
+
+template <int N> TT2_DEV void g6_wait() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0, "g6_wait: add the count");
+}
+
+template <bool AK, bool BKC, int BN_>
+__global__ __launch_bounds__(G6_NT, 1) void gemm6_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
+                                                         int k_split, float* ws, int ntm, int ntn) {
+  using G = G6<BN_>;
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nt = ntm * ntn;
-  const int bid = blockIdx.x;
+  const int wm = wave / G::WN, wn = wave % G::WN;
+  const int nt = ntm * ntn, bid = blockIdx.x;
   const int q8 = nt / 8, rr = nt % 8, x = bid % 8;
   const int tile = (x < rr ? x * (q8 + 1) : rr * (q8 + 1) + (x - rr) * q8) + bid / 8;
-  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
-  const int kb = blockIdx.y * k_split;
-  const int ke = min(K, kb + k_split);
-  if (AK) A.inner_max = ke; else A.outer_max = ke;
-  if (BKC) B.inner_max = ke; else B.outer_max = ke;
-  const int nkt = (ke - kb + 31) / 32;
+  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * BN_;
+  const int kb = blockIdx.y * k_split, ke = min(K, kb + k_split);
+  const int nkt = (ke - kb + 63) / 64;
+  const bool tail = ((ke - kb) & 63) != 0;
   const bool do_ks = !AK && E.ksum && (tile % ntn) == 0;
   float ks[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  uint32_t oa[G::A_INST], ob[G::B_INST];
+  g6_offsets<AK>(oa, A, m0, lane, wave);
+  g6_offsets<BKC>(ob, B, n0, lane, wave);
 
-  f32x4 acc[4][4];
+  f32x4 acc[G::MI][G::NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < G::MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll
-  for (int t = 0; t < SLOTS - 1; ++t)
-    if (t < nkt) {
-      g5_issue<AK>(A, smem + t * G5_SLOT, m0, kb + 32 * t, lane, wave);
-      g5_issue<BKC>(B, smem + t * G5_SLOT + G5_OPB, n0, kb + 32 * t, lane, wave);
+  auto issue = [&](int step, int stage) {
+    char* sa = smem + stage * G::STAGE;
+    const int k0 = kb + 64 * step;
+    if (tail && step == nkt - 1) {
+      g6_issue_tail<AK>(A, oa, sa, k0, ke, lane, wave);
+      g6_issue_tail<BKC>(B, ob, sa + G::A_BYTES, k0, ke, lane, wave);
+    } else {
+      g6_issue<AK>(A, oa, sa, k0, wave);
+      g6_issue<BKC>(B, ob, sa + G::A_BYTES, k0, wave);
     }
-  int slot = 0;
-  for (int kt = 0; kt < nkt; ++kt) {
-    if (SLOTS == 3 && kt + 1 < nkt) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_barrier" ::: "memory");   // step kt landed everywhere; step kt-1's slot is free
-    if (kt + SLOTS - 1 < nkt) {
-      const int s2 = slot == 0 ? SLOTS - 1 : slot - 1;
-      g5_issue<AK>(A, smem + s2 * G5_SLOT, m0, kb + 32 * (kt + SLOTS - 1), lane, wave);
-      g5_issue<BKC>(B, smem + s2 * G5_SLOT + G5_OPB, n0, kb + 32 * (kt + SLOTS - 1), lane, wave);
+  };
+#pragma unroll
+  for (int s = 0; s < G::STAGES - 1; ++s)
+    if (s < nkt) issue(s, s);
+
+  int stage = 0;
+  for (int t = 0; t < nkt; ++t) {
+    G6_STAMP(t, 0)
+    if (G::STAGES == 3 && t + 1 < nkt) g6_wait<G::INST>();
+    else g6_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // last step's reads retired (WAR)
+    __builtin_amdgcn_s_barrier();   // step t landed everywhere; step t-1's stage is free
+    G6_STAMP(t, 1)
+    const bool more = t + G::STAGES - 1 < nkt;
+    const int nstep = t + G::STAGES - 1, nstage = stage == 0 ? G::STAGES - 1 : stage - 1;
+#ifdef TT2_G6_NOIL
+    if (more) issue(nstep, nstage);
+#endif
+    G6_STAMP(t, 2)
+    const char* sa = smem + stage * G::STAGE;
+    const char* sb = sa + G::A_BYTES;
+    char* na = smem + nstage * G::STAGE;
+    const int nk0 = kb + 64 * nstep;
+    const bool ntl = tail && nstep == nkt - 1;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      Frag8<bf16> fa[G::MI], fb[G::NJ];
+#pragma unroll
+      for (int i = 0; i < G::MI; ++i) g6_frag<AK>(fa[i], sa, wm * G::TM + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < G::NJ; ++j) g6_frag<BKC>(fb[j], sb, wn * G::TN + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < G::MI; ++i) {
+#pragma unroll
+        for (int j = 0; j < G::NJ; ++j) mma16(fa[i], fb[j], acc[i][j]);
+#ifndef TT2_G6_NOIL
+        // the next stage's copies ride between the MFMA rows (the TA is otherwise idle
+        // while the MFMAs run): copy q goes after MFMA row floor(q * 2 MI / INST)
+        const int slot = kk * G::MI + i;
+#pragma unroll
+        for (int q = 0; q < G::INST; ++q)
+          if (q * 2 * G::MI / G::INST == slot) {
+            if (more) {
+              if (q < G::A_INST) g6_issue_one<AK>(A, oa[q], na, nk0, ke, wave * G::A_INST + q, lane, ntl);
+              else g6_issue_one<BKC>(B, ob[q - G::A_INST], na + G::A_BYTES, nk0, ke,
+                                     wave * G::B_INST + q - G::A_INST, lane, ntl);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#endif
+      }
     }
-    const char* sa = smem + slot * G5_SLOT;
-    const char* sb = sa + G5_OPB;
-    Frag8<bf16> fa[4], fb[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) g5_frag<AK>(fa[i], sa, wm * 64 + 16 * i, lane);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) g5_frag<BKC>(fb[j], sb, wn * 64 + 16 * j, lane);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) mma16(fa[i], fb[j], acc[i][j]);
     if (!AK && do_ks) {
-      // k rows 2*(tid>>4), +1 of the [32 k][128 m] A image, m-chunk tid & 15
+      // m-chunk tid & 31 (sub-image (tid >> 4) & 1), k rows 4 * (tid >> 5) .. +3
+      const int cc = tid & 31;
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const int kr = 2 * (tid >> 4) + r;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(sa + kr * 256 + (((tid & 15) ^ mc_swz(kr)) << 4));
+      for (int r = 0; r < 4; ++r) {
+        const int kr = 4 * (tid >> 5) + r;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(sa + (cc >> 4) * 16384 + kr * 256 +
+                                                          (((cc & 15) ^ mc_swz(kr)) << 4));
 #pragma unroll
         for (int j = 0; j < 8; ++j) ks[j] += (float)v[j];
       }
     }
-    slot = slot == SLOTS - 1 ? 0 : slot + 1;
+    stage = stage == G::STAGES - 1 ? 0 : stage + 1;
   }
-  asm volatile("s_barrier" ::: "memory");   // ring free for the epilogue
+  G6_STAMP(nkt, 0)
+  __syncthreads();   // every wave is done with the ring
 
   if (!AK && do_ks) {
     float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      ks[j] += __shfl_xor(ks[j], 16, 64);
-      ks[j] += __shfl_xor(ks[j], 32, 64);
-    }
-    if (lane < 16) {
+    for (int j = 0; j < 8; ++j) ks[j] += __shfl_xor(ks[j], 32, 64);
+    if (lane < 32) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) red[(wave * 16 + lane) * 8 + j] = ks[j];
+      for (int j = 0; j < 8; ++j) red[(wave * 32 + lane) * 8 + j] = ks[j];
     }
     __syncthreads();
-    if (tid < 128) {
+    if (tid < 256) {
       const int cc = tid >> 3, j = tid & 7, m = m0 + tid;
-      const float v = (red[(0 * 16 + cc) * 8 + j] + red[(1 * 16 + cc) * 8 + j]) +
-                      (red[(2 * 16 + cc) * 8 + j] + red[(3 * 16 + cc) * 8 + j]);
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += red[(w * 32 + cc) * 8 + j];
       if (m < M) {
         if (ws) ws[(int64_t)gridDim.y * M * N + (int64_t)blockIdx.y * M + m] = v;
         else E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + v : v;
@@ -1257,26 +943,28 @@ __global__ __launch_bounds__(NT, G5<SLOTS>::WG_PER_CU) void gemm5_kernel(OpDesc 
 
   float* cs = reinterpret_cast<float*>(smem);
   const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
+  constexpr int CPR = BN_ / 8;   // 8-column chunks per C row
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    if (wm == q) {
+  for (int p = 0; p < 256 / G::EPI_ROWS; ++p) {
+    if ((wm * G::TM) / G::EPI_ROWS == p) {
+      const int rb = wm * G::TM - p * G::EPI_ROWS;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < G::MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < G::NJ; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            cs[(16 * i + 4 * (lane >> 4) + r) * EPI_LD + wn * 64 + 16 * j + (lane & 15)] = acc[i][j][r];
+            cs[(rb + 16 * i + 4 * (lane >> 4) + r) * G::EPI_LDW + wn * G::TN + 16 * j + (lane & 15)] = acc[i][j][r];
     }
     __syncthreads();
 #pragma unroll 2
-    for (int it = 0; it < 4; ++it) {
-      const int id = tid + NT * it;   // 64 rows x 16 chunks of 8
-      const int row = id >> 4, c8 = (id & 15) * 8;
-      const int m = m0 + 64 * q + row, n = n0 + c8;
+    for (int it = 0; it < G::EPI_ROWS * CPR / G6_NT; ++it) {
+      const int id = tid + G6_NT * it;
+      const int row = id / CPR, c8 = (id % CPR) * 8;
+      const int m = m0 + p * G::EPI_ROWS + row, n = n0 + c8;
       if (m >= M || n >= N) continue;
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + row * EPI_LD + c8);
-      const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * EPI_LD + c8 + 4);
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + row * G::EPI_LDW + c8);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * G::EPI_LDW + c8 + 4);
       const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       if (ws) {
         float* w = ws + ((int64_t)blockIdx.y * M + m) * N + n;
@@ -1293,18 +981,272 @@ __global__ __launch_bounds__(NT, G5<SLOTS>::WG_PER_CU) void gemm5_kernel(OpDesc 
     }
     __syncthreads();
   }
+  G6_STAMP(nkt, 3)
 }
 
-template <bool AK, bool BKC, int SLOTS>
-hipError_t launch5(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
+template <bool AK, bool BKC, int BN_>
+hipError_t launch6(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
                    hipStream_t s) {
   int k_split = K;
   if (splits > 1) {
-    k_split = ((K + splits - 1) / splits + 31) / 32 * 32;
+    k_split = ((K + splits - 1) / splits + 63) / 64 * 64;
     splits = (K + k_split - 1) / k_split;
   }
-  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm5_kernel<AK, BKC, SLOTS>), dim3(ntm * ntn, splits), dim3(NT), 0, s, A, B, E, M, N, K, k_split,
+  const int ntm = (M + 255) / 256, ntn = (N + BN_ - 1) / BN_;
+  hipLaunchKernelGGL((gemm6_kernel<AK, BKC, BN_>), dim3(ntm * ntn, splits), dim3(G6_NT), 0, s, A, B, E, M, N, K,
+                     k_split, splits > 1 ? ws : nullptr, ntm, ntn);
+  if (splits > 1 && !E.main_only) {
+    const int64_t total = (int64_t)M * N;
+    int64_t nb = (total + 255) / 256;
+    int blocks = (int)(nb < 4096 ? nb : 4096);
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, splits, E, M, N);
+  }
+  return hipGetLastError();
+}
+
+// =====================================================================================
+// v7 (bf16, plain operands): warp-specialised 256 x 128 tile.  In v6 every wave both
+// issues LDS-DMA copies and multiplies; an LDS-DMA issue stalls its wave while the
+// CU's address path (~64 B/clk) drains, so the MFMA stream of all 8 waves stops for
+// ~700 cycles per K step (in-kernel s_memtime timeline).  Here 4 loader waves (one per
+// SIMD) do nothing but copy, three K steps deep into a 3-stage ring, and 8 MFMA waves
+// (4 M x 2 N, 64 x 64 each) only read fragments and multiply; one s_barrier per step
+// hands stages over (loaders wait their copies of step t+1 with a counted vmcnt first).
+// The MFMA operands are swapped (D = B A^T: each lane holds 4 consecutive C columns of
+// one row) and v_permlane16_swap pairs adjacent column blocks, so every lane stores 8
+// consecutive columns of a row straight from registers -- no LDS round trip for C.
+// ksum (row sums of an M-contiguous A) comes from the A fragments of the wn == 0 waves.
+// =====================================================================================
+constexpr int G7_NT = 768;                          // 8 MFMA waves + 4 loader waves
+constexpr int G7_A = 256 * 128, G7_B = 128 * 128;   // bytes per stage: 64 k x 2 B per row
+constexpr int G7_STAGE = G7_A + G7_B;               // 48 KB
+constexpr int G7_STAGES = 3;
+constexpr int G7_AI = G7_A / 1024 / 4, G7_BI = G7_B / 1024 / 4;   // copies per loader wave: 8 + 4
+
+// Loader-lane state of one operand (NI copies per step).  Plain operands: a loop-
+// invariant byte offset from a wave-uniform base.  Conv operands (implicit im2col,
+// ld = C, element (outer, inner) at (outer + tap - pad) * C + ci) also track the
+// copy's conv coordinates incrementally (64 k per step, C >= 64 and T >= 64 so one
+// conditional wrap suffices): K-contiguous A (k = tap * C + ci): tap and ci of the
+// chunk, t of the row; M/N-contiguous B (k = token row): t of the k row, tap of the
+// column.  A copy reads the zero page when its chunk is conv padding or k >= ke.
+template <int NI> struct G7Lane {
+  uint32_t off[NI];
+  int t[NI], tap[NI], ci[NI];
+};
+
+template <bool KC, int NI>
+TT2_DEV void g7_lane_init(G7Lane<NI>& L, const OpDesc& d, int r0, int kb, int lane, int lw) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int inst = lw * NI + i;
+    if (KC) {
+      const int row = inst * 8 + (lane >> 3);
+      const int gc = (lane & 7) ^ (row & 7);
+      const int r = min(r0 + row, d.outer_max - 1);
+      L.off[i] = (uint32_t)(((int64_t)r * d.ld + gc * 8) * 2);
+      if (d.conv_t > 0) {
+        const int k = kb + gc * 8;
+        L.t[i] = r % d.conv_t;
+        L.tap[i] = k / d.conv_c;
+        L.ci[i] = k - L.tap[i] * d.conv_c;
+      }
+    } else {
+      const int sub = inst >> 4, kr = (inst & 15) * 4 + (lane >> 4);
+      const int gc = (lane & 15) ^ mc_swz(kr);
+      int col = r0 + sub * 128 + gc * 8;
+      col = col < d.inner_max ? col : d.inner_max - 8;
+      L.off[i] = (uint32_t)(((int64_t)kr * d.ld + col) * 2);
+      if (d.conv_t > 0) {
+        L.t[i] = (kb + kr) % d.conv_t;
+        L.tap[i] = col / d.conv_c;
+        L.ci[i] = 0;
+      }
+    }
+  }
+}
+
+template <bool KC, int NI>
+TT2_DEV void g7_issue(const OpDesc& d, G7Lane<NI>& L, char* lds, int k0, int ke, int lane, int lw, bool tl) {
+  const bool conv = d.conv_t > 0;
+  const int64_t shift = conv ? (int64_t)d.conv_pad * d.conv_c : 0;
+  const char* base = reinterpret_cast<const char*>(d.p) + ((KC ? (int64_t)k0 : (int64_t)k0 * d.ld) - shift) * 2;
+  if (!conv && !tl) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      __builtin_amdgcn_global_load_lds((gvoid_t*)(base + L.off[i]), (lvoid_t*)(lds + (lw * NI + i) * 1024), 16, 0,
+                                       0);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int inst = lw * NI + i;
+    int k;
+    if (KC) {
+      const int row = inst * 8 + (lane >> 3);
+      k = k0 + ((lane & 7) ^ (row & 7)) * 8;
+    } else {
+      k = k0 + (inst & 15) * 4 + (lane >> 4);
+    }
+    bool ok = k < ke;
+    if (conv) {
+      ok = ok && (unsigned)(L.t[i] + L.tap[i] - d.conv_pad) < (unsigned)d.conv_t;
+      if (KC) {   // next step: k += 64 within (tap, ci)
+        L.ci[i] += 64;
+        if (L.ci[i] >= d.conv_c) { L.ci[i] -= d.conv_c; ++L.tap[i]; }
+      } else {    // next step: token row += 64
+        L.t[i] += 64;
+        if (L.t[i] >= d.conv_t) L.t[i] -= d.conv_t;
+      }
+    }
+    const void* src = ok ? (const void*)(base + L.off[i]) : (const void*)g_zero_page;
+    __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(lds + inst * 1024), 16, 0, 0);
+  }
+}
+
+template <bool AK, bool BKC>
+__global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
+                                                         int k_split, float* ws, int ntm, int ntn) {
+  __shared__ __attribute__((aligned(1024))) char smem[G7_STAGES * G7_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nt = ntm * ntn, bid = blockIdx.x;
+  const int q8 = nt / 8, rr = nt % 8, x = bid % 8;
+  const int tile = (x < rr ? x * (q8 + 1) : rr * (q8 + 1) + (x - rr) * q8) + bid / 8;
+  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 128;
+  const int kb = blockIdx.y * k_split, ke = min(K, kb + k_split);
+  const int nkt = (ke - kb + 63) / 64;
+  const bool tail = ((ke - kb) & 63) != 0;
+
+  if (wave >= 8) {   // ------------------------------------------------ loader waves
+    const int lw = wave - 8;
+    G7Lane<G7_AI> la;
+    G7Lane<G7_BI> lb;
+    g7_lane_init<AK>(la, A, m0, kb, lane, lw);
+    g7_lane_init<BKC>(lb, B, n0, kb, lane, lw);
+    auto issue = [&](int step, int stage) {   // steps are issued in order 0, 1, 2, ...
+      char* sa = smem + stage * G7_STAGE;
+      const int k0 = kb + 64 * step;
+      const bool tl = tail && step == nkt - 1;
+      g7_issue<AK>(A, la, sa, k0, ke, lane, lw, tl);
+      g7_issue<BKC>(B, lb, sa + G7_A, k0, ke, lane, lw, tl);
+    };
+    issue(0, 0);
+    if (nkt > 1) { issue(1, 1); asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); }
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    int st = 2;
+    for (int t = 0; t < nkt; ++t) {
+      if (t + 2 < nkt) {
+        issue(t + 2, st);
+        st = st == 2 ? 0 : st + 1;
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // step t+1 landed, t+2 in flight
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------ MFMA waves
+  const int wm = wave >> 1, wn = wave & 1;
+  const bool do_ks = !AK && E.ksum && (tile % ntn) == 0 && wn == 0;
+  float ks[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __builtin_amdgcn_s_barrier();
+  int stage = 0;
+  for (int t = 0; t < nkt; ++t) {
+    G6_STAMP(t, 0)
+    const char* sa = smem + stage * G7_STAGE;
+    const char* sb = sa + G7_A;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      Frag8<bf16> fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) g6_frag<AK>(fa[i], sa, wm * 64 + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g6_frag<BKC>(fb[j], sb, wn * 64 + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mma16(fb[j], fa[i], acc[i][j]);   // D[n][m]
+      if (!AK && do_ks) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ks[i] += (float)fa[i].v[e];
+      }
+    }
+    stage = stage == 2 ? 0 : stage + 1;
+    G6_STAMP(t, 1)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this stage's reads retired (WAR vs the next copy)
+    __builtin_amdgcn_s_barrier();
+  }
+  G6_STAMP(nkt, 0)
+
+  if (!AK && do_ks) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ks[i] += __shfl_xor(ks[i], 16, 64);
+      ks[i] += __shfl_xor(ks[i], 32, 64);
+      const int m = m0 + wm * 64 + 16 * i + lane;
+      if (lane < 16 && m < M) {
+        if (ws) ws[(int64_t)gridDim.y * M * N + (int64_t)blockIdx.y * M + m] = ks[i];
+        else E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + ks[i] : ks[i];
+      }
+    }
+  }
+
+  // lane (q = lane >> 4) holds C[m][n0 + wn*64 + 16 j + 4 q + r] in acc[i][j][r]; swapping
+  // column blocks (2p, 2p+1) between row pairs q, q^1 leaves 8 consecutive columns per lane
+  const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
+  const int q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + 16 * i + (lane & 15);
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * pr][r]),
+                                                         __float_as_uint(acc[i][2 * pr + 1][r]), false, false);
+        v[r] = __uint_as_float(sw[0]);
+        v[4 + r] = __uint_as_float(sw[1]);
+      }
+      const int n = n0 + wn * 64 + 16 * (2 * pr + (q & 1)) + 8 * (q >> 1);
+      if (m >= M || n >= N) continue;
+      if (ws) {
+        float* w = ws + ((int64_t)blockIdx.y * M + m) * N + n;
+        if (n + 8 <= N && (N % 4) == 0) {
+          *reinterpret_cast<f32x4*>(w) = f32x4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4*>(w + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+          for (int j = 0; j < 8; ++j)
+            if (n + j < N) w[j] = v[j];
+        }
+      } else {
+        epi_store8(E, seed, m, n, N, v);
+      }
+    }
+  }
+  G6_STAMP(nkt, 3)
+}
+
+template <bool AK, bool BKC>
+hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
+                   hipStream_t s) {
+  int k_split = K;
+  if (splits > 1) {
+    k_split = ((K + splits - 1) / splits + 63) / 64 * 64;
+    splits = (K + k_split - 1) / k_split;
+  }
+  const int ntm = (M + 255) / 256, ntn = (N + 127) / 128;
+  hipLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(ntm * ntn, splits), dim3(G7_NT), 0, s, A, B, E, M, N, K, k_split,
                      splits > 1 ? ws : nullptr, ntm, ntn);
   if (splits > 1 && !E.main_only) {
     const int64_t total = (int64_t)M * N;
@@ -1323,8 +1265,8 @@ extern "C" size_t tt2_gemm_workspace_size(const tt2_gemm_args* a) {
 }
 
 // Kernel selection (also exported as tt2_gemm_plan): 1 v1 register-staged, 2 v2
-// LDS-DMA 128^2, 3 skinny (M <= 32), 4-7 v3 pipelines, 8 v4 256^2, 9/10 v5 BK=32 ring
-// (3 / 2 slots).  Returns -1 (error set) for an unsupported fusion request.
+// LDS-DMA 128^2, 3 skinny (M <= 32), 11 / 12 v6 256x256 / 256x128, 13 v7 warp-
+// specialised 256x128 (auto).  Returns -1 (error set) for an unsupported fusion request.
 static int gemm_plan(const tt2_gemm_args* a) {
   const int var = a->kernel_variant;
   const int64_t a_inner = a->trans_a ? a->m : a->k, b_inner = a->trans_b ? a->n : a->k;
@@ -1339,21 +1281,23 @@ static int gemm_plan(const tt2_gemm_args* a) {
   if (skinny) return 3;
   // LDS-DMA kernels: bf16, every 16-B chunk either fully inside or fully outside its row
   const bool v2 = a->dtype_in == TT2_BF16 && var != 1 && a_inner % 8 == 0 && b_inner % 8 == 0;
-  if (a->a_ksum && !(v2 && (var < 4 || var == 9 || var == 10) && a->trans_a && a->a_conv_t == 0))
+  if (a->a_ksum && !(v2 && a->trans_a && a->a_conv_t == 0))
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ksum needs bf16, trans_a, no conv A, the LDS-DMA kernel"), -1;
   if (!v2) return 1;
-  // v4: 256^2 tiles (K-contiguous A).  Auto only for GEMMs with a full chip of such
-  // tiles and a long K (4096^3: +20 % over v2); the training step's d_model = 512
-  // shapes measure faster on v2 (more CUs pulling operands), or variant 8 forces it.
-  const bool big = (int64_t)((a->m + 255) / 256) * ((a->n + 255) / 256) >= 256 && a->k >= 1024;
-  if (!a->trans_a && !a->a_ksum && (var == 8 || (var == 0 && big))) return 8;
-  // v5 auto: the BK=32 / 2-slot / 4-workgroups-per-CU form for activation GEMMs with
-  // enough 128^2 tiles to give every CU four (e.g. 12800 x 2048 x 512: +15 % fwd, +25 %
-  // dgrad); fewer tiles pile four workgroups onto a fraction of the CUs: those stay on v2
-  const int64_t tiles128 = (int64_t)((a->m + 127) / 128) * ((a->n + 127) / 128);
-  if (var == 9) return 9;
-  if (var == 10 || (var == 0 && !a->trans_a && !a->a_ksum && tiles128 >= 1024 && a->k <= 1024)) return 10;
-  if (var >= 4 && var <= 7) return var;
+  // 256-row-tile kernels (v6 / v7) need per-lane byte offsets that fit 32 bits; v6
+  // plain operands only.  Auto = v7, the warp-specialised 256 x 128 kernel (fastest on
+  // every GEMM of the training step: 1.2-1.6x v2).
+  const bool v6ok = a->a_conv_t == 0 && a->b_conv_t == 0 &&
+                    (int64_t)(a->trans_a ? a->k : a->m) * a->lda * 2 < (1LL << 31) &&
+                    (int64_t)(a->trans_b ? a->k : a->n) * a->ldb * 2 < (1LL << 31);
+  if ((var == 11 || var == 12) && v6ok) return var;
+  // v7 also takes implicit-im2col operands (its loaders track tap / time per copy)
+  // when every conv has C >= 64 and T >= 64 (one wrap per 64-deep K step)
+  auto conv_ok = [](int t, int c) { return t == 0 || (t >= 64 && c >= 64); };
+  const bool v7ok = conv_ok(a->a_conv_t, a->a_conv_c) && conv_ok(a->b_conv_t, a->b_conv_c) &&
+                    (int64_t)(a->trans_a ? a->k : a->m) * a->lda * 2 < (1LL << 31) &&
+                    (int64_t)(a->trans_b ? a->k : a->n) * a->ldb * 2 < (1LL << 31);
+  if ((var == 13 || var == 0) && v7ok) return 13;
   return 2;
 }
 
@@ -1420,35 +1364,22 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
                        a->m, a->n, a->k, F);
     return tt2_check_launch(hipGetLastError(), "tt2_gemm(skinny)");
   }
-  if (plan == 8) {
-    if (!a->trans_b) err = launch4<true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
-    else err = launch4<false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
-    return tt2_check_launch(err, "tt2_gemm(v4)");
+  if (plan == 13) {
+    if (!a->trans_a && !a->trans_b) err = launch7<true, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    else if (!a->trans_a && a->trans_b) err = launch7<true, false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    else if (a->trans_a && !a->trans_b) err = launch7<false, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    else err = launch7<false, false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    return tt2_check_launch(err, "tt2_gemm(v7)");
   }
-  if (plan == 9 || plan == 10) {
-#define TT2_G5(S)                                                                                            \
-    if (!a->trans_a && !a->trans_b) err = launch5<true, true, S>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);   \
-    else if (!a->trans_a && a->trans_b) err = launch5<true, false, S>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
-    else if (a->trans_a && !a->trans_b) err = launch5<false, true, S>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
-    else err = launch5<false, false, S>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
-    if (plan == 9) { TT2_G5(3) } else { TT2_G5(2) }
-#undef TT2_G5
-    return tt2_check_launch(err, "tt2_gemm(v5)");
-  }
-  if (plan >= 4 && plan <= 7) {
-    // v3 configurations: 4 = BM128/2 stages, 5 = BM128/3, 6 = BM256/3 (K-contiguous A), 7 = BM128/4
-    const int var = plan;
-#define TT2_G3(AK_, BK_)                                                                              \
-    if (var == 6 && AK_) err = launch3<AK_, BK_, 256, 3>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
-    else if (var == 5 || var == 6) err = launch3<AK_, BK_, 128, 3>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
-    else if (var == 7) err = launch3<AK_, BK_, 128, 4>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
-    else err = launch3<AK_, BK_, 128, 2>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
-    if (!a->trans_a && !a->trans_b) { TT2_G3(true, true) }
-    else if (!a->trans_a && a->trans_b) { TT2_G3(true, false) }
-    else if (a->trans_a && !a->trans_b) { TT2_G3(false, true) }
-    else { TT2_G3(false, false) }
-#undef TT2_G3
-    return tt2_check_launch(err, "tt2_gemm(v3)");
+  if (plan == 11 || plan == 12) {
+#define TT2_G6(BN_)                                                                                           \
+    if (!a->trans_a && !a->trans_b) err = launch6<true, true, BN_>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);   \
+    else if (!a->trans_a && a->trans_b) err = launch6<true, false, BN_>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
+    else if (a->trans_a && !a->trans_b) err = launch6<false, true, BN_>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
+    else err = launch6<false, false, BN_>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    if (plan == 11) { TT2_G6(256) } else { TT2_G6(128) }
+#undef TT2_G6
+    return tt2_check_launch(err, "tt2_gemm(v6)");
   }
   if (plan == 2) {
     if (!a->trans_a && !a->trans_b) err = launch2<true, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);

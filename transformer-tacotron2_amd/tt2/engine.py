@@ -36,19 +36,35 @@ def sinusoid_table(max_len: int, dim: int) -> torch.Tensor:
     return pe
 
 
-def auto_splits(n_out: int, n_in: int, k: int) -> int:
-    """Split-K factor for a weight-gradient GEMM (long K = tokens, few output tiles)."""
+def _wide(dtype, conv, m: int, *inner: int) -> bool:
+    """True when tt2_gemm's auto plan takes the 256 x 128 kernel (v7) for a GEMM with
+    m output rows: bf16, 8-aligned inner dims, conv operands (T, C, pad) with T, C >= 64,
+    not the skinny decode path (see gemm.hip gemm_plan)."""
+    conv_ok = conv is None or (conv[0] >= 64 and conv[1] >= 64)
+    return dtype == torch.bfloat16 and conv_ok and m > 32 and all(d % 8 == 0 for d in inner)
+
+
+def auto_splits(n_out: int, n_in: int, k: int, wide: bool = False) -> int:
+    """Split-K factor for a weight-gradient GEMM (long K = tokens, few output tiles).
+    v7 (256 x 128 tiles): ~256 workgroups, >= 512 k each, at most 16 slabs (measured:
+    512x512x12800 sp16 < sp32 < sp8; 2048x512x12800 sp8 best)."""
+    if wide:
+        tiles = ((n_out + 255) // 256) * ((n_in + 127) // 128)
+        return max(1, min(16, 256 // tiles, k // 512))
     tiles = ((n_out + 127) // 128) * ((n_in + 127) // 128)
     if tiles >= 256:
         return 1
-    s = max(1, min(32, 512 // tiles, k // 256))
-    return s
+    return max(1, min(32, 512 // tiles, k // 256))
 
 
-def act_splits(m: int, n: int, k: int) -> int:
-    """Split-K factor for an activation GEMM: only when its 128x128 tiles cannot fill
-    the 256 CUs (the encoder's 2048-token GEMMs); the epilogue then runs in the
-    split-K reduce."""
+def act_splits(m: int, n: int, k: int, wide: bool = False) -> int:
+    """Split-K factor for an activation GEMM: only when its tiles cannot fill the 256
+    CUs (the encoder's 2048-token GEMMs); the epilogue then runs in the split-K reduce."""
+    if wide:
+        tiles = ((m + 255) // 256) * ((n + 127) // 128)
+        if tiles >= 128 or k < 1024 or m <= 32:
+            return 1
+        return max(1, min(8, 256 // tiles, k // 512))
     tiles = ((m + 127) // 128) * ((n + 127) // 128)
     if tiles >= 192 or k < 1024 or m <= 32:   # m <= 32: the decode step's skinny weight-streaming GEMM
         return 1
@@ -246,14 +262,15 @@ class TTSEngine:
     def _lin(self, x, w, out, m, n, k, bias=None, act=ACT_NONE, drop=NO_DROP, res=None, ldx=None, ldo=None,
              a_conv=None, beta=0.0, **fuse):
         ops.gemm(x, w, out, m, n, k, ldx or k, k, ldo or n, bias=bias, res=res, ldr=ldo or n, act=act, drop=drop,
-                 a_conv=a_conv, beta=beta, ws=self.ws, splits=act_splits(m, n, k), **fuse)
+                 a_conv=a_conv, beta=beta, ws=self.ws,
+                 splits=act_splits(m, n, k, _wide(x.dtype, a_conv, m, k) and not fuse), **fuse)
 
     def _dgrad(self, dy, w, out, m, n_in, n_out, res=None, gate=None, gate_scale=1.0, ldy=None, ldo=None,
                a_conv=None, beta=0.0):
         """out[m, n_in] = dy[m, n_out] @ W[n_out, n_in] (+res) (*gate)"""
         ops.gemm(dy, w, out, m, n_in, n_out, ldy or n_out, n_in, ldo or n_in, trans_b=True, res=res,
                  ldr=ldo or n_in, gate=gate, ldg=ldo or n_in, gate_scale=gate_scale, a_conv=a_conv, beta=beta,
-                 ws=self.ws, splits=act_splits(m, n_in, n_out))
+                 ws=self.ws, splits=act_splits(m, n_in, n_out, _wide(dy.dtype, a_conv, m, n_out, n_in)))
 
     def _conv_dgrad(self, dy, wflip, out, m, cin, cout, K, T, ldo=None, beta=0.0):
         """out[m, cin] = conv1d(dy, flipped W): implicit im2col of dy x wflip[cin][tap][cout]"""
@@ -266,7 +283,8 @@ class TTSEngine:
         # the fused path rides on the LDS-DMA kernel: bf16 with 8-aligned M and N
         fused = gb is not None and dy.dtype == torch.bfloat16 and n_out % 8 == 0 and n_in % 8 == 0
         ops.gemm(dy, x, gw, n_out, n_in, m, ldy or n_out, ldx or n_in, n_in, trans_a=True, trans_b=True,
-                 splits=auto_splits(n_out, n_in, m), b_conv=b_conv, ws=self.ws, a_ksum=gb if fused else None)
+                 splits=auto_splits(n_out, n_in, m, _wide(dy.dtype, b_conv, n_out, n_out, n_in)), b_conv=b_conv, ws=self.ws,
+                 a_ksum=gb if fused else None)
         if gb is not None and not fused:
             self._bias(dy, ldy or n_out, m, n_out, gb)
 

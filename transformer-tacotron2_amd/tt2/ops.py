@@ -60,7 +60,7 @@ _WS = Workspace()
 def gemm(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=None, res=None, ldr=0,
          gate=None, ldg=0, gate_scale=1.0, alpha=1.0, beta=0.0, act=0, drop: Drop = NO_DROP, splits=1,
          a_conv=None, b_conv=None, ws: Workspace | None = None, variant: int = 0, a_ksum=None, a_ksum_beta=0.0,
-         a_ln=None, kv=None):
+         a_ln=None, kv=None, main_only=False):
     """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see tt2_capi.h tt2_gemm_args.
     a_ksum (f32 [m], bf16 trans_a only): a_ksum = a_ksum_beta * a_ksum + sum_k A(m,k).
     a_ln = (branch, gamma, beta, out, eps): multiply LN(A + branch), writing it to out (skinny path).
@@ -96,6 +96,7 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=Non
         cache, t_ptr, col0, bstride, ld = kv
         g.kv_cache, g.kv_t, g.kv_col0, g.kv_bstride, g.kv_ld = ptr(cache), ptr(t_ptr), col0, bstride, ld
     g.splits = max(1, splits)
+    g.main_only = int(main_only)   # dev measurement: skip the split-K reduce
     if g.splits > 1:
         need = L.tt2_gemm_workspace_size(C.byref(g))
         buf = (ws or _WS).get(need)
