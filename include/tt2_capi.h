@@ -98,8 +98,15 @@ size_t tt2_gemm_workspace_size(const tt2_gemm_args* a);
 int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream);
 /* Kernel tt2_gemm would launch for these args (no device work): 1 register-staged
  * 128x128 (any dtype), 2 LDS-DMA 128x128 (bf16), 3 skinny decode (m <= 32),
- * 4-7 deeper LDS pipelines, 8 256x256, 9/10 BK=32 LDS ring; -1 invalid. */
+ * 11 / 12 LDS-DMA 256x256 / 256x128, 13 warp-specialised 256x128; -1 invalid. */
 int tt2_gemm_plan(const tt2_gemm_args* a);
+
+/* Grouped GEMM: up to 8 independent problems in ONE launch of the v7 kernel (every
+ * problem must be v7-eligible -- tt2_gemm_plan(p) == 13 -- and share trans_a/trans_b;
+ * each problem's own splits / workspace; one grouped split-K reduce follows).  Used for
+ * the weight gradients of a layer, which share K = tokens.  Replaces the per-linear
+ * weight-gradient calls of the reference's autograd backward (see tt2_gemm). */
+int tt2_gemm_grouped(const tt2_gemm_args* probs, int32_t n, hipStream_t stream);
 
 /* ---------------------------------------------------------------- attention
  * Scaled dot-product attention over heads of width 64, read in place from

@@ -144,3 +144,32 @@ def test_wgrad_fused_bias_ksum(splits, conv, variant):
     assert rel(gb, ref_b) < 1e-6
     if not conv:
         assert rel(dw, dy.double().t() @ x.double()) < 1e-5
+
+
+@pytest.mark.parametrize("splits", [1, 3])
+def test_gemm_grouped_matches_single(splits):
+    """tt2_gemm_grouped over weight-gradient problems of different shapes (with fused
+    bias sums, one conv-B problem, a K tail) equals the float64 reference."""
+    g = torch.Generator().manual_seed(5 + splits)
+    T, cin, pad = 100, 64, 2
+    M = 3 * T
+    probs, refs = [], []
+    for n_out, n_in, conv in [(512, 512, False), (200, 64, False), (136, 5 * cin, True), (1536, 128, False)]:
+        dy = torch.randn(M, n_out, generator=g).bfloat16().cuda()
+        x = torch.randn(M, cin if conv else n_in, generator=g).bfloat16().cuda()
+        dw = torch.empty(n_out, n_in, device="cuda")
+        gb = torch.full((n_out,), 2.0, device="cuda")
+        probs.append(dict(a=dy, b=x, c=dw, m=n_out, n=n_in, k=M, lda=n_out, ldb=x.shape[1], ldc=n_in, trans_a=True,
+                          trans_b=True, splits=splits, b_conv=(T, cin, pad) if conv else None, a_ksum=gb,
+                          a_ksum_beta=0.5))
+        if conv:
+            xp = torch.nn.functional.pad(x.double().view(3, T, cin), (0, 0, pad, pad))
+            cols = torch.cat([xp[:, t:t + T] for t in range(5)], dim=2).reshape(M, 5 * cin)
+            ref = dy.double().t() @ cols
+        else:
+            ref = dy.double().t() @ x.double()
+        refs.append((dw, ref, gb, 1.0 + dy.double().sum(0)))
+    ops.gemm_grouped(probs)
+    for dw, ref, gb, ref_b in refs:
+        assert rel(dw, ref) < 1e-5
+        assert rel(gb, ref_b) < 1e-6

@@ -48,20 +48,25 @@ def main(variant=None):
     for key, flops, _, _, _, saved in probe.rec:
         if saved is None:
             continue
-        if variant is not None:
-            saved.kernel_variant = int(variant)
+        grouped = key[0] == "gemm_grouped"
+        if variant is not None and not grouped:
+            saved[0].kernel_variant = int(variant)
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(10):
-            check(L.tt2_gemm(C.byref(saved), stream_ptr()), "gemm")
+            if grouped:
+                check(L.tt2_gemm_grouped(saved, len(saved), stream_ptr()), "gemm_grouped")
+            else:
+                check(L.tt2_gemm(C.byref(saved[0]), stream_ptr()), "gemm")
         e.record()
         torch.cuda.synchronize()
         t = s.elapsed_time(e) * 1e-3 / 10
-        conv = saved.a_conv_t > 0 or saved.b_conv_t > 0
-        epi = ("b" if saved.bias else "") + ("r" if saved.res else "") + ("g" if saved.gate else "") + \
-              ("a%d" % saved.act if saved.act else "") + ("d" if saved.drop_thr else "")
-        k = (saved.m, saved.n, saved.k, saved.trans_a, saved.trans_b, saved.splits, conv, epi, saved.dtype_out)
+        g0 = saved[0]
+        conv = any(g.a_conv_t > 0 or g.b_conv_t > 0 for g in saved)
+        epi = ("b" if g0.bias else "") + ("r" if g0.res else "") + ("g" if g0.gate else "") + \
+              ("a%d" % g0.act if g0.act else "") + ("d" if g0.drop_thr else "") + ("G%d" % len(saved) if grouped else "")
+        k = (g0.m, g0.n, g0.k, g0.trans_a, g0.trans_b, g0.splits, conv, epi, g0.dtype_out)
         grp = groups[k]
         grp[0] += 1
         grp[1] += t

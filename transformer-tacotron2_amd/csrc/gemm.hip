@@ -20,6 +20,8 @@
 // Split-K (gridDim.z > 1) writes raw f32 partial slabs to the workspace and a
 // second kernel (gemm_splitk_reduce) sums them in a fixed order (bitwise
 // reproducible) and applies the epilogue.
+#include <algorithm>
+
 #include "tt2_common.h"
 #include "tt2_capi.h"
 #include "tt2_internal.h"
@@ -209,12 +211,12 @@ __global__ __launch_bounds__(NT) void gemm_kernel(OpDesc A, OpDesc B, EpiParams 
       }
 }
 
-__global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int M, int N) {
+TT2_DEV void splitk_reduce_body(const float* ws, int splits, const EpiParams& E, int M, int N, int bx, int nbx) {
   const int64_t total = (int64_t)M * N;
   const uint32_t seed = E.drop.thr ? *E.drop.seed : 0u;
   if (E.ksum) {   // [splits][M] k-sum partials after the C slabs, fixed split order
     const float* kp = ws + splits * total;
-    for (int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; m < M; m += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t m = bx * (int64_t)blockDim.x + threadIdx.x; m < M; m += (int64_t)nbx * blockDim.x) {
       float v = 0.f;
       for (int z = 0; z < splits; ++z) v += kp[z * (int64_t)M + m];
       E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + v : v;
@@ -223,7 +225,7 @@ __global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int
   if ((N & 3) == 0) {
     // 4 consecutive columns per thread (16-B partial-slab loads), fixed split order
     const int64_t t4 = total / 4;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < t4; i += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t i = bx * (int64_t)blockDim.x + threadIdx.x; i < t4; i += (int64_t)nbx * blockDim.x) {
       // two accumulators, 4 slab loads in flight per step (fixed order per element)
       f32x4 v = reinterpret_cast<const f32x4*>(ws)[i], w = f32x4{0.f, 0.f, 0.f, 0.f};
       int z = 1;
@@ -243,12 +245,16 @@ __global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int
     }
     return;
   }
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = bx * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)nbx * blockDim.x) {
     float v = 0.f;
     for (int z = 0; z < splits; ++z) v += ws[z * total + i];
     const int m = (int)(i / N), n = (int)(i % N);
     st_any(E.c, (int64_t)m * E.ldc + n, E.c_dt, epi_value(E, seed, m, n, v));
   }
+}
+
+__global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int M, int N) {
+  splitk_reduce_body(ws, splits, E, M, N, blockIdx.x, gridDim.x);
 }
 
 template <typename T, bool AK, bool BKC>
@@ -1104,19 +1110,31 @@ TT2_DEV void g7_issue(const OpDesc& d, G7Lane<NI>& L, char* lds, int k0, int ke,
   }
 }
 
+// One GEMM problem of a (possibly grouped) v7 launch.  Work item = (split, tile).
+struct G7Prob {
+  OpDesc A, B;
+  EpiParams E;
+  int M, N, K, k_split, splits, ntn, items, item0;
+  float* ws;   // split-K slabs [splits][M][N] (+ [splits][M] k-sums); used when splits > 1
+};
+constexpr int G7_MAXP = 8;
+struct G7Group {
+  G7Prob p[G7_MAXP];
+  int np, items;
+};
+
 template <bool AK, bool BKC>
-__global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
-                                                         int k_split, float* ws, int ntm, int ntn) {
-  __shared__ __attribute__((aligned(1024))) char smem[G7_STAGES * G7_STAGE];
+TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
+  const OpDesc& A = P.A;
+  const OpDesc& B = P.B;
+  const EpiParams& E = P.E;
+  const int M = P.M, N = P.N, K = P.K, ntn = P.ntn;
+  float* ws = P.splits > 1 ? P.ws : nullptr;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nt = ntm * ntn, bid = blockIdx.x;
-  const int q8 = nt / 8, rr = nt % 8, x = bid % 8;
-  const int tile = (x < rr ? x * (q8 + 1) : rr * (q8 + 1) + (x - rr) * q8) + bid / 8;
   const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 128;
-  const int kb = blockIdx.y * k_split, ke = min(K, kb + k_split);
+  const int kb = split * P.k_split, ke = min(K, kb + P.k_split);
   const int nkt = (ke - kb + 63) / 64;
   const bool tail = ((ke - kb) & 63) != 0;
-
   if (wave >= 8) {   // ------------------------------------------------ loader waves
     const int lw = wave - 8;
     G7Lane<G7_AI> la;
@@ -1195,7 +1213,7 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(OpDesc A, OpDesc B, Epi
       ks[i] += __shfl_xor(ks[i], 32, 64);
       const int m = m0 + wm * 64 + 16 * i + lane;
       if (lane < 16 && m < M) {
-        if (ws) ws[(int64_t)gridDim.y * M * N + (int64_t)blockIdx.y * M + m] = ks[i];
+        if (ws) ws[(int64_t)P.splits * M * N + (int64_t)split * M + m] = ks[i];
         else E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + ks[i] : ks[i];
       }
     }
@@ -1221,7 +1239,7 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(OpDesc A, OpDesc B, Epi
       const int n = n0 + wn * 64 + 16 * (2 * pr + (q & 1)) + 8 * (q >> 1);
       if (m >= M || n >= N) continue;
       if (ws) {
-        float* w = ws + ((int64_t)blockIdx.y * M + m) * N + n;
+        float* w = ws + ((int64_t)split * M + m) * N + n;
         if (n + 8 <= N && (N % 4) == 0) {
           *reinterpret_cast<f32x4*>(w) = f32x4{v[0], v[1], v[2], v[3]};
           *reinterpret_cast<f32x4*>(w + 4) = f32x4{v[4], v[5], v[6], v[7]};
@@ -1237,22 +1255,61 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(OpDesc A, OpDesc B, Epi
   G6_STAMP(nkt, 3)
 }
 
+// flat block index -> XCD-contiguous work item (blocks b and b + 8 share an XCD)
+TT2_DEV int xcd_item(int bid, int n) {
+  const int q = n / 8, r = n % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+template <bool AK, bool BKC>
+__global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(G7Prob P) {
+  __shared__ __attribute__((aligned(1024))) char smem[G7_STAGES * G7_STAGE];
+  const int u = xcd_item(blockIdx.x, P.items);
+  g7_item<AK, BKC>(P, u % (P.items / P.splits), u / (P.items / P.splits), smem);
+}
+
+// Grouped launch: up to G7_MAXP independent problems of one layout (e.g. all weight
+// gradients of a layer, which share K = tokens), one workgroup per work item.
+template <bool AK, bool BKC>
+__global__ __launch_bounds__(G7_NT, 1) void gemm7g_kernel(G7Group G) {
+  __shared__ __attribute__((aligned(1024))) char smem[G7_STAGES * G7_STAGE];
+  const int u = xcd_item(blockIdx.x, G.items);
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < G7_MAXP; ++i)
+    if (i < G.np && u >= G.p[i].item0) p = i;
+  const G7Prob& P = G.p[p];
+  const int local = u - P.item0, nt = P.items / P.splits;
+  g7_item<AK, BKC>(P, local % nt, local / nt, smem);
+}
+
+// split-K reduce of every split problem of a group (blockIdx.y = problem)
+__global__ void gemm_splitk_reduce_g(G7Group G) {
+  const G7Prob& P = G.p[blockIdx.y];
+  if (P.splits > 1) splitk_reduce_body(P.ws, P.splits, P.E, P.M, P.N, blockIdx.x, gridDim.x);
+}
+
+G7Prob g7_prob(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits,
+                            float* ws) {
+  G7Prob P{A, B, E, M, N, K, K, 1, (N + 127) / 128, 0, 0, ws};
+  if (splits > 1) {
+    P.k_split = ((K + splits - 1) / splits + 63) / 64 * 64;
+    P.splits = (K + P.k_split - 1) / P.k_split;
+  }
+  P.items = ((M + 255) / 256) * P.ntn * P.splits;
+  return P;
+}
+
 template <bool AK, bool BKC>
 hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
                    hipStream_t s) {
-  int k_split = K;
-  if (splits > 1) {
-    k_split = ((K + splits - 1) / splits + 63) / 64 * 64;
-    splits = (K + k_split - 1) / k_split;
-  }
-  const int ntm = (M + 255) / 256, ntn = (N + 127) / 128;
-  hipLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(ntm * ntn, splits), dim3(G7_NT), 0, s, A, B, E, M, N, K, k_split,
-                     splits > 1 ? ws : nullptr, ntm, ntn);
-  if (splits > 1 && !E.main_only) {
+  const G7Prob P = g7_prob(A, B, E, M, N, K, splits, ws);
+  hipLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, P);
+  if (P.splits > 1 && !E.main_only) {
     const int64_t total = (int64_t)M * N;
     int64_t nb = (total + 255) / 256;
     int blocks = (int)(nb < 4096 ? nb : 4096);
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, splits, E, M, N);
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, P.splits, E, M, N);
   }
   return hipGetLastError();
 }
@@ -1303,8 +1360,8 @@ static int gemm_plan(const tt2_gemm_args* a) {
 
 extern "C" int tt2_gemm_plan(const tt2_gemm_args* a) { return gemm_plan(a); }
 
-extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
-  if (a->m <= 0 || a->n <= 0) return TT2_OK;
+// Validate one GEMM request and build its operand / epilogue descriptors.
+static int gemm_prep(const tt2_gemm_args* a, OpDesc& A, OpDesc& B, EpiParams& ep) {
   const int esz = a->dtype_in == TT2_BF16 ? 2 : 4;
   const int E = 16 / esz;
   auto misaligned = [&](const void* p, int64_t ld) {
@@ -1320,13 +1377,13 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   if (a->splits > 1 && (!a->workspace || a->ws_bytes < tt2_gemm_workspace_size(a)))
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: split-K workspace too small");
 
-  OpDesc A{a->a, a->lda, 0, 0, a->a_conv_t, a->a_conv_c, a->a_conv_pad};
-  OpDesc B{a->b, a->ldb, 0, 0, a->b_conv_t, a->b_conv_c, a->b_conv_pad};
+  A = OpDesc{a->a, a->lda, 0, 0, a->a_conv_t, a->a_conv_c, a->a_conv_pad};
+  B = OpDesc{a->b, a->ldb, 0, 0, a->b_conv_t, a->b_conv_c, a->b_conv_pad};
   if (!a->trans_a) { A.outer_max = a->m; A.inner_max = a->k; } else { A.outer_max = a->k; A.inner_max = a->m; }
   if (!a->trans_b) { B.outer_max = a->n; B.inner_max = a->k; } else { B.outer_max = a->k; B.inner_max = a->n; }
   if (a->k <= 0) return tt2_set_error(TT2_E_INVALID, "tt2_gemm: k must be > 0");
 
-  EpiParams ep;
+  ep = EpiParams{};
   ep.c = a->c; ep.ldc = a->ldc; ep.c_dt = a->dtype_out;
   ep.bias = a->bias;
   ep.res = a->res; ep.ldr = a->ldr; ep.res_dt = a->res_dtype;
@@ -1348,6 +1405,14 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
     ep.vec = ok(a->c, a->ldc, a->dtype_out) && ok(a->res, a->ldr, a->res_dtype) &&
              ok(a->gate, a->ldg, a->gate_dtype) && (reinterpret_cast<uintptr_t>(a->bias) % 16 == 0);
   }
+  return TT2_OK;
+}
+
+extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
+  if (a->m <= 0 || a->n <= 0) return TT2_OK;
+  OpDesc A, B;
+  EpiParams ep;
+  if (const int rc = gemm_prep(a, A, B, ep); rc != TT2_OK) return rc;
   float* ws = reinterpret_cast<float*>(a->workspace);
   const int sp = a->splits > 1 ? a->splits : 1;
 
@@ -1396,4 +1461,42 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   if (a->dtype_in == TT2_BF16) { TT2_GEMM_CASE(bf16) } else { TT2_GEMM_CASE(float) }
 #undef TT2_GEMM_CASE
   return tt2_check_launch(err, "tt2_gemm");
+}
+
+extern "C" int tt2_gemm_grouped(const tt2_gemm_args* probs, int n, hipStream_t stream) {
+  if (n <= 0) return TT2_OK;
+  if (!probs || n > G7_MAXP) return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: 1..8 problems");
+  G7Group G{};
+  int reduce_blocks = 0, ta = -1, tb = -1, main_only = 1;
+  for (int i = 0; i < n; ++i) {
+    const tt2_gemm_args* a = probs + i;
+    if (a->m <= 0 || a->n <= 0) continue;
+    OpDesc A, B;
+    EpiParams ep;
+    if (const int rc = gemm_prep(a, A, B, ep); rc != TT2_OK) return rc;
+    if (gemm_plan(a) != 13)
+      return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: every problem must take the v7 kernel (bf16, "
+                                          "8-aligned inner dims, conv T, C >= 64, no decode fusions)");
+    if (ta < 0) { ta = a->trans_a; tb = a->trans_b; }
+    if (a->trans_a != ta || a->trans_b != tb)
+      return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: problems must share trans_a / trans_b");
+    G7Prob P = g7_prob(A, B, ep, a->m, a->n, a->k, a->splits > 1 ? a->splits : 1,
+                       reinterpret_cast<float*>(a->workspace));
+    P.item0 = G.items;
+    G.items += P.items;
+    G.p[G.np++] = P;
+    main_only &= a->main_only;
+    if (P.splits > 1) {
+      const int64_t nb = ((int64_t)a->m * a->n + 255) / 256;
+      reduce_blocks = (int)std::max<int64_t>(reduce_blocks, nb < 4096 ? nb : 4096);
+    }
+  }
+  if (G.np == 0) return TT2_OK;
+  if (!ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<true, true>), dim3(G.items), dim3(G7_NT), 0, stream, G);
+  else if (!ta && tb) hipLaunchKernelGGL((gemm7g_kernel<true, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
+  else if (ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<false, true>), dim3(G.items), dim3(G7_NT), 0, stream, G);
+  else hipLaunchKernelGGL((gemm7g_kernel<false, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
+  if (reduce_blocks > 0 && !main_only)
+    hipLaunchKernelGGL(gemm_splitk_reduce_g, dim3(reduce_blocks, G.np), dim3(256), 0, stream, G);
+  return tt2_check_launch(hipGetLastError(), "tt2_gemm_grouped");
 }

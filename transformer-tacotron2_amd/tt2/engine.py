@@ -157,6 +157,9 @@ class Arena:
         mk("g_xb", (Md, d))
         mk("g_res", (Md, d))
         mk("g_br", (Md, d))
+        mk("g_br2", (Md, d))    # per-branch dY buffers: a layer's weight gradients run as one
+        mk("g_br3", (Md, d))    # grouped GEMM at the end of its backward (Engine._flush_wgrads)
+        mk("g_cq", (Md, d))
         mk("g_f1", (Md, F))
         mk("g_qkv", (Md, 3 * d))
         mk("g_att", (Md, d))
@@ -187,6 +190,7 @@ class TTSEngine:
                  seed: int = 0):
         self.cfg = c = cfg or TTSConfig()
         assert c.d_model == 512 and c.head_dim == 64, "kernels are built for d_model 512, head_dim 64"
+        self._wq = None   # weight-gradient requests queued for one grouped launch (see _defer_wgrads)
         self.cd = dtype
         self.dev = torch.device(device)
         self.lay = Layout(build_slots(c))
@@ -279,7 +283,13 @@ class TTSEngine:
 
     def _wgrad(self, dy, x, gw, n_out, n_in, m, ldy=None, ldx=None, b_conv=None, gb=None):
         """gw[n_out, n_in] (f32) = dy[m, n_out]^T @ x[m, n_in]; gb (optional) = the
-        bias gradient sum_m dy[m, :], fused into the GEMM's A-tile pass for bf16."""
+        bias gradient sum_m dy[m, :], fused into the GEMM's A-tile pass for bf16.
+        Inside a _defer_wgrads() scope, v7-eligible requests are queued and launched
+        together by _flush_wgrads (their inputs must stay live until then)."""
+        if self._wq is not None and _wide(dy.dtype, b_conv, n_out, n_out, n_in):
+            self._wq.append(dict(a=dy, b=x, c=gw, m=n_out, n=n_in, k=m, lda=ldy or n_out, ldb=ldx or n_in, ldc=n_in,
+                                 trans_a=True, trans_b=True, b_conv=b_conv, a_ksum=gb))
+            return
         # the fused path rides on the LDS-DMA kernel: bf16 with 8-aligned M and N
         fused = gb is not None and dy.dtype == torch.bfloat16 and n_out % 8 == 0 and n_in % 8 == 0
         ops.gemm(dy, x, gw, n_out, n_in, m, ldy or n_out, ldx or n_in, n_in, trans_a=True, trans_b=True,
@@ -287,6 +297,20 @@ class TTSEngine:
                  a_ksum=gb if fused else None)
         if gb is not None and not fused:
             self._bias(dy, ldy or n_out, m, n_out, gb)
+
+    def _defer_wgrads(self):
+        self._wq = []
+
+    def _flush_wgrads(self):
+        """Launch the queued weight gradients as grouped v7 GEMMs (<= 8 per launch), one
+        split-K factor per group: about 256 work items, >= 512 tokens per split."""
+        q, self._wq = self._wq, None
+        for i in range(0, len(q), 8):
+            grp = q[i:i + 8]
+            tiles = sum(((p["m"] + 255) // 256) * ((p["n"] + 127) // 128) for p in grp)
+            kmin = min(p["k"] for p in grp)
+            sp = max(1, min(16, 256 // tiles, kmin // 512))
+            ops.gemm_grouped([dict(p, splits=sp) for p in grp], ws=self.ws)
 
     def _bias(self, dy, ld, m, n, gb):
         ops.colsum(dy, ld, m, n, gb, ws=self.ws)
@@ -484,29 +508,30 @@ class TTSEngine:
             p, base = f"dec{l}.", SITE_DEC_LAYER + 4 * l
             x_in = A[f"dx{l}"]
             h1, h2 = A[f"dh1{l}"], A[f"dh2{l}"]
+            self._defer_wgrads()
             # LN3 + FFN
             ops.layernorm_bwd(gx, h2, A[f"df2{l}"], self.P(p + "ln3.g"), A[f"dln3m{l}"], A[f"dln3r{l}"], A["g_res"],
-                              A["g_br"], self.G(p + "ln3.g"), self.G(p + "ln3.b"), Md,
+                              A["g_br3"], self.G(p + "ln3.g"), self.G(p + "ln3.b"), Md,
                               drop=self.drop(base + 3, c.dropout), ws=self.ws, dbias=self.G(p + "ffn2.b"))
-            self._wgrad(A["g_br"], A[f"df1{l}"], self.G(p + "ffn2.w"), d, F, Md)
-            self._dgrad(A["g_br"], self.W(p + "ffn2.w"), A["g_f1"], Md, F, d, gate=A[f"df1{l}"],
+            self._wgrad(A["g_br3"], A[f"df1{l}"], self.G(p + "ffn2.w"), d, F, Md)
+            self._dgrad(A["g_br3"], self.W(p + "ffn2.w"), A["g_f1"], Md, F, d, gate=A[f"df1{l}"],
                         gate_scale=gs(c.dropout))
             self._wgrad(A["g_f1"], h2, self.G(p + "ffn1.w"), F, d, Md, gb=self.G(p + "ffn1.b"))
             self._dgrad(A["g_f1"], self.W(p + "ffn1.w"), gx2, Md, d, F, res=A["g_res"])
             gx, gx2 = gx2, gx
             # LN2 + cross attention
             ops.layernorm_bwd(gx, h1, A[f"dco{l}"], self.P(p + "ln2.g"), A[f"dln2m{l}"], A[f"dln2r{l}"], A["g_res"],
-                              A["g_br"], self.G(p + "ln2.g"), self.G(p + "ln2.b"), Md,
+                              A["g_br2"], self.G(p + "ln2.g"), self.G(p + "ln2.b"), Md,
                               drop=self.drop(base + 1, c.dropout), ws=self.ws, dbias=self.G(p + "co.b"))
-            self._wgrad(A["g_br"], A[f"dcatt{l}"], self.G(p + "co.w"), d, d, Md)
-            self._dgrad(A["g_br"], self.W(p + "co.w"), A["g_att"], Md, d, d)
+            self._wgrad(A["g_br2"], A[f"dcatt{l}"], self.G(p + "co.w"), d, d, Md)
+            self._dgrad(A["g_br2"], self.W(p + "co.w"), A["g_att"], Md, d, d)
             ko = 2 * d * l
-            g_cq = A["g_qkv"][:, :d]
+            g_cq = A["g_cq"]
             ops.attn_bwd(A[f"dcq{l}"], mkv[:, ko:], mkv[:, ko + d:], A[f"dcatt{l}"], A["g_att"], A[f"dclse{l}"],
-                         A["delta"], g_cq, g_mkv[:, ko:], g_mkv[:, ko + d:], d, kvld, kvld, d, d, 3 * d, kvld, kvld,
+                         A["delta"], g_cq, g_mkv[:, ko:], g_mkv[:, ko + d:], d, kvld, kvld, d, d, d, kvld, kvld,
                          B, H, Ty, Tx, A["text_len"], False, scale)
-            self._wgrad(g_cq, h1, self.G(p + "cq.w"), d, d, Md, ldy=3 * d, gb=self.G(p + "cq.b"))
-            self._dgrad(g_cq, self.W(p + "cq.w"), gx2, Md, d, d, ldy=3 * d, res=A["g_res"])
+            self._wgrad(g_cq, h1, self.G(p + "cq.w"), d, d, Md, gb=self.G(p + "cq.b"))
+            self._dgrad(g_cq, self.W(p + "cq.w"), gx2, Md, d, d, res=A["g_res"])
             gx, gx2 = gx2, gx
             # LN1 + self attention
             ops.layernorm_bwd(gx, x_in, A[f"do{l}"], self.P(p + "ln1.g"), A[f"dln1m{l}"], A[f"dln1r{l}"],
@@ -521,6 +546,7 @@ class TTSEngine:
             self._wgrad(gq, x_in, self.G(p + "qkv.w"), 3 * d, d, Md, gb=self.G(p + "qkv.b"))
             self._dgrad(gq, self.W(p + "qkv.w"), gx2, Md, d, 3 * d, res=A["g_res"])
             gx, gx2 = gx2, gx
+            self._flush_wgrads()
             self._ready(p + "qkv.w")
         # ---------------- decoder pre-net
         g_proj = A["g_br"]
@@ -543,6 +569,7 @@ class TTSEngine:
         gxe2 = A["g_xb"].view(-1)[:Me * d].view(Me, d)
         gres = A["g_res"].view(-1)[:Me * d].view(Me, d)
         gbr = A["g_br"].view(-1)[:Me * d].view(Me, d)
+        gbr2 = A["g_br2"].view(-1)[:Me * d].view(Me, d)
         gf1 = A["g_f1"].view(-1)[:Me * F].view(Me, F)
         gatt = A["g_att"].view(-1)[:Me * d].view(Me, d)
         gq = A["g_qkv"].view(-1)[:Me * 3 * d].view(Me, 3 * d)
@@ -551,11 +578,12 @@ class TTSEngine:
         for l in reversed(range(c.n_enc)):
             p, base = f"enc{l}.", SITE_ENC_LAYER + 4 * l
             x_in, h1 = A[f"ex{l}"], A[f"eh1{l}"]
-            ops.layernorm_bwd(gxe, h1, A[f"ef2{l}"], self.P(p + "ln2.g"), A[f"eln2m{l}"], A[f"eln2r{l}"], gres, gbr,
+            self._defer_wgrads()
+            ops.layernorm_bwd(gxe, h1, A[f"ef2{l}"], self.P(p + "ln2.g"), A[f"eln2m{l}"], A[f"eln2r{l}"], gres, gbr2,
                               self.G(p + "ln2.g"), self.G(p + "ln2.b"), Me, drop=self.drop(base + 2, c.dropout),
                               ws=self.ws, dbias=self.G(p + "ffn2.b"))
-            self._wgrad(gbr, A[f"ef1{l}"], self.G(p + "ffn2.w"), d, F, Me)
-            self._dgrad(gbr, self.W(p + "ffn2.w"), gf1, Me, F, d, gate=A[f"ef1{l}"], gate_scale=gs(c.dropout))
+            self._wgrad(gbr2, A[f"ef1{l}"], self.G(p + "ffn2.w"), d, F, Me)
+            self._dgrad(gbr2, self.W(p + "ffn2.w"), gf1, Me, F, d, gate=A[f"ef1{l}"], gate_scale=gs(c.dropout))
             self._wgrad(gf1, h1, self.G(p + "ffn1.w"), F, d, Me, gb=self.G(p + "ffn1.b"))
             self._dgrad(gf1, self.W(p + "ffn1.w"), gxe2, Me, d, F, res=gres)
             gxe, gxe2 = gxe2, gxe
@@ -571,6 +599,7 @@ class TTSEngine:
             self._wgrad(gq, x_in, self.G(p + "qkv.w"), 3 * d, d, Me, gb=self.G(p + "qkv.b"))
             self._dgrad(gq, self.W(p + "qkv.w"), gxe2, Me, d, 3 * d, res=gres)
             gxe, gxe2 = gxe2, gxe
+            self._flush_wgrads()
             self._ready(p + "qkv.w")
         # ---------------- encoder pre-net
         ops.posenc_bwd(gxe, self.pe, gbr, self.G("enc.alpha"), Me, Tx, drop=self.drop(SITE_ENC_PE, c.dropout),

@@ -57,14 +57,12 @@ class Workspace:
 _WS = Workspace()
 
 
-def gemm(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=None, res=None, ldr=0,
-         gate=None, ldg=0, gate_scale=1.0, alpha=1.0, beta=0.0, act=0, drop: Drop = NO_DROP, splits=1,
-         a_conv=None, b_conv=None, ws: Workspace | None = None, variant: int = 0, a_ksum=None, a_ksum_beta=0.0,
-         a_ln=None, kv=None, main_only=False):
-    """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see tt2_capi.h tt2_gemm_args.
-    a_ksum (f32 [m], bf16 trans_a only): a_ksum = a_ksum_beta * a_ksum + sum_k A(m,k).
-    a_ln = (branch, gamma, beta, out, eps): multiply LN(A + branch), writing it to out (skinny path).
-    kv = (cache, t_ptr, col0, bstride, ld): also store columns >= col0 to the KV cache at step *t_ptr."""
+def gemm_args(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=None, res=None, ldr=0,
+              gate=None, ldg=0, gate_scale=1.0, alpha=1.0, beta=0.0, act=0, drop: Drop = NO_DROP, splits=1,
+              a_conv=None, b_conv=None, ws: Workspace | None = None, variant: int = 0, a_ksum=None,
+              a_ksum_beta=0.0, a_ln=None, kv=None, main_only=False, defer_ws: bool = False) -> GemmArgs:
+    """Build the tt2_gemm_args of one request (see tt2_capi.h).  defer_ws: only size the
+    split-K workspace (ws_bytes); the caller places it."""
     L = lib()
     g = GemmArgs()
     g.a, g.b, g.c = a.data_ptr(), b.data_ptr(), c.data_ptr()
@@ -99,18 +97,56 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=Non
     g.main_only = int(main_only)   # dev measurement: skip the split-K reduce
     if g.splits > 1:
         need = L.tt2_gemm_workspace_size(C.byref(g))
-        buf = (ws or _WS).get(need)
-        g.workspace, g.ws_bytes = buf.data_ptr(), buf.numel()
+        g.ws_bytes = need
+        if not defer_ws:
+            g.workspace = (ws or _WS).get(need).data_ptr()
+    return g
+
+
+def gemm(a, b, c, m, n, k, lda, ldb, ldc, **kw):
+    """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see tt2_capi.h tt2_gemm_args.
+    a_ksum (f32 [m], bf16 trans_a only): a_ksum = a_ksum_beta * a_ksum + sum_k A(m,k).
+    a_ln = (branch, gamma, beta, out, eps): multiply LN(A + branch), writing it to out (skinny path).
+    kv = (cache, t_ptr, col0, bstride, ld): also store columns >= col0 to the KV cache at step *t_ptr."""
+    L = lib()
+    g = gemm_args(a, b, c, m, n, k, lda, ldb, ldc, **kw)
     if PROBE is not None:
-        key = ("gemm", L.tt2_gemm_plan(C.byref(g)), int(trans_a), int(trans_b))
+        key = ("gemm", L.tt2_gemm_plan(C.byref(g)), g.trans_a, g.trans_b)
         esz = 2 if g.dtype_in == _lib.DT_BF16 else 4
         algo_bytes = esz * (m * k + n * k) + (2 if g.dtype_out == _lib.DT_BF16 else 4) * m * n
         PROBE.begin()
         check(L.tt2_gemm(C.byref(g), stream_ptr()), "tt2_gemm")
-        PROBE.end(key, 2.0 * m * n * k, algo_bytes, g)
+        PROBE.end(key, 2.0 * m * n * k, algo_bytes, [g])
         return c
     check(L.tt2_gemm(C.byref(g), stream_ptr()), "tt2_gemm")
     return c
+
+
+def gemm_grouped(problems, ws: Workspace | None = None):
+    """One tt2_gemm_grouped launch (v7) over up to 8 requests, each a dict of gemm()
+    arguments (a, b, c, m, n, k, lda, ldb, ldc + keywords); their split-K slabs get
+    disjoint slices of one workspace."""
+    L = lib()
+    arr = (GemmArgs * len(problems))()
+    offs, total = [], 0
+    for i, p in enumerate(problems):
+        arr[i] = gemm_args(defer_ws=True, **p)
+        offs.append(total)
+        total += (arr[i].ws_bytes + 255) // 256 * 256
+    if total:
+        base = (ws or _WS).get(total).data_ptr()
+        for i in range(len(problems)):
+            if arr[i].splits > 1:
+                arr[i].workspace = base + offs[i]
+    if PROBE is not None:
+        key = ("gemm_grouped", 13, arr[0].trans_a, arr[0].trans_b)
+        flops = sum(2.0 * g.m * g.n * g.k for g in arr)
+        ab = sum(2 * (g.m * g.k + g.n * g.k) + (2 if g.dtype_out == _lib.DT_BF16 else 4) * g.m * g.n for g in arr)
+        PROBE.begin()
+        check(L.tt2_gemm_grouped(arr, len(problems), stream_ptr()), "tt2_gemm_grouped")
+        PROBE.end(key, flops, ab, list(arr))
+        return
+    check(L.tt2_gemm_grouped(arr, len(problems), stream_ptr()), "tt2_gemm_grouped")
 
 
 class LaunchProbe:
@@ -129,9 +165,10 @@ class LaunchProbe:
         e = torch.cuda.Event(enable_timing=True)
         e.record()
         saved = None
-        if args is not None:
-            saved = GemmArgs()
-            C.pointer(saved)[0] = args
+        if args is not None:   # a copy of the launch's tt2_gemm_args (array for a grouped launch)
+            saved = (GemmArgs * len(args))()
+            for i, g in enumerate(args):
+                saved[i] = g
         self.rec.append((key, flops, self._s, e, algo_bytes, saved))
 
     def summary(self):
@@ -155,11 +192,15 @@ class LaunchProbe:
             if k != key or saved is None:
                 continue
             torch.cuda.synchronize()
-            saved.main_only = 1      # the kernel alone (a split-K reduce is a different kernel)
+            for g in saved:
+                g.main_only = 1      # the kernel alone (a split-K reduce is a different kernel)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(reps):
-                check(L.tt2_gemm(C.byref(saved), stream_ptr()), "tt2_gemm(replay)")
+                if len(saved) == 1 and k[0] == "gemm":
+                    check(L.tt2_gemm(C.byref(saved[0]), stream_ptr()), "tt2_gemm(replay)")
+                else:
+                    check(L.tt2_gemm_grouped(saved, len(saved), stream_ptr()), "tt2_gemm_grouped(replay)")
             e.record()
             torch.cuda.synchronize()
             total += s.elapsed_time(e) * 1e-3 / reps
