@@ -158,6 +158,8 @@ def roofline(model, text, tl, mel, ml):
     tot_f = sum(v[1] for v in summ.values())
     achieved = flops / secs / 1e12
     kname = gemm_kernel_name(*key[1:4])
+    if key[0] == "gemm_grouped":
+        kname = kname.replace("gemm7_kernel", "gemm7g_kernel")
     traffic, tsrc = None, None
     prof = os.path.join(ROOT, "profiles")
     tfiles = sorted(f for f in os.listdir(prof) if f.endswith("_traffic.json")) if os.path.isdir(prof) else []

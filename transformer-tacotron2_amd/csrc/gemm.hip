@@ -44,6 +44,9 @@ struct EpiParams {
   int main_only;                  // split-K: skip the reduce launch (measurement hook)
 };
 
+// fixed-order split-K slab reduce + epilogue (defined after epi_store8)
+__global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int M, int N);
+
 TT2_DEV float ld_any(const void* p, int64_t i, int dt) {
   return dt == TT2_BF16 ? (float)reinterpret_cast<const bf16*>(p)[i] : reinterpret_cast<const float*>(p)[i];
 }
@@ -211,51 +214,6 @@ __global__ __launch_bounds__(NT) void gemm_kernel(OpDesc A, OpDesc B, EpiParams 
       }
 }
 
-TT2_DEV void splitk_reduce_body(const float* ws, int splits, const EpiParams& E, int M, int N, int bx, int nbx) {
-  const int64_t total = (int64_t)M * N;
-  const uint32_t seed = E.drop.thr ? *E.drop.seed : 0u;
-  if (E.ksum) {   // [splits][M] k-sum partials after the C slabs, fixed split order
-    const float* kp = ws + splits * total;
-    for (int64_t m = bx * (int64_t)blockDim.x + threadIdx.x; m < M; m += (int64_t)nbx * blockDim.x) {
-      float v = 0.f;
-      for (int z = 0; z < splits; ++z) v += kp[z * (int64_t)M + m];
-      E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + v : v;
-    }
-  }
-  if ((N & 3) == 0) {
-    // 4 consecutive columns per thread (16-B partial-slab loads), fixed split order
-    const int64_t t4 = total / 4;
-    for (int64_t i = bx * (int64_t)blockDim.x + threadIdx.x; i < t4; i += (int64_t)nbx * blockDim.x) {
-      // two accumulators, 4 slab loads in flight per step (fixed order per element)
-      f32x4 v = reinterpret_cast<const f32x4*>(ws)[i], w = f32x4{0.f, 0.f, 0.f, 0.f};
-      int z = 1;
-      for (; z + 3 < splits; z += 4) {
-        const f32x4 a0 = reinterpret_cast<const f32x4*>(ws + z * total)[i];
-        const f32x4 a1 = reinterpret_cast<const f32x4*>(ws + (z + 1) * total)[i];
-        const f32x4 a2 = reinterpret_cast<const f32x4*>(ws + (z + 2) * total)[i];
-        const f32x4 a3 = reinterpret_cast<const f32x4*>(ws + (z + 3) * total)[i];
-        v += a0 + a2;
-        w += a1 + a3;
-      }
-      for (; z < splits; ++z) v += reinterpret_cast<const f32x4*>(ws + z * total)[i];
-      v += w;
-      const int m = (int)(4 * i / N), n = (int)(4 * i % N);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) st_any(E.c, (int64_t)m * E.ldc + n + j, E.c_dt, epi_value(E, seed, m, n + j, v[j]));
-    }
-    return;
-  }
-  for (int64_t i = bx * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)nbx * blockDim.x) {
-    float v = 0.f;
-    for (int z = 0; z < splits; ++z) v += ws[z * total + i];
-    const int m = (int)(i / N), n = (int)(i % N);
-    st_any(E.c, (int64_t)m * E.ldc + n, E.c_dt, epi_value(E, seed, m, n, v));
-  }
-}
-
-__global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int M, int N) {
-  splitk_reduce_body(ws, splits, E, M, N, blockIdx.x, gridDim.x);
-}
 
 template <typename T, bool AK, bool BKC>
 hipError_t launch_t(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits,
@@ -426,6 +384,70 @@ TT2_DEV void epi_store8(const EpiParams& E, uint32_t seed, int m, int n0, int N,
   }
   for (int j = 0; j < 8; ++j)
     if (n0 + j < N) st_any(E.c, off + j, E.c_dt, epi_value(E, seed, m, n0 + j, v[j]));
+}
+
+TT2_DEV void splitk_reduce_body(const float* ws, int splits, const EpiParams& E, int M, int N, int bx, int nbx) {
+  const int64_t total = (int64_t)M * N;
+  const uint32_t seed = E.drop.thr ? *E.drop.seed : 0u;
+  if (E.ksum) {   // [splits][M] k-sum partials after the C slabs, fixed split order
+    const float* kp = ws + splits * total;
+    for (int64_t m = bx * (int64_t)blockDim.x + threadIdx.x; m < M; m += (int64_t)nbx * blockDim.x) {
+      float v = 0.f;
+      for (int z = 0; z < splits; ++z) v += kp[z * (int64_t)M + m];
+      E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + v : v;
+    }
+  }
+  if ((N & 7) == 0 && E.vec) {
+    // 8 consecutive columns per thread: 2 x 16-B slab loads per split (fixed split order),
+    // then the vectorised chunk epilogue (16-B bias / residual / gate / C loads and stores)
+    const int64_t t8 = total / 8;
+    for (int64_t i = bx * (int64_t)blockDim.x + threadIdx.x; i < t8; i += (int64_t)nbx * blockDim.x) {
+      const f32x4* w0 = reinterpret_cast<const f32x4*>(ws) + 2 * i;
+      f32x4 lo = w0[0], hi = w0[1];
+      for (int z = 1; z < splits; ++z) {
+        const f32x4* wz = reinterpret_cast<const f32x4*>(ws + z * total) + 2 * i;
+        lo += wz[0];
+        hi += wz[1];
+      }
+      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const int m = (int)(8 * i / N), n = (int)(8 * i % N);
+      epi_store8(E, seed, m, n, N, v);
+    }
+    return;
+  }
+  if ((N & 3) == 0) {
+    // 4 consecutive columns per thread (16-B partial-slab loads), fixed split order
+    const int64_t t4 = total / 4;
+    for (int64_t i = bx * (int64_t)blockDim.x + threadIdx.x; i < t4; i += (int64_t)nbx * blockDim.x) {
+      // two accumulators, 4 slab loads in flight per step (fixed order per element)
+      f32x4 v = reinterpret_cast<const f32x4*>(ws)[i], w = f32x4{0.f, 0.f, 0.f, 0.f};
+      int z = 1;
+      for (; z + 3 < splits; z += 4) {
+        const f32x4 a0 = reinterpret_cast<const f32x4*>(ws + z * total)[i];
+        const f32x4 a1 = reinterpret_cast<const f32x4*>(ws + (z + 1) * total)[i];
+        const f32x4 a2 = reinterpret_cast<const f32x4*>(ws + (z + 2) * total)[i];
+        const f32x4 a3 = reinterpret_cast<const f32x4*>(ws + (z + 3) * total)[i];
+        v += a0 + a2;
+        w += a1 + a3;
+      }
+      for (; z < splits; ++z) v += reinterpret_cast<const f32x4*>(ws + z * total)[i];
+      v += w;
+      const int m = (int)(4 * i / N), n = (int)(4 * i % N);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st_any(E.c, (int64_t)m * E.ldc + n + j, E.c_dt, epi_value(E, seed, m, n + j, v[j]));
+    }
+    return;
+  }
+  for (int64_t i = bx * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)nbx * blockDim.x) {
+    float v = 0.f;
+    for (int z = 0; z < splits; ++z) v += ws[z * total + i];
+    const int m = (int)(i / N), n = (int)(i % N);
+    st_any(E.c, (int64_t)m * E.ldc + n, E.c_dt, epi_value(E, seed, m, n, v));
+  }
+}
+
+__global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int M, int N) {
+  splitk_reduce_body(ws, splits, E, M, N, blockIdx.x, gridDim.x);
 }
 
 template <bool AK, bool BKC>
