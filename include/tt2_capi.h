@@ -92,6 +92,25 @@ typedef struct tt2_gemm_args {
   /* measurement hook: with splits > 1, launch only the main kernel (partials stay in
    * the workspace, C is not written), so a per-kernel timing excludes the reduce */
   int32_t main_only;
+  /* more decode-step epilogues, skinny path only:
+   * - scaled positional encoding: when pe_table != NULL, out[m, n] += (*pe_alpha) *
+   *   pe_table[(*pe_t) * n_cols + n] after the rest of the epilogue (f32 table [T][n]);
+   * - frame emit (the mel/stop heads GEMM): when emit_mel != NULL, with t = *emit_t < emit_tmax,
+   *   columns n < emit_nmels also go to emit_mel[(m * emit_tmax + t) * emit_nmels + n] (f32) and
+   *   emit_prev[m * emit_nmels + n] (bf16, the next step's pre-net input), column emit_nmels to
+   *   emit_stop[m * emit_tmax + t]; the last workgroup to finish then sets *emit_t = t + 1,
+   *   *emit_seed += 1 (if non-NULL) and re-zeroes *emit_done (a device int the caller zeroes
+   *   once).  Replaces the tt2_decode_emit launch. */
+  const float* pe_table;
+  const float* pe_alpha;
+  const int32_t* pe_t;
+  float* emit_mel;
+  float* emit_stop;
+  void* emit_prev;
+  int32_t* emit_t;
+  uint32_t* emit_seed;
+  int32_t* emit_done;
+  int32_t emit_nmels, emit_tmax;
 } tt2_gemm_args;
 
 size_t tt2_gemm_workspace_size(const tt2_gemm_args* a);
@@ -201,6 +220,14 @@ typedef struct tt2_ln_args {
 int tt2_layernorm_fwd(const tt2_ln_args* a, hipStream_t stream);
 size_t tt2_layernorm_bwd_workspace_size(const tt2_ln_args* a);
 int tt2_layernorm_bwd(const tt2_ln_args* a, hipStream_t stream);
+/* Decode-step residual combine + LayerNorm (bf16 x / y, c = 512):
+ *   y[m, :] = LN(x[m, :] + bias + sum_{s < splits} part[s][m][:]) * gamma + beta
+ * part: the raw f32 partial slabs [splits][m][c] of a skinny split-K projection (tt2_gemm
+ * with splits > 1 and main_only; splits 1, 2, 4, 8 or 16), summed in a fixed order.
+ * Replaces the output-projection epilogue + residual + LayerNorm of a decoder sublayer
+ *  where splitting K spreads the weight stream over more CUs. */
+int tt2_ln_combine(const void* x, const float* part, int32_t splits, const float* bias, const float* gamma,
+                   const float* beta, void* y, int32_t m, int32_t c, float eps, hipStream_t stream);
 
 /* ------------------------------------------------------------- BatchNorm
  * fwd: out = drop(act((y - mean)*rstd*gamma + beta)) (+ res), statistics over

@@ -52,7 +52,7 @@ def test_graph_replay_equals_eager():
     assert torch.equal(a1, a2)
 
 
-@pytest.mark.parametrize("fuse", [0, 2])
+@pytest.mark.parametrize("fuse", [0, 2, 3])
 def test_decode_fusion_levels_match(fuse):
     """bf16 decode with the KV scatter (default level 1) vs no fusion / also the fused
     LayerNorm prologues: same frames within bf16 rounding of the LN output."""
@@ -66,6 +66,8 @@ def test_decode_fusion_levels_match(fuse):
     a, _ = ref.run(text.cuda(), tl.cuda(), T, stop_threshold=None)
     b, _ = out.run(text.cuda(), tl.cuda(), T, stop_threshold=None)
     assert rel(b, a) < (1e-6 if fuse == 0 else 2e-2)
+    # the frame-emit epilogue advanced the device step counter once per frame
+    assert out.t.item() == T
 
 
 def test_stop_token_early_exit():

@@ -1,0 +1,168 @@
+"""Decode-step kernels vs float64 torch references (GPU): the skinny-M GEMM over every
+K regime (one pass per wave slice and multi-pass), its LayerNorm prologue, KV-cache
+scatter, positional-encoding and frame-emit epilogues, and the decode attention over a
+KV cache at short and long key counts."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from tt2 import ops  # noqa: E402
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _bf(shape, gen, scale=1.0):
+    return (torch.randn(shape, generator=gen) * scale).bfloat16().cuda()
+
+
+@pytest.mark.parametrize("m", [1, 17, 32])
+@pytest.mark.parametrize("n,k", [(81, 512), (256, 80), (256, 256), (1536, 512), (512, 2048), (40, 1000),
+                                 (24, 2104), (16, 8)])
+def test_skinny_gemm_k_regimes(m, n, k):
+    g = torch.Generator().manual_seed(m * 7 + k)
+    A, W = _bf((m, k), g), _bf((n, k), g)
+    bias = torch.randn(n, generator=g).cuda()
+    C = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+    ops.gemm(A, W, C, m, n, k, k, k, n, bias=bias, variant=3)
+    ref = A.double() @ W.double().t() + bias.double()
+    assert rel(C, ref) < 1e-2
+
+
+def test_skinny_ln_prologue_and_kv_scatter():
+    g = torch.Generator().manual_seed(11)
+    m, n, k, Tm = 29, 1536, 512, 40
+    x, br = _bf((m, k), g), _bf((m, k), g)
+    gam, bet = torch.randn(k, generator=g).cuda(), torch.randn(k, generator=g).cuda()
+    W = _bf((n, k), g, 0.05)
+    h = torch.empty(m, k, dtype=torch.bfloat16, device="cuda")
+    C = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+    cache = torch.zeros(m, Tm, 1024, dtype=torch.bfloat16, device="cuda")
+    t = torch.tensor([13], dtype=torch.int32, device="cuda")
+    ops.gemm(x, W, C, m, n, k, k, k, n, a_ln=(br, gam, bet, h, 1e-5), kv=(cache, t, 512, Tm * 1024, 1024),
+             variant=3)
+    hr = F.layer_norm(x.double() + br.double(), (k,), gam.double(), bet.double(), 1e-5)
+    assert rel(h, hr) < 1e-2
+    ref = h.double() @ W.double().t()
+    assert rel(C, ref) < 1e-2
+    assert torch.equal(cache[:, 13], C[:, 512:])
+    assert cache[:, :13].abs().sum().item() == 0 and cache[:, 14:].abs().sum().item() == 0
+
+
+def test_skinny_pe_epilogue():
+    g = torch.Generator().manual_seed(3)
+    m, n, k = 32, 512, 256
+    A, W = _bf((m, k), g), _bf((n, k), g, 0.1)
+    bias = torch.randn(n, generator=g).cuda()
+    pe = torch.randn(50, n, generator=g).cuda()
+    alpha = torch.tensor([0.7], device="cuda")
+    t = torch.tensor([21], dtype=torch.int32, device="cuda")
+    C = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+    ops.gemm(A, W, C, m, n, k, k, k, n, bias=bias, pe=(pe, alpha, t), variant=3)
+    ref = A.double() @ W.double().t() + bias.double() + 0.7 * pe[21].double()
+    assert rel(C, ref) < 1e-2
+
+
+def test_skinny_emit_advances_step():
+    """Three heads GEMMs with the emit epilogue: frames land at t = 0, 1, 2, the
+    previous-frame buffer holds the last one, the seed advances, the arrival counter is
+    re-armed, and frames past t_max are not written."""
+    g = torch.Generator().manual_seed(5)
+    m, n, k, nm, Tm = 32, 81, 512, 80, 2
+    W = _bf((n, k), g, 0.1)
+    bias = torch.randn(n, generator=g).cuda()
+    mel = torch.zeros(m, Tm, nm, device="cuda")
+    stop = torch.zeros(m, Tm, device="cuda")
+    prev = torch.zeros(m, nm, dtype=torch.bfloat16, device="cuda")
+    t = torch.zeros(1, dtype=torch.int32, device="cuda")
+    seed = torch.full((1,), 7, dtype=torch.int32, device="cuda")
+    done = torch.zeros(1, dtype=torch.int32, device="cuda")
+    heads = torch.empty(m, 96, device="cuda")
+    outs = []
+    for step in range(3):
+        A = _bf((m, k), g)
+        ops.gemm(A, W, heads, m, n, k, k, k, 96, bias=bias, emit=(mel, stop, prev, t, seed, done, nm, Tm),
+                 variant=3)
+        ref = A.double() @ W.double().t() + bias.double()
+        outs.append(ref)
+        assert rel(heads[:, :n], ref) < 1e-5
+        assert t.item() == step + 1 and seed.item() == 8 + step and done.item() == 0
+    for s in range(Tm):
+        assert rel(mel[:, s], outs[s][:, :nm]) < 1e-5
+        assert rel(stop[:, s], outs[s][:, nm]) < 1e-5
+    assert rel(prev, outs[Tm - 1][:, :nm]) < 1e-2   # step 2 (t = Tm) writes no frame
+
+
+@pytest.mark.parametrize("k,sp", [(512, 4), (2048, 8), (2048, 16), (512, 2)])
+def test_skinny_split_slabs_ln_combine(k, sp):
+    """Split-K slabs of the skinny kernel folded by tt2_ln_combine = LN(x + bias + X W^T)."""
+    g = torch.Generator().manual_seed(k + sp)
+    m, n = 32, 512
+    A, W = _bf((m, k), g), _bf((n, k), g, 0.05)
+    x = _bf((m, n), g)
+    bias, gam, bet = (torch.randn(n, generator=g).cuda() for _ in range(3))
+    slab = torch.full((sp * m * n,), float("nan"), device="cuda")
+
+    class WS:
+        def get(self, nbytes):
+            assert nbytes <= slab.numel() * 4
+            return slab
+
+    dummy = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+    ops.gemm(A, W, dummy, m, n, k, k, k, n, splits=sp, main_only=True, ws=WS(), variant=3)
+    part = A.double() @ W.double().t()
+    assert rel(slab.view(sp, m, n).sum(0), part) < 1e-5
+    y = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+    ops.ln_combine(x, slab, sp, bias, gam, bet, y, m)
+    ref = F.layer_norm(x.double() + bias.double() + part, (n,), gam.double(), bet.double(), 1e-5)
+    assert rel(y, ref) < 1e-2
+
+
+def _attn_ref(q, K, V, nk, scale):
+    B, H = q.shape[0], q.shape[1] // 64
+    out = torch.zeros(B, H * 64, dtype=torch.float64)
+    for b in range(B):
+        n = int(nk[b])
+        if n == 0:
+            continue
+        for h in range(H):
+            qq = q[b, h * 64:(h + 1) * 64].double().cpu()
+            kk = K[b, :n, h * 64:(h + 1) * 64].double().cpu()
+            vv = V[b, :n, h * 64:(h + 1) * 64].double().cpu()
+            p = torch.softmax(kk @ qq * scale, 0)
+            out[b, h * 64:(h + 1) * 64] = p @ vv
+    return out
+
+
+@pytest.mark.parametrize("t", [0, 6, 33, 257, 1999])
+def test_attn_decode_self_cache(t):
+    g = torch.Generator().manual_seed(t)
+    B, H, d, Tm = 4, 8, 512, 2000
+    qkv = _bf((B, 3 * d), g)
+    cache = _bf((B, Tm, 2 * d), g)
+    tp = torch.tensor([t], dtype=torch.int32, device="cuda")
+    out = torch.empty(B, d, dtype=torch.bfloat16, device="cuda")
+    ops.attn_decode(qkv, cache, cache[:, :, d:], out, 3 * d, Tm * 2 * d, 2 * d, Tm * 2 * d, 2 * d, d, B, H, Tm,
+                    t_ptr=tp, scale=0.125)
+    ref = _attn_ref(qkv[:, :d], cache[:, :, :d], cache[:, :, d:], [t + 1] * B, 0.125)
+    assert rel(out, ref) < 1e-2
+
+
+def test_attn_decode_cross_ragged():
+    g = torch.Generator().manual_seed(9)
+    B, H, d, Tx = 5, 8, 512, 128
+    q = _bf((B, d), g)
+    mem = _bf((B, Tx, 2 * d), g)
+    kl = torch.tensor([128, 1, 0, 77, 9], dtype=torch.int32, device="cuda")
+    out = torch.empty(B, d, dtype=torch.bfloat16, device="cuda")
+    ops.attn_decode(q, mem, mem[:, :, d:], out, d, Tx * 2 * d, 2 * d, Tx * 2 * d, 2 * d, d, B, H, Tx, key_len=kl,
+                    scale=1 / math.sqrt(64))
+    ref = _attn_ref(q, mem[:, :, :d], mem[:, :, d:], kl.tolist(), 0.125)
+    assert rel(out, ref) < 1e-2
+    assert out[2].float().abs().sum().item() == 0   # no keys -> zeros, never NaN

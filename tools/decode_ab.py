@@ -19,9 +19,10 @@ model.eval()
 g = torch.Generator().manual_seed(1)
 text = torch.randint(1, 80, (bench.DEC_B, bench.TX), generator=g).cuda()
 tl = torch.full((bench.DEC_B,), bench.TX, dtype=torch.int32, device="cuda")
-for fuse in (0, 1, 2, 0, 1, 2):
+CFGS = [(1, 4, 8), (2, 4, 8), (3, 4, 8), (3, 2, 4), (3, 4, 16), (3, 8, 16)]
+for fuse, so, sf in CFGS + CFGS:
     dec = Decoder(model.engine, bench.DEC_B, bench.TX, bench.DEC_T)
-    dec.fuse = fuse
+    dec.fuse, dec.split_o, dec.split_f = fuse, so, sf
     dec.encode(text, tl)
     dec.capture()
     dec.reset()
@@ -32,4 +33,4 @@ for fuse in (0, 1, 2, 0, 1, 2):
     dec.decode_loop(400, stop_threshold=None)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print(f"fuse={fuse}: {dt / 400 * 1e6:.1f} us/step")
+    print(f"fuse={fuse} split_o={so} split_f={sf}: {dt / 400 * 1e6:.1f} us/step", flush=True)

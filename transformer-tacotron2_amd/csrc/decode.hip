@@ -7,10 +7,12 @@
 // step (prenet -> 6 layers -> heads -> emit) is captured once as a hipGraph and
 // replayed T times with no host round trip.
 //
-// attn_decode: workgroup = one (batch, head), 4 waves split the keys into
-// contiguous quarters; each wave takes 8 keys per iteration (8 lanes x 16-B per
-// 64-wide head row, for K and for V), keeps an online softmax, and the four
-// partial (max, sum, o[64]) are merged through LDS.  HBM-bound on the cache.
+// attn_decode: workgroup = one (batch, head), 8 waves split the keys into
+// contiguous eighths; each wave takes 32 keys per iteration (8 lanes x 16-B per
+// 64-wide head row, for K and for V; all 8 loads of a lane issued before the
+// first use, so an iteration costs one memory round trip), keeps an online
+// softmax, and the eight partial (max, sum, o[64]) are merged through LDS.
+// Latency-bound at decode sizes; HBM-bound on the cache at long t.
 #include <math.h>
 
 #include "tt2_capi.h"
@@ -43,52 +45,63 @@ struct DecArgs {
   float scale;
 };
 
-template <typename T>
-__global__ __launch_bounds__(NT) void attn_decode_kernel(DecArgs a) {
-  __shared__ float sm[4], sl[4], so[4][D];
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
+  constexpr int U = 4;   // 8-key groups per wave per iteration: 2*U 16-B loads in flight per lane
+  __shared__ float sm[NW], sl[NW], so[NW][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int dc = lane & 7, kg = lane >> 3;   // 8-dim chunk, key slot within an 8-key group
+  float qv[8];
+  load8f(reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld + h * D + dc * 8, qv);
   int nk = a.tk;
   if (a.t_ptr) nk = min(nk, *a.t_ptr + 1);
   if (a.key_len) nk = min(nk, a.key_len[b]);
   nk = max(nk, 0);
-  const int dc = lane & 7, kg = lane >> 3;   // 8-dim chunk, key slot within an 8-key group
-  float qv[8];
-  load8f(reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld + h * D + dc * 8, qv);
   const float c = a.scale * LOG2E;
-  const int per = (nk + 3) / 4;
+  // contiguous per-wave key ranges, multiples of 8 keys
+  const int per = ((nk + NW - 1) / NW + 7) & ~7;
   const int k0 = w * per, k1 = min(nk, k0 + per);
   const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)b * a.k_bstride + h * D + dc * 8;
   const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)b * a.v_bstride + h * D + dc * 8;
   float m = -INFINITY, l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int kb = k0; kb < k1; kb += 8) {
-    const int key = kb + kg;
-    const bool ok = key < k1;
-    float kv[8], vv[8];
-    if (ok) {
-      load8f(K + (int64_t)key * a.k_ld, kv);
-      load8f(V + (int64_t)key * a.v_ld, vv);
-    } else {
+  for (int kb = k0; kb < k1; kb += 8 * U) {
+    float kv[U][8], vv[U][8];
+    // every load of the iteration first (clamped to the last valid key: branch-free)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { kv[j] = 0.f; vv[j] = 0.f; }
+    for (int u = 0; u < U; ++u) {
+      const int key = min(kb + 8 * u + kg, k1 - 1);
+      load8f(K + (int64_t)key * a.k_ld, kv[u]);
+      load8f(V + (int64_t)key * a.v_ld, vv[u]);
     }
-    float s = 0.f;
+    float s[U];
+    float mx = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += qv[j] * kv[j];
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
-    s = ok ? s * c : -INFINITY;
-    float mx = s;
+    for (int u = 0; u < U; ++u) {
+      float x = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x += qv[j] * kv[u][j];
+      x += __shfl_xor(x, 1, 64);
+      x += __shfl_xor(x, 2, 64);
+      x += __shfl_xor(x, 4, 64);
+      s[u] = kb + 8 * u + kg < k1 ? x * c : -INFINITY;
+      mx = fmaxf(mx, s[u]);
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);   // m = -inf -> 0
-    const float p = exp2f(s - mn);       // masked -> 0
-    l = l * alpha + p;
+    const float mn = fmaxf(m, mx);          // finite: the group's first key is always valid
+    const float alpha = exp2f(m - mn);      // m = -inf -> 0
+    l *= alpha;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = o[j] * alpha + p * vv[j];
+    for (int j = 0; j < 8; ++j) o[j] *= alpha;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float p = exp2f(s[u] - mn);     // masked -> 0
+      l += p;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += p * vv[u][j];
+    }
     m = mn;
   }
   // combine the 8 key slots (same m across the wave)
@@ -106,9 +119,11 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(DecArgs a) {
   if (threadIdx.x < D) {
     const int d = threadIdx.x;
     float M = -INFINITY;
-    for (int i = 0; i < 4; ++i) M = fmaxf(M, sm[i]);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) M = fmaxf(M, sm[i]);
     float L = 0.f, O = 0.f;
-    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
       const float f = sm[i] == -INFINITY ? 0.f : exp2f(sm[i] - M);
       L += sl[i] * f;
       O += so[i][d] * f;
@@ -166,8 +181,9 @@ extern "C" int tt2_attn_decode(const tt2_attn_decode_args* p, hipStream_t s) {
   a.q_ld = p->q_ld; a.k_bstride = p->k_bstride; a.k_ld = p->k_ld; a.v_bstride = p->v_bstride; a.v_ld = p->v_ld;
   a.o_ld = p->o_ld; a.key_len = p->key_len; a.t_ptr = p->t_ptr; a.tk = p->tk; a.H = p->heads; a.scale = p->scale;
   dim3 g(p->batch * p->heads);
-  if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(attn_decode_kernel<bf16>, g, dim3(NT), 0, s, a);
-  else hipLaunchKernelGGL(attn_decode_kernel<float>, g, dim3(NT), 0, s, a);
+  // 8 waves per (batch, head): each wave takes 1/8 of the keys, 32 keys per iteration
+  if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL((attn_decode_kernel<bf16, 8>), g, dim3(8 * 64), 0, s, a);
+  else hipLaunchKernelGGL((attn_decode_kernel<float, 8>), g, dim3(8 * 64), 0, s, a);
   return tt2_check_launch(hipGetLastError(), "tt2_attn_decode");
 }
 

@@ -599,85 +599,136 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
 
 // =====================================================================================
 // skinny-M (decode, M <= 32) bf16: out[M, N] = X[M, K] W[N, K]^T.  The problem is a
-// weight stream: every workgroup owns 16 output columns and streams their W rows
-// straight to registers (no LDS round trip), the 4 waves split K, and one MFMA
-// 16x16x32 per 16 rows x 16 columns x 32 k.  Cross-wave sums go through LDS.
+// latency-bound weight stream: every workgroup owns 16 output columns, its 4 waves split
+// K, and each lane issues its WHOLE slice of W (NCH 16-B chunks) before anything else,
+// then its X chunks (or the LayerNorm prologue), so the kernel pays about one memory
+// round trip instead of one per 32-deep K step.  One MFMA 16x16x32 per 16 rows x 16
+// columns x 32 k; cross-wave sums go through LDS.  Decode-step epilogues: KV-cache
+// scatter (QKV projection), scaled positional encoding (pre-net projection) and the
+// frame emit (mel/stop heads: mel_seq / stop_seq / previous frame, then the last
+// workgroup to finish advances the device step counter).
 // =====================================================================================
 constexpr int SK_COLS = 16;
 
-// Decode-step fusions carried by the skinny kernel (tt2_gemm_args a_ln_* / kv_*).
+// Decode-step fusions carried by the skinny kernel (tt2_gemm_args a_ln_* / kv_* / pe_* / emit_*).
 struct SkinnyFuse {
   const bf16* br; const float* gamma; const float* beta; bf16* h_out; float eps;   // LN prologue (gamma != 0)
   bf16* kv; const int32_t* kv_t; int kv_col0; int64_t kv_bstride, kv_ld;           // KV scatter (kv != 0)
+  const float* pe; const float* pe_alpha; const int32_t* pe_t;                     // + alpha * pe[t][n]
+  float* emit_mel; float* emit_stop; bf16* emit_prev; int32_t* emit_t; uint32_t* emit_seed;
+  int32_t* emit_done; int emit_nmels, emit_tmax;                                   // frame emit (heads)
 };
 
 constexpr int SK_LN_LD = 512 + 8;   // bf16 per LDS row of the normalised A (16-B pad)
 
+template <int NCH, bool LN>
 __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t ldx, const bf16* W, int64_t ldw,
-                                                         EpiParams E, int M, int N, int K, SkinnyFuse F) {
+                                                         EpiParams E, int M, int N, int K, SkinnyFuse F,
+                                                         float* slab, int kper) {
   __shared__ float red[4][32][SK_COLS + 1];
   extern __shared__ __attribute__((aligned(16))) bf16 s_h[];   // [32][SK_LN_LD] when F.gamma (K == 512)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * SK_COLS;
-  if (F.gamma) {
-    // h = LN(x + br) for the (<= 32) rows: rows wave, wave + 4, ... with every load issued
-    // before the first reduction; h goes to LDS (the A operand below) and, from one
-    // workgroup, to F.h_out (the next residual)
-    const int c0 = lane * 8;
-    union U { uint4 u; bf16x8 v; } a[8], b[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int row = min(wave + 4 * u, M - 1);
-      a[u].u = *reinterpret_cast<const uint4*>(X + (int64_t)row * ldx + c0);
-      b[u].u = *reinterpret_cast<const uint4*>(F.br + (int64_t)row * ldx + c0);
-    }
-    const f32x4 g0 = *reinterpret_cast<const f32x4*>(F.gamma + c0), g1 = *reinterpret_cast<const f32x4*>(F.gamma + c0 + 4);
-    const f32x4 b0 = *reinterpret_cast<const f32x4*>(F.beta + c0), b1 = *reinterpret_cast<const f32x4*>(F.beta + c0 + 4);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int row = wave + 4 * u;
-      if (row >= M) break;
-      float v[8], sum = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { v[j] = (float)a[u].v[j] + (float)b[u].v[j]; sum += v[j]; }
-      const float mu = wave_sum(sum) / K;
-      float sq = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { const float d = v[j] - mu; sq += d * d; }
-      const float rs = rsqrtf(wave_sum(sq) / K + F.eps);
-      bf16x8 h;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        h[j] = (bf16)((v[j] - mu) * rs * (j < 4 ? g0[j] : g1[j - 4]) + (j < 4 ? b0[j] : b1[j - 4]));
-      *reinterpret_cast<bf16x8*>(s_h + row * SK_LN_LD + c0) = h;
-      if (blockIdx.x == 0) *reinterpret_cast<bf16x8*>(F.h_out + (int64_t)row * K + c0) = h;
-    }
-    __syncthreads();
-  }
-  const int kq = ((K + 127) / 128) * 32;                 // per-wave K slice, multiple of 32
-  const int kb = wave * kq, ke = min(K, kb + kq);
   const int r = lane & 15, g = lane >> 4;
   const int n = n0 + r;
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   const bool nok = n < N, r0ok = r < M, r1ok = r + 16 < M;
+  // device scalars of the epilogue, issued up front
+  const uint32_t seed = E.drop.thr ? *E.drop.seed : 0u;
+  const int kv_t = F.kv ? *F.kv_t : 0;
+  const int pe_t = F.pe ? *F.pe_t : 0;
+  const float pe_al = F.pe ? *F.pe_alpha : 0.f;
+  const int em_t = F.emit_mel ? *F.emit_t : 0;
   const bf16* wrow = W + (int64_t)(nok ? n : 0) * ldw;
   const bf16* x0 = X + (int64_t)(r0ok ? r : 0) * ldx;
   const bf16* x1 = X + (int64_t)(r1ok ? r + 16 : 0) * ldx;
   union U { uint4 u; bf16x8 v; };
-  for (int k = kb; k < ke; k += 32) {
-    const int kk = k + 8 * g;
-    const bool kok = kk < ke;
-    U w, a0, a1;
-    w.u = (nok && kok) ? *reinterpret_cast<const uint4*>(wrow + kk) : make_uint4(0, 0, 0, 0);
-    if (F.gamma) {
-      a0.u = (r0ok && kok) ? *reinterpret_cast<const uint4*>(s_h + r * SK_LN_LD + kk) : make_uint4(0, 0, 0, 0);
-      a1.u = (r1ok && kok) ? *reinterpret_cast<const uint4*>(s_h + (r + 16) * SK_LN_LD + kk) : make_uint4(0, 0, 0, 0);
-    } else {
-      a0.u = (r0ok && kok) ? *reinterpret_cast<const uint4*>(x0 + kk) : make_uint4(0, 0, 0, 0);
-      a1.u = (r1ok && kok) ? *reinterpret_cast<const uint4*>(x1 + kk) : make_uint4(0, 0, 0, 0);
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  // split-K (slab != 0): workgroup row blockIdx.y takes k in [kbeg, kend) and stores its raw
+  // partial sums to slab[blockIdx.y][m][n] (f32, no epilogue; tt2_ln_combine sums them)
+  const int kbeg = slab ? blockIdx.y * kper : 0;
+  const int kend = slab ? min(K, kbeg + kper) : K;
+  float e_bias = 0.f, e_res0 = 0.f, e_res1 = 0.f, e_pe = 0.f;
+  const int ecol = threadIdx.x & 15, erow = threadIdx.x >> 4, enn = n0 + ecol;
+  for (int ks = kbeg; ks < kend; ks += 4 * NCH * 32) {
+    const int kb = ks + wave * (NCH * 32);
+    U w[NCH], a0[NCH], a1[NCH];
+    // (1) this lane's whole W slice: branch-free (an out-of-range chunk reads the zero page)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int kk = kb + 32 * c + 8 * g;
+      w[c].u = *reinterpret_cast<const uint4*>(nok && kk < kend ? (const void*)(wrow + kk) : (const void*)g_zero_page);
     }
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0.v, w.v, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1.v, w.v, acc1, 0, 0, 0);
+    if constexpr (LN) {
+      // (2a) h = LN(x + br) for the (<= 32) rows (K == 512, one pass): rows wave, wave + 4, ...,
+      // every load issued before the first reduction; h goes to LDS (the A operand) and,
+      // from workgroup 0, to F.h_out (the next residual)
+      const int c0 = lane * 8;
+      U xa[8], xb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int row = min(wave + 4 * u, M - 1);
+        xa[u].u = *reinterpret_cast<const uint4*>(X + (int64_t)row * ldx + c0);
+        xb[u].u = *reinterpret_cast<const uint4*>(F.br + (int64_t)row * ldx + c0);
+      }
+      const f32x4 g0 = *reinterpret_cast<const f32x4*>(F.gamma + c0), g1 = *reinterpret_cast<const f32x4*>(F.gamma + c0 + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(F.beta + c0), b1 = *reinterpret_cast<const f32x4*>(F.beta + c0 + 4);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int row = wave + 4 * u;
+        float v[8], sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { v[j] = (float)xa[u].v[j] + (float)xb[u].v[j]; sum += v[j]; }
+        const float mu = wave_sum(sum) / K;
+        float sq = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = v[j] - mu; sq += d * d; }
+        const float rs = rsqrtf(wave_sum(sq) / K + F.eps);
+        bf16x8 h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          h[j] = (bf16)((v[j] - mu) * rs * (j < 4 ? g0[j] : g1[j - 4]) + (j < 4 ? b0[j] : b1[j - 4]));
+        if (row < M) {
+          *reinterpret_cast<bf16x8*>(s_h + row * SK_LN_LD + c0) = h;
+          if (blockIdx.x == 0) *reinterpret_cast<bf16x8*>(F.h_out + (int64_t)row * K + c0) = h;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int kk = kb + 32 * c + 8 * g;
+        const bool ok = kk < K;
+        a0[c].u = (r0ok && ok) ? *reinterpret_cast<const uint4*>(s_h + r * SK_LN_LD + kk) : z4;
+        a1[c].u = (r1ok && ok) ? *reinterpret_cast<const uint4*>(s_h + (r + 16) * SK_LN_LD + kk) : z4;
+      }
+    } else {
+      // (2b) the X chunks, also all in flight
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int kk = kb + 32 * c + 8 * g;
+        a0[c].u = *reinterpret_cast<const uint4*>(r0ok && kk < kend ? (const void*)(x0 + kk) : (const void*)g_zero_page);
+        a1[c].u = *reinterpret_cast<const uint4*>(r1ok && kk < kend ? (const void*)(x1 + kk) : (const void*)g_zero_page);
+      }
+      // keep every load above the first MFMA (the scheduler would otherwise interleave
+      // them and pay one memory round trip per pair)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ks == kbeg && !slab) {
+      // the epilogue's own operands (bias, residual, PE row), in flight behind the
+      // operand loads instead of a second round trip after the reduction
+      const bool ec = enn < N;
+      if (E.bias && ec) e_bias = E.bias[enn];
+      if (E.res && ec) {
+        if (erow < M) e_res0 = ld_any(E.res, (int64_t)erow * E.ldr + enn, E.res_dt);
+        if (erow + 16 < M) e_res1 = ld_any(E.res, (int64_t)(erow + 16) * E.ldr + enn, E.res_dt);
+      }
+      if (F.pe && ec) e_pe = pe_al * F.pe[(int64_t)pe_t * N + enn];
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c].v, w[c].v, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[c].v, w[c].v, acc1, 0, 0, 0);
+    }
   }
   // acc layout: row 4*(lane>>4) + i, col lane & 15
 #pragma unroll
@@ -686,16 +737,53 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t 
     red[wave][16 + 4 * g + i][r] = acc1[i];
   }
   __syncthreads();
-  const uint32_t seed = E.drop.thr ? *E.drop.seed : 0u;
-  for (int o = threadIdx.x; o < 32 * SK_COLS; o += NT) {
-    const int row = o / SK_COLS, col = o % SK_COLS;
-    const int m = row, nn = n0 + col;
+  if (slab) {
+#pragma unroll
+    for (int hrow = 0; hrow < 2; ++hrow) {
+      const int m = erow + 16 * hrow;
+      if (m < M && enn < N)
+        slab[((int64_t)blockIdx.y * M + m) * N + enn] =
+            (red[0][m][ecol] + red[1][m][ecol]) + (red[2][m][ecol] + red[3][m][ecol]);
+    }
+    return;
+  }
+  // bias / residual were prefetched: the epilogue proper runs without them
+  EpiParams Ep = E;
+  Ep.bias = nullptr;
+  Ep.res = nullptr;
+  Ep.alpha = 1.f;
+#pragma unroll
+  for (int hrow = 0; hrow < 2; ++hrow) {
+    const int row = erow + 16 * hrow, col = ecol;
+    const int m = row, nn = enn;
     if (m < M && nn < N) {
       const float v = (red[0][row][col] + red[1][row][col]) + (red[2][row][col] + red[3][row][col]);
-      const float o = epi_value(E, seed, m, nn, v);
-      st_any(E.c, (int64_t)m * E.ldc + nn, E.c_dt, o);
+      float y = epi_value(Ep, seed, m, nn, E.alpha * v + e_bias + (hrow ? e_res1 : e_res0));
+      y += e_pe;
+      st_any(E.c, (int64_t)m * E.ldc + nn, E.c_dt, y);
       if (F.kv && nn >= F.kv_col0)
-        F.kv[(int64_t)m * F.kv_bstride + (int64_t)(*F.kv_t) * F.kv_ld + (nn - F.kv_col0)] = (bf16)o;
+        F.kv[(int64_t)m * F.kv_bstride + (int64_t)kv_t * F.kv_ld + (nn - F.kv_col0)] = (bf16)y;
+      if (F.emit_mel && em_t < F.emit_tmax) {
+        if (nn < F.emit_nmels) {
+          F.emit_mel[((int64_t)m * F.emit_tmax + em_t) * F.emit_nmels + nn] = y;
+          F.emit_prev[(int64_t)m * F.emit_nmels + nn] = (bf16)y;
+        } else if (nn == F.emit_nmels) {
+          F.emit_stop[(int64_t)m * F.emit_tmax + em_t] = y;
+        }
+      }
+    }
+  }
+  if (F.emit_mel) {
+    // every workgroup has read the step counter (it addressed its stores with it): the
+    // last one to arrive advances it (and the dropout seed) and re-arms the counter
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int prev = __hip_atomic_fetch_add(F.emit_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == (int)gridDim.x - 1) {
+        *F.emit_done = 0;
+        *F.emit_t = em_t + 1;
+        if (F.emit_seed) *F.emit_seed += 1u;
+      }
     }
   }
 }
@@ -1349,14 +1437,25 @@ extern "C" size_t tt2_gemm_workspace_size(const tt2_gemm_args* a) {
 static int gemm_plan(const tt2_gemm_args* a) {
   const int var = a->kernel_variant;
   const int64_t a_inner = a->trans_a ? a->m : a->k, b_inner = a->trans_b ? a->n : a->k;
+  // skinny split-K exists only as raw partial slabs (main_only) for tt2_ln_combine
   const bool skinny = a->dtype_in == TT2_BF16 && a->m <= 32 && !a->trans_a && !a->trans_b && a->k % 8 == 0 &&
-                      a->a_conv_t == 0 && a->splits <= 1 && (var == 0 || var == 3);
+                      a->a_conv_t == 0 && (a->splits <= 1 || a->main_only) && (var == 0 || var == 3);
+  if (skinny && a->splits > 1 && (a->a_ln_gamma || a->kv_cache || a->pe_table || a->emit_mel ||
+                                  a->k % (32 * a->splits) != 0))
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: skinny split-K slabs need k % (32 splits) == 0, no fusions"), -1;
   if ((a->a_ln_gamma || a->kv_cache) && !skinny)
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln / kv fusions need the skinny path (bf16, m <= 32, NT)"), -1;
   if (a->a_ln_gamma && (a->k != 512 || a->lda != a->k || !a->a_ln_branch || !a->a_ln_beta || !a->a_ln_out))
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln needs k == lda == 512, branch, beta and out"), -1;
   if (a->kv_cache && (!a->kv_t || a->dtype_out != TT2_BF16))
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: kv scatter needs kv_t and a bf16 output"), -1;
+  if ((a->pe_table || a->emit_mel) && !skinny)
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: pe / emit epilogues need the skinny path (bf16, m <= 32, NT)"), -1;
+  if (a->pe_table && (!a->pe_alpha || !a->pe_t))
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: pe epilogue needs pe_alpha and pe_t"), -1;
+  if (a->emit_mel && (!a->emit_stop || !a->emit_prev || !a->emit_t || !a->emit_done || a->emit_nmels >= a->n ||
+                      a->emit_nmels <= 0 || a->emit_tmax <= 0))
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: emit epilogue needs stop/prev/t/done and n > emit_nmels"), -1;
   if (skinny) return 3;
   // LDS-DMA kernels: bf16, every 16-B chunk either fully inside or fully outside its row
   const bool v2 = a->dtype_in == TT2_BF16 && var != 1 && a_inner % 8 == 0 && b_inner % 8 == 0;
@@ -1444,11 +1543,28 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   if (plan == 3) {   // skinny-M weight-streaming path (decode step)
     SkinnyFuse F{reinterpret_cast<const bf16*>(a->a_ln_branch), a->a_ln_gamma, a->a_ln_beta,
                  reinterpret_cast<bf16*>(a->a_ln_out), a->a_ln_eps, reinterpret_cast<bf16*>(a->kv_cache), a->kv_t,
-                 a->kv_col0, a->kv_bstride, a->kv_ld};
+                 a->kv_col0, a->kv_bstride, a->kv_ld, a->pe_table, a->pe_alpha, a->pe_t, a->emit_mel, a->emit_stop,
+                 reinterpret_cast<bf16*>(a->emit_prev), a->emit_t, a->emit_seed, a->emit_done, a->emit_nmels,
+                 a->emit_tmax};
     const size_t lds = a->a_ln_gamma ? 32 * SK_LN_LD * sizeof(bf16) : 0;
-    hipLaunchKernelGGL(gemm_skinny_kernel, dim3((a->n + SK_COLS - 1) / SK_COLS), dim3(NT), lds, stream,
-                       reinterpret_cast<const bf16*>(a->a), a->lda, reinterpret_cast<const bf16*>(a->b), a->ldb, ep,
-                       a->m, a->n, a->k, F);
+    // split-K (splits > 1, main_only): raw partial slabs [splits][m][n] f32 in the workspace
+    const int sp = a->splits > 1 ? a->splits : 1;
+    const int kper = sp > 1 ? ((a->k + sp - 1) / sp + 31) / 32 * 32 : a->k;
+    float* slab = sp > 1 ? reinterpret_cast<float*>(a->workspace) : nullptr;
+    const dim3 grid((a->n + SK_COLS - 1) / SK_COLS, sp > 1 ? (a->k + kper - 1) / kper : 1);
+    const bf16* X = reinterpret_cast<const bf16*>(a->a);
+    const bf16* Wt = reinterpret_cast<const bf16*>(a->b);
+    // per-wave K slice = NCH x 32: one pass for K <= 4 * NCH * 32
+    const int nch = kper <= 128 ? 1 : kper <= 256 ? 2 : kper <= 512 ? 4 : kper <= 1024 ? 8 : 16;
+#define TT2_SK(NCH, LN) hipLaunchKernelGGL((gemm_skinny_kernel<NCH, LN>), grid, dim3(NT), lds, stream, X, a->lda, Wt, \
+                                           a->ldb, ep, a->m, a->n, a->k, F, slab, kper)
+    if (a->a_ln_gamma) TT2_SK(4, true);   // k == 512 (checked by the plan)
+    else if (nch == 1) TT2_SK(1, false);
+    else if (nch == 2) TT2_SK(2, false);
+    else if (nch == 4) TT2_SK(4, false);
+    else if (nch == 8) TT2_SK(8, false);
+    else TT2_SK(16, false);
+#undef TT2_SK
     return tt2_check_launch(hipGetLastError(), "tt2_gemm(skinny)");
   }
   if (plan == 13) {

@@ -91,6 +91,46 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(LnArgs a) {
   if (lane == 0 && a.mean) { a.mean[row] = mean; a.rstd[row] = rstd; }
 }
 
+// Decode-step residual combine + LayerNorm: y = LN(x + bias + sum_s part[s]) over the
+// 512 columns of a row, where part holds the raw partial sums of a skinny split-K
+// projection ([S][M][512] f32).  One wave per row, every load (x, the S slabs, bias,
+// gamma, beta) issued before the first reduction: one memory round trip.
+template <int S>
+__global__ __launch_bounds__(NT) void ln_combine_kernel(const bf16* x, const float* part, const float* bias,
+                                                        const float* gamma, const float* beta, bf16* y, int M,
+                                                        float eps) {
+  constexpr int C = 512;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int c0 = lane * 8;
+  float v[8], p[S][8], bb[8], g[8], be[8];
+  ld8(x + (int64_t)row * C + c0, v);
+#pragma unroll
+  for (int s = 0; s < S; ++s) ld8(part + ((int64_t)s * M + row) * C + c0, p[s]);
+  ld8(bias + c0, bb);
+  ld8(gamma + c0, g);
+  ld8(beta + c0, be);
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float a = bb[j];
+#pragma unroll
+    for (int s = 0; s < S; ++s) a += p[s][j];   // fixed order: reproducible
+    v[j] += a;
+    sum += v[j];
+  }
+  const float mean = wave_sum(sum) / C;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { const float d = v[j] - mean; sq += d * d; }
+  const float rstd = rsqrtf(wave_sum(sq) / C + eps);
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (v[j] - mean) * rstd * g[j] + be[j];
+  st8(y + (int64_t)row * C + c0, o);
+}
+
 // Backward: 8 waves per workgroup, one 512-wide row per wave at a time, software-
 // pipelined: the raw x / branch / dy chunks of the wave's next row are loaded before the
 // current row is reduced, so every wave always has a row of loads in flight.  The
@@ -508,6 +548,26 @@ extern "C" int tt2_layernorm_fwd(const tt2_ln_args* p, hipStream_t s) {
   if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(ln_fwd_kernel<bf16>, g, dim3(NT), 0, s, a);
   else hipLaunchKernelGGL(ln_fwd_kernel<float>, g, dim3(NT), 0, s, a);
   return tt2_check_launch(hipGetLastError(), "tt2_layernorm_fwd");
+}
+
+extern "C" int tt2_ln_combine(const void* x, const float* part, int32_t splits, const float* bias,
+                              const float* gamma, const float* beta, void* y, int32_t m, int32_t c, float eps,
+                              hipStream_t s) {
+  if (c != 512) return tt2_set_error(TT2_E_INVALID, "tt2_ln_combine: c must be 512");
+  if (!x || !part || !bias || !gamma || !beta || !y) return tt2_set_error(TT2_E_INVALID, "tt2_ln_combine: null");
+  if (m <= 0) return TT2_OK;
+  const dim3 g((m + 3) / 4);
+  const bf16* X = reinterpret_cast<const bf16*>(x);
+  bf16* Y = reinterpret_cast<bf16*>(y);
+  switch (splits) {
+    case 1: hipLaunchKernelGGL(ln_combine_kernel<1>, g, dim3(NT), 0, s, X, part, bias, gamma, beta, Y, m, eps); break;
+    case 2: hipLaunchKernelGGL(ln_combine_kernel<2>, g, dim3(NT), 0, s, X, part, bias, gamma, beta, Y, m, eps); break;
+    case 4: hipLaunchKernelGGL(ln_combine_kernel<4>, g, dim3(NT), 0, s, X, part, bias, gamma, beta, Y, m, eps); break;
+    case 8: hipLaunchKernelGGL(ln_combine_kernel<8>, g, dim3(NT), 0, s, X, part, bias, gamma, beta, Y, m, eps); break;
+    case 16: hipLaunchKernelGGL(ln_combine_kernel<16>, g, dim3(NT), 0, s, X, part, bias, gamma, beta, Y, m, eps); break;
+    default: return tt2_set_error(TT2_E_INVALID, "tt2_ln_combine: splits must be 1, 2, 4, 8 or 16");
+  }
+  return tt2_check_launch(hipGetLastError(), "tt2_ln_combine");
 }
 
 static int ln_bwd_blocks(int m) {

@@ -42,6 +42,9 @@ class GemmArgs(C.Structure):
         ("a_ln_branch", vp), ("a_ln_gamma", vp), ("a_ln_beta", vp), ("a_ln_out", vp), ("a_ln_eps", f32),
         ("kv_cache", vp), ("kv_t", vp), ("kv_col0", i32), ("kv_bstride", i64), ("kv_ld", i64),
         ("main_only", i32),
+        ("pe_table", vp), ("pe_alpha", vp), ("pe_t", vp),
+        ("emit_mel", vp), ("emit_stop", vp), ("emit_prev", vp), ("emit_t", vp), ("emit_seed", vp),
+        ("emit_done", vp), ("emit_nmels", i32), ("emit_tmax", i32),
     ]
 
 
@@ -196,6 +199,7 @@ SIGNATURES.update({
     "tt2_layernorm_fwd": ([P_(LnArgs), vp], C.c_int),
     "tt2_layernorm_bwd_workspace_size": ([P_(LnArgs)], sz),
     "tt2_layernorm_bwd": ([P_(LnArgs), vp], C.c_int),
+    "tt2_ln_combine": ([vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp], C.c_int),
     "tt2_batchnorm_workspace_size": ([P_(BnArgs)], sz),
     "tt2_batchnorm_fwd": ([P_(BnArgs), vp], C.c_int),
     "tt2_batchnorm_bwd": ([P_(BnArgs), vp], C.c_int),

@@ -26,6 +26,19 @@ from .engine import TTSEngine
 from .ops import NO_DROP, Drop
 
 
+class _Slab:
+    """Fixed buffer for the split-K partial slabs (a Workspace stand-in that never grows,
+    so the captured graph keeps its pointer)."""
+
+    def __init__(self, t: torch.Tensor):
+        self.t = t
+
+    def get(self, nbytes: int) -> torch.Tensor:
+        if nbytes > self.t.numel() * 4:
+            raise ValueError(f"decode slab too small: {nbytes} bytes")
+        return self.t
+
+
 class Decoder:
     def __init__(self, engine: TTSEngine, batch: int, text_len: int, t_max: int, prenet_dropout: bool = False,
                  seed: int = 0):
@@ -54,11 +67,19 @@ class Decoder:
         self.stop_seq = z(B, t_max, dt=torch.float32)
         self.t = torch.zeros(1, dtype=torch.int32, device=dev)
         self.seed = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.emit_done = torch.zeros(1, dtype=torch.int32, device=dev)   # heads-GEMM arrival counter
+        # bf16: the scaled PE rides in the pre-net projection's epilogue and the frame emit
+        # in the heads GEMM's (skinny-path epilogues; 2 launches fewer per step)
+        self.fused_io = cd == torch.bfloat16 and batch <= 32
         self.graph = None
-        # bf16 decode-step fusions in the skinny GEMM: 0 none, 1 KV-cache scatter in the
-        # QKV epilogue, 2 also the LayerNorms as GEMM prologues (measured slower: every
-        # workgroup recomputes the 32-row statistics on its critical path)
-        self.fuse = 1
+        # bf16 decode-step schedules: 0 no fusion, 1 KV-cache scatter in the QKV epilogue,
+        # 2 also the LayerNorms as GEMM prologues (every workgroup recomputes the 32-row
+        # statistics), 3 (default) KV scatter + split-K o / co / ffn2 whose slabs a
+        # residual + LayerNorm combine kernel folds (tools/decode_ab.py measures them).
+        # The skinny-path fusions need batch <= 32; larger batches run unfused.
+        self.fuse = 3 if cd == torch.bfloat16 and batch <= 32 else 0
+        self.split_o, self.split_f = 4, 8
+        self.slab = _Slab(torch.zeros(16 * 32 * d, dtype=torch.float32, device=dev))
 
     # ----------------------------------------------------------------- one step
     def step(self):
@@ -75,8 +96,13 @@ class Decoder:
             drop=d1)
         lin(self.p1, e.W("dec.fc2.w"), self.p2, B, c.dec_prenet, c.dec_prenet, bias=e.P("dec.fc2.b"), act=ACT_RELU,
             drop=d2)
-        lin(self.p2, e.W("dec.proj.w"), self.proj, B, d, c.dec_prenet, bias=e.P("dec.proj.b"))
-        ops.posenc_fwd(self.proj, e.P("dec.alpha"), e.pe, self.x0, B, 1, t_ptr=self.t)
+        if self.fused_io:
+            # x0 = proj(p2) + alpha * pe[t], the scaled PE in the projection's epilogue
+            lin(self.p2, e.W("dec.proj.w"), self.x0, B, d, c.dec_prenet, bias=e.P("dec.proj.b"),
+                pe=(e.pe, e.P("dec.alpha"), self.t))
+        else:
+            lin(self.p2, e.W("dec.proj.w"), self.proj, B, d, c.dec_prenet, bias=e.P("dec.proj.b"))
+            ops.posenc_fwd(self.proj, e.P("dec.alpha"), e.pe, self.x0, B, 1, t_ptr=self.t)
         mkv = A["mkv"]
         kvld = c.n_dec * 2 * d
         eps = c.ln_eps
@@ -84,6 +110,8 @@ class Decoder:
         # normalises its A rows and publishes the LN output for the residual path), and
         # the K/V columns of the QKV projection go straight into the KV cache: 8 kernels
         # per layer instead of 12.
+        if e.cd == torch.bfloat16 and self.fuse == 3:
+            return self._step_layers_split(B, d, F, H, scale)
         if e.cd != torch.bfloat16 or self.fuse < 2:
             return self._step_layers_unfused(lin, B, d, F, H, scale, kv_fused=e.cd == torch.bfloat16 and self.fuse == 1)
         x, ln_prev = self.x0, None          # ln_prev: (branch, gamma, beta, out) pending on x
@@ -114,8 +142,64 @@ class Decoder:
             # LN3(h2 + f2) is fused into the next consumer (next layer's QKV, or the heads)
             x, ln_prev = self.h2, (self.f2, e.P(p + "ln3.g"), e.P(p + "ln3.b"), xs[l % 2])
         lin(x, e.W("heads.w"), self.heads, B, c.n_mels + 1, d, bias=e.P("heads.b"), ldo=96,
-            a_ln=ln_prev + (eps,))
-        self._emit()
+            a_ln=ln_prev + (eps,), emit=self._emit_args())
+
+    def _step_layers_split(self, B, d, F, H, scale):
+        """Decoder layers with split-K output projections: o, co and ffn2 (the K = 512 /
+        2048 GEMMs whose 32 column tiles would leave most CUs idle) write raw partial slabs
+        from splits x more workgroups, and tt2_ln_combine folds the slabs + bias + residual
+        into the sublayer's LayerNorm.  11 launches per layer, as the unfused path, but the
+        weight stream of those three is spread over 4-8x the CUs."""
+        e, c, A = self.e, self.e.cfg, self.A
+        lin = e._lin
+        x = self.x0
+        mkv = A["mkv"]
+        kvld = c.n_dec * 2 * d
+        eps = c.ln_eps
+        slab = self.slab
+
+        def split(xin, w, n, k, sp):
+            ops.gemm(xin, w, self.o, B, n, k, k, k, n, splits=sp, main_only=True, ws=slab)
+
+        for l in range(c.n_dec):
+            p = f"dec{l}."
+            cache = self.cache[l]
+            lin(x, e.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"),
+                kv=(cache, self.t, d, self.Tmax * 2 * d, 2 * d))
+            ops.attn_decode(self.qkv, cache, cache[:, :, d:], self.att, 3 * d, self.Tmax * 2 * d, 2 * d,
+                            self.Tmax * 2 * d, 2 * d, d, B, H, self.Tmax, t_ptr=self.t, scale=scale)
+            split(self.att, e.W(p + "o.w"), d, d, self.split_o)
+            ops.ln_combine(x, slab.t, self.split_o, e.P(p + "o.b"), e.P(p + "ln1.g"), e.P(p + "ln1.b"), self.h1, B,
+                           eps)
+            lin(self.h1, e.W(p + "cq.w"), self.cq, B, d, d, bias=e.P(p + "cq.b"))
+            ko = 2 * d * l
+            ops.attn_decode(self.cq, mkv[:, ko:], mkv[:, ko + d:], self.catt, d, self.Tx * kvld, kvld,
+                            self.Tx * kvld, kvld, d, B, H, self.Tx, key_len=A["text_len"], scale=scale)
+            split(self.catt, e.W(p + "co.w"), d, d, self.split_o)
+            ops.ln_combine(self.h1, slab.t, self.split_o, e.P(p + "co.b"), e.P(p + "ln2.g"), e.P(p + "ln2.b"),
+                           self.h2, B, eps)
+            lin(self.h2, e.W(p + "ffn1.w"), self.f1, B, F, d, bias=e.P(p + "ffn1.b"), act=ACT_RELU)
+            split(self.f1, e.W(p + "ffn2.w"), d, F, self.split_f)
+            xn = self.xa if x is not self.xa else self.xb
+            ops.ln_combine(self.h2, slab.t, self.split_f, e.P(p + "ffn2.b"), e.P(p + "ln3.g"), e.P(p + "ln3.b"),
+                           xn, B, eps)
+            x = xn
+        self._heads(x)
+
+    def _emit_args(self):
+        """Frame emit fused into the heads GEMM (bf16 skinny path): mel/stop/prev stores,
+        then the last workgroup advances the step counter and the dropout seed."""
+        return (self.mel_seq, self.stop_seq, self.prev, self.t, self.seed, self.emit_done, self.e.cfg.n_mels,
+                self.Tmax)
+
+    def _heads(self, x):
+        c, e = self.e.cfg, self.e
+        if self.fused_io:
+            e._lin(x, e.W("heads.w"), self.heads, self.B, c.n_mels + 1, c.d_model, bias=e.P("heads.b"), ldo=96,
+                   emit=self._emit_args())
+        else:
+            e._lin(x, e.W("heads.w"), self.heads, self.B, c.n_mels + 1, c.d_model, bias=e.P("heads.b"), ldo=96)
+            self._emit()
 
     def _emit(self):
         c = self.e.cfg
@@ -152,8 +236,7 @@ class Decoder:
             lin(self.f1, e.W(p + "ffn2.w"), self.f2, B, d, F, bias=e.P(p + "ffn2.b"))
             ops.layernorm_fwd(self.h2, self.f2, e.P(p + "ln3.g"), e.P(p + "ln3.b"), xn, None, None, B, c.ln_eps)
             x, xn = xn, (self.xb if xn is self.xa else self.xa)
-        lin(x, e.W("heads.w"), self.heads, B, c.n_mels + 1, d, bias=e.P("heads.b"), ldo=96)
-        self._emit()
+        self._heads(x)
 
     # ----------------------------------------------------------------- driver
     def reset(self):

@@ -60,7 +60,8 @@ _WS = Workspace()
 def gemm_args(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bias=None, res=None, ldr=0,
               gate=None, ldg=0, gate_scale=1.0, alpha=1.0, beta=0.0, act=0, drop: Drop = NO_DROP, splits=1,
               a_conv=None, b_conv=None, ws: Workspace | None = None, variant: int = 0, a_ksum=None,
-              a_ksum_beta=0.0, a_ln=None, kv=None, main_only=False, defer_ws: bool = False) -> GemmArgs:
+              a_ksum_beta=0.0, a_ln=None, kv=None, pe=None, emit=None, main_only=False,
+              defer_ws: bool = False) -> GemmArgs:
     """Build the tt2_gemm_args of one request (see tt2_capi.h).  defer_ws: only size the
     split-K workspace (ws_bytes); the caller places it."""
     L = lib()
@@ -93,6 +94,14 @@ def gemm_args(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bia
     if kv is not None:
         cache, t_ptr, col0, bstride, ld = kv
         g.kv_cache, g.kv_t, g.kv_col0, g.kv_bstride, g.kv_ld = ptr(cache), ptr(t_ptr), col0, bstride, ld
+    if pe is not None:
+        table, alpha, t_ptr = pe
+        g.pe_table, g.pe_alpha, g.pe_t = ptr(table), ptr(alpha), ptr(t_ptr)
+    if emit is not None:
+        mel_seq, stop_seq, prev, t_ptr, seed, done, n_mels, t_max = emit
+        g.emit_mel, g.emit_stop, g.emit_prev = ptr(mel_seq), ptr(stop_seq), ptr(prev)
+        g.emit_t, g.emit_seed, g.emit_done = ptr(t_ptr), ptr(seed), ptr(done)
+        g.emit_nmels, g.emit_tmax = n_mels, t_max
     g.splits = max(1, splits)
     g.main_only = int(main_only)   # dev measurement: skip the split-K reduce
     if g.splits > 1:
@@ -107,7 +116,10 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, **kw):
     """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see tt2_capi.h tt2_gemm_args.
     a_ksum (f32 [m], bf16 trans_a only): a_ksum = a_ksum_beta * a_ksum + sum_k A(m,k).
     a_ln = (branch, gamma, beta, out, eps): multiply LN(A + branch), writing it to out (skinny path).
-    kv = (cache, t_ptr, col0, bstride, ld): also store columns >= col0 to the KV cache at step *t_ptr."""
+    kv = (cache, t_ptr, col0, bstride, ld): also store columns >= col0 to the KV cache at step *t_ptr.
+    pe = (table, alpha, t_ptr): add alpha * table[*t_ptr] to every output row (skinny path).
+    emit = (mel_seq, stop_seq, prev, t_ptr, seed, done, n_mels, t_max): the decode frame emit
+    (see tt2_capi.h), which also advances *t_ptr."""
     L = lib()
     g = gemm_args(a, b, c, m, n, k, lda, ldb, ldc, **kw)
     if PROBE is not None:
@@ -271,6 +283,12 @@ def layernorm_fwd(x, branch, gamma, beta, y, mean, rstd, m, eps=1e-5, drop: Drop
     a.m, a.c, a.dtype, a.eps = m, x.shape[-1], dt(x), eps
     _drop_into(a, drop)
     check(L.tt2_layernorm_fwd(C.byref(a), stream_ptr()), "tt2_layernorm_fwd")
+
+
+def ln_combine(x, part, splits, bias, gamma, beta, y, m, eps=1e-5):
+    """y = LN(x + bias + sum_s part[s]) (decode step; part = a skinny split-K GEMM's slabs)."""
+    check(lib().tt2_ln_combine(x.data_ptr(), part.data_ptr(), splits, bias.data_ptr(), gamma.data_ptr(),
+                               beta.data_ptr(), y.data_ptr(), m, x.shape[-1], eps, stream_ptr()), "tt2_ln_combine")
 
 
 def layernorm_bwd(dy, x, branch, gamma, mean, rstd, dx, dbranch, dgamma, dbeta, m, drop: Drop = NO_DROP,
