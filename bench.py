@@ -178,6 +178,46 @@ def roofline(model, text, tl, mel, ml):
     }
 
 
+LF_B, LF_T = 64, 2000
+LF_STEP_BYTES = 4.45e7 + 6 * LF_B * TX * 2 * 512 * 2     # weights + cross K/V per step
+LF_KEY_BYTES = 6 * LF_B * 2 * 512 * 2                     # self K/V bytes per cached position
+
+
+def longform_bench(model):
+    """cfg5: long-form AR decode, B=64, 128 phonemes, T_max=2000, per-utterance frame caps
+    ~ U[1000, 2000] (seeded) end the loop early; frames/s = sum of caps / wall time."""
+    from tt2.infer import Decoder
+    g = torch.Generator().manual_seed(5)
+    text = torch.randint(1, 80, (LF_B, TX), generator=g).cuda()
+    tl = torch.full((LF_B,), TX, dtype=torch.int32, device="cuda")
+    caps = torch.randint(1000, LF_T + 1, (LF_B,), generator=g)
+    was = model.engine.training
+    model.eval()
+    dec = Decoder(model.engine, LF_B, TX, LF_T)
+    dec.encode(text, tl)
+    dec.capture()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dec.encode(text, tl)
+    dec.reset()
+    # random weights give a meaningless stop head: the seeded caps stand in for the stop
+    # positions (the loop polls them every 32 frames exactly as it polls stop flags)
+    n = dec.decode_loop(LF_T, stop_threshold=None, limits=caps)
+    mel, out_len = dec.postnet(n, None, caps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    model.train(was)
+    frames = int(out_len.sum())
+    algo = n * LF_STEP_BYTES + LF_KEY_BYTES * n * (n + 1) / 2
+    return {"value": round(frames / dt, 1), "unit": "frames/s", "ms_per_run": round(dt * 1e3, 2),
+            "steps_run": n, "frames": frames, "ms_per_frame_step": round(dt / n * 1e3, 4),
+            "config": {"workload": "long-form AR decode: encoder + hipGraph decode steps until every utterance "
+                                   "stops or reaches its cap + post-net", "batch": LF_B, "text_len": TX,
+                       "t_max": LF_T, "caps": "U[1000, 2000] seeded", "dtype": "bf16 (fp16 kernels not built)"},
+            "roofline": {"bound": "hbm", "achieved": round(algo / dt / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+                         "frac": round(algo / dt / 8e12, 4), "traffic": None}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -185,7 +225,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-decode", action="store_true", help="skip the cfg3 decode measurement")
+    ap.add_argument("--no-decode", action="store_true", help="skip the cfg3 / cfg5 decode measurements")
+    ap.add_argument("--no-longform", action="store_true", help="skip the cfg5 long-form decode measurement")
     args = ap.parse_args()
 
     from tt2.config import TTSConfig
@@ -260,6 +301,11 @@ def main():
         log("[bench] decode (cfg3)")
         dec = decode_bench(model)
         log(f"[bench] decode {dec['value']:.0f} frames/s ({dec['ms_per_frame_step']} ms/step)")
+    lf = None
+    if rank == 0 and world == 1 and not args.no_decode and not args.no_longform:
+        log("[bench] long-form decode (cfg5)")
+        lf = longform_bench(model)
+        log(f"[bench] long-form {lf['value']:.0f} frames/s ({lf['steps_run']} steps)")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[bench] cpu baseline (oracle on host cores)")
@@ -277,6 +323,7 @@ def main():
             "roofline": rl,
             "cpu_baseline": cpu,
             "decode": dec,
+            "decode_longform": lf,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

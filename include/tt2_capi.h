@@ -74,7 +74,7 @@ typedef struct tt2_gemm_args {
    * A tiles already staged in LDS.  Requires bf16, trans_a, no conv on A. */
   float* a_ksum;
   float a_ksum_beta;
-  /* decode-step fusions, skinny path only (bf16, m <= 32, A and B K-contiguous):
+  /* decode-step fusions, skinny path only (bf16, m <= 64 (LN prologue m <= 32), A and B K-contiguous):
    * - LayerNorm prologue on A: when a_ln_gamma != NULL the GEMM multiplies
    *   h = LN(A + a_ln_branch) (row-wise over the k = 512 columns, eps a_ln_eps) instead of A,
    *   and writes h to a_ln_out [m, k] (ld k);
@@ -116,7 +116,7 @@ typedef struct tt2_gemm_args {
 size_t tt2_gemm_workspace_size(const tt2_gemm_args* a);
 int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream);
 /* Kernel tt2_gemm would launch for these args (no device work): 1 register-staged
- * 128x128 (any dtype), 2 LDS-DMA 128x128 (bf16), 3 skinny decode (m <= 32),
+ * 128x128 (any dtype), 2 LDS-DMA 128x128 (bf16), 3 skinny decode (m <= 64),
  * 11 / 12 LDS-DMA 256x256 / 256x128, 13 warp-specialised 256x128; -1 invalid. */
 int tt2_gemm_plan(const tt2_gemm_args* a);
 

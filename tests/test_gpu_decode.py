@@ -92,3 +92,45 @@ def test_skinny_gemm(m):
     ops.gemm(A, B, C, m, n, k, k, k, n, bias=bias, act=1, variant=3)
     ref = (A.double() @ B.double().t() + bias.double()).relu()
     assert rel(C, ref) < 1e-5
+
+
+def test_decode_wide_batch_matches_oracle():
+    """A 40-utterance batch takes the 64-row skinny kernels (4 row blocks per MFMA column
+    tile): bf16 frames match the fp32 CPU oracle at the bf16 tolerance."""
+    oracle = init_deterministic(TransformerTTSOracle(OracleConfig()), 4).eval()
+    model = TransformerTTS(TTSConfig(), dtype=torch.bfloat16).eval()
+    model.load_state_dict(oracle.state_dict())
+    g = torch.Generator().manual_seed(8)
+    B, Tx, T = 40, 11, 6
+    text = torch.randint(1, 80, (B, Tx), generator=g)
+    tl = torch.randint(3, Tx + 1, (B,), generator=g)
+    for b in range(B):
+        text[b, tl[b]:] = 0
+    ref_after, _, ref_before, ref_stop = oracle.infer(text, tl, T, force_len=True)
+    after, out_len = model.infer(text, tl, T, stop_threshold=None)
+    assert rel(after, ref_after) < 6e-2
+    dec = model._decoders[(B, Tx, T, False)]
+    assert dec.fuse == 3 and dec.fused_io
+    assert rel(dec.mel_seq[:, :T], ref_before) < 6e-2
+
+
+def test_long_form_limits_early_exit():
+    """cfg5 shape (B=64, T_max=2000): per-utterance frame caps end the loop at the last
+    cap (polled every 32 frames), out_len = caps, frames stay finite, and the first frames
+    equal a short run of the same batch."""
+    torch.manual_seed(0)
+    model = TransformerTTS(TTSConfig(), dtype=torch.bfloat16).eval()
+    g = torch.Generator().manual_seed(2)
+    B, Tx, Tm = 64, 128, 2000
+    text = torch.randint(1, 80, (B, Tx), generator=g).cuda()
+    tl = torch.full((B,), Tx, dtype=torch.long, device="cuda")
+    caps = torch.randint(300, 700, (B,), generator=g)
+    dec = Decoder(model.engine, B, Tx, Tm)
+    after, out_len = dec.run(text, tl, Tm, stop_threshold=None, limits=caps)
+    n = after.shape[1]
+    assert int(caps.max()) <= n < int(caps.max()) + 32
+    assert torch.equal(out_len.cpu(), caps)
+    assert torch.isfinite(dec.mel_seq[:, :n]).all()
+    short = Decoder(model.engine, B, Tx, 8)
+    short.run(text, tl, 8, stop_threshold=None)
+    assert rel(short.mel_seq[:, :8], dec.mel_seq[:, :8]) < 1e-6

@@ -19,7 +19,7 @@ model.eval()
 g = torch.Generator().manual_seed(1)
 text = torch.randint(1, 80, (bench.DEC_B, bench.TX), generator=g).cuda()
 tl = torch.full((bench.DEC_B,), bench.TX, dtype=torch.int32, device="cuda")
-CFGS = [(1, 4, 8), (2, 4, 8), (3, 4, 8), (3, 2, 4), (3, 4, 16), (3, 8, 16)]
+CFGS = [(1, 4, 8), (2, 4, 8), (3, 4, 8), (3, 2, 4), (3, 4, 16)]
 for fuse, so, sf in CFGS + CFGS:
     dec = Decoder(model.engine, bench.DEC_B, bench.TX, bench.DEC_T)
     dec.fuse, dec.split_o, dec.split_f = fuse, so, sf

@@ -598,7 +598,7 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
 }
 
 // =====================================================================================
-// skinny-M (decode, M <= 32) bf16: out[M, N] = X[M, K] W[N, K]^T.  The problem is a
+// skinny-M (decode, M <= 64) bf16: out[M, N] = X[M, K] W[N, K]^T.  The problem is a
 // latency-bound weight stream: every workgroup owns 16 output columns, its 4 waves split
 // K, and each lane issues its WHOLE slice of W (NCH 16-B chunks) before anything else,
 // then its X chunks (or the LayerNorm prologue), so the kernel pays about one memory
@@ -621,17 +621,18 @@ struct SkinnyFuse {
 
 constexpr int SK_LN_LD = 512 + 8;   // bf16 per LDS row of the normalised A (16-B pad)
 
-template <int NCH, bool LN>
+template <int NCH, bool LN, int MR>
 __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t ldx, const bf16* W, int64_t ldw,
                                                          EpiParams E, int M, int N, int K, SkinnyFuse F,
                                                          float* slab, int kper) {
-  __shared__ float red[4][32][SK_COLS + 1];
+  static_assert(!LN || MR == 2, "LN prologue: m <= 32");
+  __shared__ float red[4][16 * MR][SK_COLS + 1];
   extern __shared__ __attribute__((aligned(16))) bf16 s_h[];   // [32][SK_LN_LD] when F.gamma (K == 512)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * SK_COLS;
   const int r = lane & 15, g = lane >> 4;
   const int n = n0 + r;
-  const bool nok = n < N, r0ok = r < M, r1ok = r + 16 < M;
+  const bool nok = n < N;
   // device scalars of the epilogue, issued up front
   const uint32_t seed = E.drop.thr ? *E.drop.seed : 0u;
   const int kv_t = F.kv ? *F.kv_t : 0;
@@ -639,20 +640,30 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t 
   const float pe_al = F.pe ? *F.pe_alpha : 0.f;
   const int em_t = F.emit_mel ? *F.emit_t : 0;
   const bf16* wrow = W + (int64_t)(nok ? n : 0) * ldw;
-  const bf16* x0 = X + (int64_t)(r0ok ? r : 0) * ldx;
-  const bf16* x1 = X + (int64_t)(r1ok ? r + 16 : 0) * ldx;
+  // MR blocks of 16 rows: block q covers rows 16 q + r
+  const bf16* xr[MR];
+  bool rok[MR];
+#pragma unroll
+  for (int q = 0; q < MR; ++q) {
+    rok[q] = 16 * q + r < M;
+    xr[q] = X + (int64_t)(rok[q] ? 16 * q + r : 0) * ldx;
+  }
   union U { uint4 u; bf16x8 v; };
   const uint4 z4 = make_uint4(0, 0, 0, 0);
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[MR];
+#pragma unroll
+  for (int q = 0; q < MR; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
   // split-K (slab != 0): workgroup row blockIdx.y takes k in [kbeg, kend) and stores its raw
   // partial sums to slab[blockIdx.y][m][n] (f32, no epilogue; tt2_ln_combine sums them)
   const int kbeg = slab ? blockIdx.y * kper : 0;
   const int kend = slab ? min(K, kbeg + kper) : K;
-  float e_bias = 0.f, e_res0 = 0.f, e_res1 = 0.f, e_pe = 0.f;
+  float e_bias = 0.f, e_res[MR], e_pe = 0.f;
+#pragma unroll
+  for (int q = 0; q < MR; ++q) e_res[q] = 0.f;
   const int ecol = threadIdx.x & 15, erow = threadIdx.x >> 4, enn = n0 + ecol;
   for (int ks = kbeg; ks < kend; ks += 4 * NCH * 32) {
     const int kb = ks + wave * (NCH * 32);
-    U w[NCH], a0[NCH], a1[NCH];
+    U w[NCH], a[MR][NCH];
     // (1) this lane's whole W slice: branch-free (an out-of-range chunk reads the zero page)
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
@@ -698,16 +709,19 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t 
       for (int c = 0; c < NCH; ++c) {
         const int kk = kb + 32 * c + 8 * g;
         const bool ok = kk < K;
-        a0[c].u = (r0ok && ok) ? *reinterpret_cast<const uint4*>(s_h + r * SK_LN_LD + kk) : z4;
-        a1[c].u = (r1ok && ok) ? *reinterpret_cast<const uint4*>(s_h + (r + 16) * SK_LN_LD + kk) : z4;
+#pragma unroll
+        for (int q = 0; q < MR; ++q)
+          a[q][c].u = (rok[q] && ok) ? *reinterpret_cast<const uint4*>(s_h + (16 * q + r) * SK_LN_LD + kk) : z4;
       }
     } else {
       // (2b) the X chunks, also all in flight
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         const int kk = kb + 32 * c + 8 * g;
-        a0[c].u = *reinterpret_cast<const uint4*>(r0ok && kk < kend ? (const void*)(x0 + kk) : (const void*)g_zero_page);
-        a1[c].u = *reinterpret_cast<const uint4*>(r1ok && kk < kend ? (const void*)(x1 + kk) : (const void*)g_zero_page);
+#pragma unroll
+        for (int q = 0; q < MR; ++q)
+          a[q][c].u = *reinterpret_cast<const uint4*>(rok[q] && kk < kend ? (const void*)(xr[q] + kk)
+                                                                          : (const void*)g_zero_page);
       }
       // keep every load above the first MFMA (the scheduler would otherwise interleave
       // them and pay one memory round trip per pair)
@@ -719,27 +733,26 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t 
       const bool ec = enn < N;
       if (E.bias && ec) e_bias = E.bias[enn];
       if (E.res && ec) {
-        if (erow < M) e_res0 = ld_any(E.res, (int64_t)erow * E.ldr + enn, E.res_dt);
-        if (erow + 16 < M) e_res1 = ld_any(E.res, (int64_t)(erow + 16) * E.ldr + enn, E.res_dt);
+#pragma unroll
+        for (int q = 0; q < MR; ++q)
+          if (erow + 16 * q < M) e_res[q] = ld_any(E.res, (int64_t)(erow + 16 * q) * E.ldr + enn, E.res_dt);
       }
       if (F.pe && ec) e_pe = pe_al * F.pe[(int64_t)pe_t * N + enn];
     }
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c].v, w[c].v, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[c].v, w[c].v, acc1, 0, 0, 0);
-    }
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int q = 0; q < MR; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[q][c].v, w[c].v, acc[q], 0, 0, 0);
   }
   // acc layout: row 4*(lane>>4) + i, col lane & 15
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    red[wave][4 * g + i][r] = acc0[i];
-    red[wave][16 + 4 * g + i][r] = acc1[i];
-  }
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int q = 0; q < MR; ++q) red[wave][16 * q + 4 * g + i][r] = acc[q][i];
   __syncthreads();
   if (slab) {
 #pragma unroll
-    for (int hrow = 0; hrow < 2; ++hrow) {
+    for (int hrow = 0; hrow < MR; ++hrow) {
       const int m = erow + 16 * hrow;
       if (m < M && enn < N)
         slab[((int64_t)blockIdx.y * M + m) * N + enn] =
@@ -753,12 +766,12 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t 
   Ep.res = nullptr;
   Ep.alpha = 1.f;
 #pragma unroll
-  for (int hrow = 0; hrow < 2; ++hrow) {
+  for (int hrow = 0; hrow < MR; ++hrow) {
     const int row = erow + 16 * hrow, col = ecol;
     const int m = row, nn = enn;
     if (m < M && nn < N) {
       const float v = (red[0][row][col] + red[1][row][col]) + (red[2][row][col] + red[3][row][col]);
-      float y = epi_value(Ep, seed, m, nn, E.alpha * v + e_bias + (hrow ? e_res1 : e_res0));
+      float y = epi_value(Ep, seed, m, nn, E.alpha * v + e_bias + e_res[hrow]);
       y += e_pe;
       st_any(E.c, (int64_t)m * E.ldc + nn, E.c_dt, y);
       if (F.kv && nn >= F.kv_col0)
@@ -1432,25 +1445,26 @@ extern "C" size_t tt2_gemm_workspace_size(const tt2_gemm_args* a) {
 }
 
 // Kernel selection (also exported as tt2_gemm_plan): 1 v1 register-staged, 2 v2
-// LDS-DMA 128^2, 3 skinny (M <= 32), 11 / 12 v6 256x256 / 256x128, 13 v7 warp-
+// LDS-DMA 128^2, 3 skinny (M <= 64), 11 / 12 v6 256x256 / 256x128, 13 v7 warp-
 // specialised 256x128 (auto).  Returns -1 (error set) for an unsupported fusion request.
 static int gemm_plan(const tt2_gemm_args* a) {
   const int var = a->kernel_variant;
   const int64_t a_inner = a->trans_a ? a->m : a->k, b_inner = a->trans_b ? a->n : a->k;
   // skinny split-K exists only as raw partial slabs (main_only) for tt2_ln_combine
-  const bool skinny = a->dtype_in == TT2_BF16 && a->m <= 32 && !a->trans_a && !a->trans_b && a->k % 8 == 0 &&
+  const bool skinny = a->dtype_in == TT2_BF16 && a->m <= 64 && !a->trans_a && !a->trans_b && a->k % 8 == 0 &&
                       a->a_conv_t == 0 && (a->splits <= 1 || a->main_only) && (var == 0 || var == 3);
   if (skinny && a->splits > 1 && (a->a_ln_gamma || a->kv_cache || a->pe_table || a->emit_mel ||
                                   a->k % (32 * a->splits) != 0))
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: skinny split-K slabs need k % (32 splits) == 0, no fusions"), -1;
   if ((a->a_ln_gamma || a->kv_cache) && !skinny)
-    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln / kv fusions need the skinny path (bf16, m <= 32, NT)"), -1;
-  if (a->a_ln_gamma && (a->k != 512 || a->lda != a->k || !a->a_ln_branch || !a->a_ln_beta || !a->a_ln_out))
-    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln needs k == lda == 512, branch, beta and out"), -1;
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln / kv fusions need the skinny path (bf16, m <= 64, NT)"), -1;
+  if (a->a_ln_gamma && (a->k != 512 || a->lda != a->k || a->m > 32 || !a->a_ln_branch || !a->a_ln_beta ||
+                        !a->a_ln_out))
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln needs k == lda == 512, m <= 32, branch, beta and out"), -1;
   if (a->kv_cache && (!a->kv_t || a->dtype_out != TT2_BF16))
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: kv scatter needs kv_t and a bf16 output"), -1;
   if ((a->pe_table || a->emit_mel) && !skinny)
-    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: pe / emit epilogues need the skinny path (bf16, m <= 32, NT)"), -1;
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: pe / emit epilogues need the skinny path (bf16, m <= 64, NT)"), -1;
   if (a->pe_table && (!a->pe_alpha || !a->pe_t))
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: pe epilogue needs pe_alpha and pe_t"), -1;
   if (a->emit_mel && (!a->emit_stop || !a->emit_prev || !a->emit_t || !a->emit_done || a->emit_nmels >= a->n ||
@@ -1556,14 +1570,19 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
     const bf16* Wt = reinterpret_cast<const bf16*>(a->b);
     // per-wave K slice = NCH x 32: one pass for K <= 4 * NCH * 32
     const int nch = kper <= 128 ? 1 : kper <= 256 ? 2 : kper <= 512 ? 4 : kper <= 1024 ? 8 : 16;
-#define TT2_SK(NCH, LN) hipLaunchKernelGGL((gemm_skinny_kernel<NCH, LN>), grid, dim3(NT), lds, stream, X, a->lda, Wt, \
-                                           a->ldb, ep, a->m, a->n, a->k, F, slab, kper)
-    if (a->a_ln_gamma) TT2_SK(4, true);   // k == 512 (checked by the plan)
-    else if (nch == 1) TT2_SK(1, false);
-    else if (nch == 2) TT2_SK(2, false);
-    else if (nch == 4) TT2_SK(4, false);
-    else if (nch == 8) TT2_SK(8, false);
-    else TT2_SK(16, false);
+#define TT2_SK(NCH, LN, MR) hipLaunchKernelGGL((gemm_skinny_kernel<NCH, LN, MR>), grid, dim3(NT), lds, stream, X, \
+                                               a->lda, Wt, a->ldb, ep, a->m, a->n, a->k, F, slab, kper)
+#define TT2_SK_M(MR)                      \
+  if (nch == 1) TT2_SK(1, false, MR);     \
+  else if (nch == 2) TT2_SK(2, false, MR); \
+  else if (nch == 4) TT2_SK(4, false, MR); \
+  else if (nch == 8) TT2_SK(8, false, MR); \
+  else if (MR == 2) TT2_SK(16, false, 2);  \
+  else TT2_SK(8, false, 4);   /* 64 rows: two passes of 8 chunks (16 would spill) */
+    if (a->a_ln_gamma) TT2_SK(4, true, 2);   // k == 512, m <= 32 (checked by the plan)
+    else if (a->m <= 32) { TT2_SK_M(2) }
+    else { TT2_SK_M(4) }
+#undef TT2_SK_M
 #undef TT2_SK
     return tt2_check_launch(hipGetLastError(), "tt2_gemm(skinny)");
   }

@@ -70,16 +70,17 @@ class Decoder:
         self.emit_done = torch.zeros(1, dtype=torch.int32, device=dev)   # heads-GEMM arrival counter
         # bf16: the scaled PE rides in the pre-net projection's epilogue and the frame emit
         # in the heads GEMM's (skinny-path epilogues; 2 launches fewer per step)
-        self.fused_io = cd == torch.bfloat16 and batch <= 32
+        self.fused_io = cd == torch.bfloat16 and batch <= 64
         self.graph = None
         # bf16 decode-step schedules: 0 no fusion, 1 KV-cache scatter in the QKV epilogue,
         # 2 also the LayerNorms as GEMM prologues (every workgroup recomputes the 32-row
         # statistics), 3 (default) KV scatter + split-K o / co / ffn2 whose slabs a
         # residual + LayerNorm combine kernel folds (tools/decode_ab.py measures them).
-        # The skinny-path fusions need batch <= 32; larger batches run unfused.
-        self.fuse = 3 if cd == torch.bfloat16 and batch <= 32 else 0
+        # The skinny-path fusions need batch <= 64 (the LN prologues <= 32); larger batches
+        # run unfused.
+        self.fuse = 3 if cd == torch.bfloat16 and batch <= 64 else 0
         self.split_o, self.split_f = 4, 8
-        self.slab = _Slab(torch.zeros(16 * 32 * d, dtype=torch.float32, device=dev))
+        self.slab = _Slab(torch.zeros(16 * max(B, 32) * d, dtype=torch.float32, device=dev))
 
     # ----------------------------------------------------------------- one step
     def step(self):
@@ -269,10 +270,16 @@ class Decoder:
         self.reset()
 
     def decode_loop(self, n_steps: int, use_graph: bool = True, stop_threshold: float | None = None,
-                    check_every: int = 32) -> int:
-        """Run up to n_steps frames; with stop_threshold, stop once every
-        utterance has emitted a stop probability >= threshold.  Returns frames run."""
+                    check_every: int = 32, limits: torch.Tensor | None = None) -> int:
+        """Run up to n_steps frames; with stop_threshold, stop once every utterance has
+        emitted a stop probability >= threshold or reached its own frame limit
+        (limits: [B] per-utterance caps, e.g. from a length model).  The batch keeps
+        stepping until the last utterance is done (polled every check_every frames).
+        Returns frames run."""
         logit_thr = None if stop_threshold is None else math.log(stop_threshold / (1.0 - stop_threshold))
+        if limits is not None:
+            limits = limits.to(device=self.stop_seq.device, dtype=torch.long)
+            n_steps = min(n_steps, int(limits.max()))
         done = 0
         while done < n_steps:
             k = min(check_every, n_steps - done)
@@ -282,13 +289,17 @@ class Decoder:
                 else:
                     self.step()
             done += k
-            if logit_thr is not None:
-                hit = (self.stop_seq[:, :done] >= logit_thr).any(dim=1)
-                if bool(hit.all()):
+            if logit_thr is not None or limits is not None:
+                fin = torch.zeros(self.B, dtype=torch.bool, device=self.stop_seq.device)
+                if logit_thr is not None:
+                    fin |= (self.stop_seq[:, :done] >= logit_thr).any(dim=1)
+                if limits is not None:
+                    fin |= limits <= done
+                if bool(fin.all()):
                     break
         return done
 
-    def postnet(self, n_frames: int, stop_threshold: float | None):
+    def postnet(self, n_frames: int, stop_threshold: float | None, limits: torch.Tensor | None = None):
         e, c, A = self.e, self.e.cfg, self.A
         B, T = self.B, n_frames
         was = e.training
@@ -306,15 +317,18 @@ class Decoder:
             hit = self.stop_seq[:, :n_frames] >= logit_thr
             first = torch.where(hit.any(1), hit.float().argmax(1) + 1, torch.full_like(out_len, n_frames))
             out_len = first.long()
+        if limits is not None:
+            out_len = torch.minimum(out_len, limits.to(out_len.device, torch.long))
         return mel_after, out_len
 
     def run(self, text, text_len, max_len: int | None = None, stop_threshold: float | None = 0.5,
-            use_graph: bool = True):
-        """Greedy decode; returns (mel_after [B, T, 80] f32, out_len [B])."""
+            use_graph: bool = True, limits: torch.Tensor | None = None):
+        """Greedy decode; returns (mel_after [B, T, 80] f32, out_len [B]).  limits: optional
+        per-utterance frame caps [B] (out_len <= limits)."""
         max_len = max_len or self.Tmax
         self.encode(text, text_len)
         if use_graph and self.graph is None:
             self.capture()
         self.reset()
-        n = self.decode_loop(max_len, use_graph, stop_threshold)
-        return self.postnet(n, stop_threshold)
+        n = self.decode_loop(max_len, use_graph, stop_threshold, limits=limits)
+        return self.postnet(n, stop_threshold, limits)
