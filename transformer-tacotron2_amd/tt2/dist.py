@@ -48,9 +48,23 @@ class GradSync:
 
     def ready(self, offset: int):
         """Every gradient at flat index >= offset is final."""
+        for i in self.take_ready(offset):
+            self._launch(*self.buckets[i])
+
+    def take_ready(self, offset: int) -> list[int]:
+        """Indices of the buckets that became complete at offset (advances the cursor
+        without launching: a captured step records where its buckets can go)."""
+        out = []
         while self.next < len(self.buckets) and self.buckets[self.next][0] >= offset:
-            self._launch(*self.buckets[self.next])
+            out.append(self.next)
             self.next += 1
+        return out
+
+    def launch(self, idx: list[int]):
+        """Launch the given buckets (in order) and advance the cursor past them."""
+        for i in idx:
+            self._launch(*self.buckets[i])
+            self.next = max(self.next, i + 1)
 
     def finish(self):
         while self.next < len(self.buckets):

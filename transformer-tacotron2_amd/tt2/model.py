@@ -158,30 +158,57 @@ class TransformerTTS:
         # the caller's warm-up eager steps size every workspace; capture must not allocate
         nbt_saved = dict(e.nbt)
         hook, e.grad_ready_hook = e.grad_ready_hook, None
+        sync = getattr(sync_grads, "__self__", None)   # a GradSync's bound finish(): overlap buckets
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        g1 = torch.cuda.CUDAGraph()
         g2 = torch.cuda.CUDAGraph() if sync_grads is not None else None
+        segs = []   # [(graph, bucket indices launched right after its replay)]
+        torch.cuda.synchronize()
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g1, stream=s):
-                e.forward(A)
-                e.loss(A)
-                e.backward(A)
-                if g2 is None:
-                    e.optimizer_step()
+            cur = [torch.cuda.CUDAGraph()]
+            cur[0].capture_begin()
+            if sync is not None and hasattr(sync, "take_ready"):
+                # cut the forward+backward graph wherever a gradient bucket becomes final,
+                # so the replay can start that bucket's all-reduce while the rest of the
+                # backward runs (RCCL stays outside the graphs, on its own stream)
+                sync.reset()
+
+                def cut(offset):
+                    if offset <= 0:       # the last buckets go to finish(): no empty tail graph
+                        return
+                    idx = sync.take_ready(offset)
+                    if idx:
+                        cur[0].capture_end()
+                        segs.append((cur[0], idx))
+                        cur[0] = torch.cuda.CUDAGraph()
+                        cur[0].capture_begin()
+                e.grad_ready_hook = cut
+            e.forward(A)
+            e.loss(A)
+            e.backward(A)
+            e.grad_ready_hook = None
+            if g2 is None:
+                e.optimizer_step()
+            cur[0].capture_end()
+            segs.append((cur[0], []))
+            if sync is not None and hasattr(sync, "take_ready"):
+                sync.reset()
             if g2 is not None:
                 with torch.cuda.graph(g2, stream=s):
                     e.optimizer_step()
         torch.cuda.current_stream().wait_stream(s)
         e.grad_ready_hook = hook
         e.nbt = nbt_saved  # capture records kernels only; each replay counts one batch
-        self._graphs[(B, Tx, Ty)] = (g1, g2)
+        self._graphs[(B, Tx, Ty)] = (segs, g2)
 
         def run(text, text_len, mel, mel_len):
             e.stage_inputs(A, text, text_len.to(torch.int32), mel, mel_len.to(torch.int32))
-            g1.replay()
+            for g, idx in segs:
+                g.replay()
+                if idx:
+                    sync.launch(idx)  # these buckets' all-reduce overlaps the next segment
             if g2 is not None:
-                sync_grads()          # bucketed RCCL all-reduce between the two graphs
+                sync_grads()          # remaining buckets, then wait for all of them
                 g2.replay()
             for k in e.nbt:
                 e.nbt[k] += 1
