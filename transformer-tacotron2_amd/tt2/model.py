@@ -52,6 +52,45 @@ class TransformerTTS:
         P, S, nbt = from_state_dict(self.cfg, sd)
         self.engine.load_slots(P, S, nbt)
 
+    def save_checkpoint(self, path: str):
+        """Training checkpoint: the SURVEY 8(b) state_dict, the Adam
+        moments in the same checkpoint naming (so the file does not depend on the internal
+        flat layout), the optimizer step, its hyper-parameters and the dropout-seed RNG state.
+        Written with torch.save; load_checkpoint resumes bit for bit."""
+        e = self.engine
+        ck = {"format": "tt2-train-1", "cfg": self.cfg.to_dict(), "model": self.state_dict(),
+              "rng": {"dropout_seed": int(e.seed.item()) & 0xFFFFFFFF}}
+        if e.exp_avg is not None:
+            zs = torch.zeros_like(e.stats)
+            mom = lambda buf: {k: v for k, v in to_state_dict(self.cfg, e.lay, buf, e.slay, zs, {}).items()  # noqa: E731
+                               if "running_" not in k and "num_batches" not in k}
+            ck["optimizer"] = {"exp_avg": mom(e.exp_avg), "exp_avg_sq": mom(e.exp_avg_sq),
+                               "step": int(e.step_t.item()), "hparams": dict(e.opt)}
+        torch.save(ck, path)
+
+    def load_checkpoint(self, path: str):
+        """Resume from save_checkpoint (tensors only: torch.load(weights_only=True))."""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        if ck.get("format") != "tt2-train-1":
+            raise ValueError(f"{path}: not a tt2 training checkpoint")
+        if ck["cfg"] != self.cfg.to_dict():
+            raise ValueError(f"{path}: config mismatch")
+        self.load_state_dict(ck["model"])
+        e = self.engine
+        opt = ck.get("optimizer")
+        if opt is not None:
+            e.init_optimizer(**opt["hparams"])
+            model_sd = ck["model"]
+            for buf, key in ((e.exp_avg, "exp_avg"), (e.exp_avg_sq, "exp_avg_sq")):
+                full = {k: opt[key].get(k, v) for k, v in model_sd.items()}   # stats keys: placeholders
+                P, _, _ = from_state_dict(self.cfg, full)
+                with torch.no_grad():
+                    for k, v in P.items():
+                        e.lay.view(buf, k).copy_(v.reshape(e.lay.view(buf, k).shape))
+            e.step_t.fill_(opt["step"])
+        seed = ck["rng"]["dropout_seed"]
+        e.seed.fill_(seed - (1 << 32) if seed >= (1 << 31) else seed)
+
     def grads_state_dict(self):
         e = self.engine
         return grads_to_state_dict_names(self.cfg, e.lay, e.grads)
