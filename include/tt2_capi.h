@@ -321,6 +321,35 @@ int tt2_adam_step(const tt2_adam_args* a, hipStream_t stream);
 /* step += 1; seed += 1 (seed may be NULL) */
 int tt2_step_bump(int32_t* step, uint32_t* seed, hipStream_t stream);
 
+/* ------------------------------------------------------------ audio data path
+ * Either side of the mel engine: log-mel extraction of the
+ * training targets and Griffin-Lim inversion of synthesised mels.  The STFT, inverse DFT
+ * and mel projections are tt2_gemm calls (f32) on window-folded bases; these are the
+ * byte-moving steps around them (all f32, caller-owned buffers, caller's stream).
+ * Frame layout: utterance b's padded signal is padded[b * Lp ...] with Lp a multiple of
+ * hop, so the batch's frames are one strided matrix (row r at sample r * hop, ld = hop) and
+ * utterance b owns rows [b * R, b * R + n_frames_b), R = Lp / hop.  Replaces the reference
+ * pipeline's librosa / torch.stft feature extraction and its vocoder hand-off. */
+/* padded[b][j] = x[b][reflect(j - pad)] for j < len_b + 2 pad (np.pad "reflect"), else 0;
+ * lens may be NULL (all len); pad < len. */
+int tt2_reflect_pad(const float* x, int64_t ldx, const int32_t* lens, int32_t batch, int32_t len, float* padded,
+                    int64_t padded_len, int32_t pad, hipStream_t stream);
+/* mag[r][k] = |spec[r][k] + i spec[r][n_bins + k]| (k < n_bins), zero padding to ld_mag. */
+int tt2_spec_magnitude(const float* spec, int64_t ld_spec, int32_t m, int32_t n_bins, float* mag, int64_t ld_mag,
+                       hipStream_t stream);
+/* out = mag * e / |e| as [re | im] rows (phase 0 where est is NULL or e == 0): Griffin-Lim's
+ * projection onto the target magnitude. */
+int tt2_spec_rephase(const float* mag, int64_t ld_mag, const float* est, int64_t ld_est, int32_t m, int32_t n_bins,
+                     float* out, int64_t ld_out, hipStream_t stream);
+/* y[b][t] = sum_f frames[b * R + f][t + n_fft/2 - f hop] / sum_f hann^2(...) for t < len_b
+ * (least-squares iSTFT overlap-add, centre padding removed), 0 beyond. */
+int tt2_overlap_add(const float* frames, int64_t ld_frames, const int32_t* lens, int32_t batch, int32_t len,
+                    int32_t rows_per_utt, int32_t n_fft, int32_t hop, float* y, int64_t ld_y, hipStream_t stream);
+/* scatter = 0: mel[b][t][c] = log(max(rows[b * R + t][c], clamp)) (t < frames_b, else log clamp);
+ * scatter = 1: rows[b * R + t][c] = exp(mel[b][t][c]) (t < frames_b, else 0).  mel [batch][t][n_mels]. */
+int tt2_mel_rows(float* rows, int64_t ld_rows, float* mel, const int32_t* frames, int32_t batch, int32_t t,
+                 int32_t n_mels, int32_t rows_per_utt, float clamp, int32_t scatter, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -199,6 +199,12 @@ SIGNATURES.update({
     "tt2_layernorm_fwd": ([P_(LnArgs), vp], C.c_int),
     "tt2_layernorm_bwd_workspace_size": ([P_(LnArgs)], sz),
     "tt2_layernorm_bwd": ([P_(LnArgs), vp], C.c_int),
+    "tt2_reflect_pad": ([vp, i64, vp, C.c_int32, C.c_int32, vp, i64, C.c_int32, vp], C.c_int),
+    "tt2_spec_magnitude": ([vp, i64, C.c_int32, C.c_int32, vp, i64, vp], C.c_int),
+    "tt2_spec_rephase": ([vp, i64, vp, i64, C.c_int32, C.c_int32, vp, i64, vp], C.c_int),
+    "tt2_overlap_add": ([vp, i64, vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, i64, vp], C.c_int),
+    "tt2_mel_rows": ([vp, i64, vp, vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, C.c_int32, vp],
+                     C.c_int),
     "tt2_ln_combine": ([vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp], C.c_int),
     "tt2_batchnorm_workspace_size": ([P_(BnArgs)], sz),
     "tt2_batchnorm_fwd": ([P_(BnArgs), vp], C.c_int),
