@@ -227,6 +227,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the cfg3 / cfg5 decode measurements")
     ap.add_argument("--no-longform", action="store_true", help="skip the cfg5 long-form decode measurement")
+    ap.add_argument("--force-dp", action="store_true", help="dev: run the DP path (bucketed RCCL all-reduce, "
+                    "segmented graph) even at world size 1")
     args = ap.parse_args()
 
     from tt2.config import TTSConfig
@@ -253,7 +255,11 @@ def main():
         eng.sync_shadow()
     model.configure_optimizer(lr=1.0, warmup=4000.0, clip_norm=1.0)
     sync = None
-    if world > 1:
+    if world > 1 or args.force_dp:
+        if world == 1:   # dev check of the DP path on one GPU: a 1-rank RCCL group
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group("nccl", rank=0, world_size=1)
         broadcast_params(model)
         sync = attach(model)
     model.train()
@@ -326,7 +332,7 @@ def main():
             "decode_longform": lf,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
