@@ -34,6 +34,7 @@ extern "C" {
 
 #define TT2_DT_F32 0
 #define TT2_DT_BF16 1
+#define TT2_DT_F16 2   /* decode step only: skinny GEMM, decode attention, ln_combine, cast2d */
 
 /* ------------------------------------------------------------------ runtime */
 const char* tt2_last_error(void);
@@ -220,14 +221,14 @@ typedef struct tt2_ln_args {
 int tt2_layernorm_fwd(const tt2_ln_args* a, hipStream_t stream);
 size_t tt2_layernorm_bwd_workspace_size(const tt2_ln_args* a);
 int tt2_layernorm_bwd(const tt2_ln_args* a, hipStream_t stream);
-/* Decode-step residual combine + LayerNorm (bf16 x / y, c = 512):
+/* Decode-step residual combine + LayerNorm (x / y of dtype bf16 or f16, c = 512):
  *   y[m, :] = LN(x[m, :] + bias + sum_{s < splits} part[s][m][:]) * gamma + beta
  * part: the raw f32 partial slabs [splits][m][c] of a skinny split-K projection (tt2_gemm
  * with splits > 1 and main_only; splits 1, 2, 4, 8 or 16), summed in a fixed order.
  * Replaces the output-projection epilogue + residual + LayerNorm of a decoder sublayer
  *  where splitting K spreads the weight stream over more CUs. */
 int tt2_ln_combine(const void* x, const float* part, int32_t splits, const float* bias, const float* gamma,
-                   const float* beta, void* y, int32_t m, int32_t c, float eps, hipStream_t stream);
+                   const float* beta, void* y, int32_t m, int32_t c, float eps, int32_t dtype, hipStream_t stream);
 
 /* ------------------------------------------------------------- BatchNorm
  * fwd: out = drop(act((y - mean)*rstd*gamma + beta)) (+ res), statistics over

@@ -134,3 +134,21 @@ def test_long_form_limits_early_exit():
     short = Decoder(model.engine, B, Tx, 8)
     short.run(text, tl, 8, stop_threshold=None)
     assert rel(short.mel_seq[:, :8], dec.mel_seq[:, :8]) < 1e-6
+
+
+def test_decode_fp16_matches_oracle():
+    """cfg5's fp16 decode step (f16 weights copy, f16 KV cache, f16 cross K/V) on a bf16
+    engine: frames match the fp32 oracle within the fp16 tolerance, and the fp16 frames sit
+    at least as close to the oracle as the bf16 ones (more mantissa bits)."""
+    oracle, model, text, tl = setup(torch.bfloat16)
+    T = 12
+    ref_after, _, ref_before, ref_stop = oracle.infer(text, tl, T, force_len=True)
+    errs = {}
+    for dt in (torch.float16, torch.bfloat16):
+        dec = Decoder(model.engine, 3, 17, T, dtype=dt)
+        after, out_len = dec.run(text.cuda(), tl.cuda(), T, stop_threshold=None)
+        errs[dt] = rel(dec.mel_seq[:, :T], ref_before)
+        assert rel(after, ref_after) < 6e-2
+        assert (out_len.cpu() == T).all()
+    assert errs[torch.float16] < 3e-2
+    assert errs[torch.float16] <= errs[torch.bfloat16] * 1.5

@@ -166,3 +166,40 @@ def test_attn_decode_cross_ragged():
     ref = _attn_ref(q, mem[:, :, :d], mem[:, :, d:], kl.tolist(), 0.125)
     assert rel(out, ref) < 1e-2
     assert out[2].float().abs().sum().item() == 0   # no keys -> zeros, never NaN
+
+
+def _h(shape, gen, scale=1.0):
+    return (torch.randn(shape, generator=gen) * scale).half().cuda()
+
+
+@pytest.mark.parametrize("m,n,k", [(32, 1536, 512), (64, 512, 2048), (17, 81, 512), (64, 256, 80)])
+def test_skinny_gemm_fp16(m, n, k):
+    g = torch.Generator().manual_seed(n + k)
+    A, W = _h((m, k), g), _h((n, k), g, 0.1)
+    bias = torch.randn(n, generator=g).cuda()
+    C = torch.empty(m, n, dtype=torch.float16, device="cuda")
+    ops.gemm(A, W, C, m, n, k, k, k, n, bias=bias, variant=3)
+    assert rel(C, A.double() @ W.double().t() + bias.double()) < 2e-3
+
+
+def test_fp16_kv_scatter_attention_ln_combine():
+    g = torch.Generator().manual_seed(13)
+    B, d, Tm, t = 48, 512, 64, 20
+    x = _h((B, d), g)
+    W = _h((3 * d, d), g, 0.05)
+    qkv = torch.empty(B, 3 * d, dtype=torch.float16, device="cuda")
+    cache = _h((B, Tm, 2 * d), g)
+    tp = torch.tensor([t], dtype=torch.int32, device="cuda")
+    ops.gemm(x, W, qkv, B, 3 * d, d, d, d, 3 * d, kv=(cache, tp, d, Tm * 2 * d, 2 * d), variant=3)
+    assert torch.equal(cache[:, t], qkv[:, d:])
+    out = torch.empty(B, d, dtype=torch.float16, device="cuda")
+    ops.attn_decode(qkv, cache, cache[:, :, d:], out, 3 * d, Tm * 2 * d, 2 * d, Tm * 2 * d, 2 * d, d, B, 8, Tm,
+                    t_ptr=tp, scale=0.125)
+    ref = _attn_ref(qkv[:, :d], cache[:, :, :d], cache[:, :, d:], [t + 1] * B, 0.125)
+    assert rel(out, ref) < 2e-3
+    slab = torch.randn(4 * B * d, device="cuda")
+    bias, gam, bet = (torch.randn(d, generator=g).cuda() for _ in range(3))
+    y = torch.empty(B, d, dtype=torch.float16, device="cuda")
+    ops.ln_combine(x, slab, 4, bias, gam, bet, y, B)
+    s = x.double() + bias.double() + slab.view(4, B, d).double().sum(0)
+    assert rel(y, F.layer_norm(s, (d,), gam.double(), bet.double(), 1e-5)) < 2e-3

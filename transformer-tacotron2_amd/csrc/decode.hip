@@ -30,6 +30,11 @@ template <> TT2_DEV void load8f(const bf16* p, float (&v)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
 }
+template <> TT2_DEV void load8f(const f16* p, float (&v)[8]) {
+  const f16x8 x = *reinterpret_cast<const f16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+}
 template <> TT2_DEV void load8f(const float* p, float (&v)[8]) {
   const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
 #pragma unroll
@@ -172,7 +177,7 @@ __global__ void decode_emit_kernel(const float* heads, int64_t hld, int B, int N
 
 extern "C" int tt2_attn_decode(const tt2_attn_decode_args* p, hipStream_t s) {
   if (p->head_dim != D) return tt2_set_error(TT2_E_INVALID, "tt2_attn_decode: head_dim must be 64");
-  const int esz = p->dtype == TT2_DT_BF16 ? 2 : 4;
+  const int esz = p->dtype == TT2_DT_F32 ? 4 : 2;
   const int64_t lds[] = {p->q_ld, p->k_ld, p->v_ld, p->k_bstride, p->v_bstride};
   for (int64_t ld : lds)
     if ((ld * esz) % 16) return tt2_set_error(TT2_E_INVALID, "tt2_attn_decode: strides must be 16-B multiples");
@@ -183,6 +188,7 @@ extern "C" int tt2_attn_decode(const tt2_attn_decode_args* p, hipStream_t s) {
   dim3 g(p->batch * p->heads);
   // 8 waves per (batch, head): each wave takes 1/8 of the keys, 32 keys per iteration
   if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL((attn_decode_kernel<bf16, 8>), g, dim3(8 * 64), 0, s, a);
+  else if (p->dtype == TT2_DT_F16) hipLaunchKernelGGL((attn_decode_kernel<f16, 8>), g, dim3(8 * 64), 0, s, a);
   else hipLaunchKernelGGL((attn_decode_kernel<float, 8>), g, dim3(8 * 64), 0, s, a);
   return tt2_check_launch(hipGetLastError(), "tt2_attn_decode");
 }

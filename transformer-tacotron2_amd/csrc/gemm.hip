@@ -48,10 +48,12 @@ struct EpiParams {
 __global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int M, int N);
 
 TT2_DEV float ld_any(const void* p, int64_t i, int dt) {
+  if (dt == TT2_F16) return (float)reinterpret_cast<const f16*>(p)[i];
   return dt == TT2_BF16 ? (float)reinterpret_cast<const bf16*>(p)[i] : reinterpret_cast<const float*>(p)[i];
 }
 TT2_DEV void st_any(void* p, int64_t i, int dt, float v) {
-  if (dt == TT2_BF16) reinterpret_cast<bf16*>(p)[i] = (bf16)v;
+  if (dt == TT2_F16) reinterpret_cast<f16*>(p)[i] = (f16)v;
+  else if (dt == TT2_BF16) reinterpret_cast<bf16*>(p)[i] = (bf16)v;
   else reinterpret_cast<float*>(p)[i] = v;
 }
 
@@ -613,19 +615,31 @@ constexpr int SK_COLS = 16;
 // Decode-step fusions carried by the skinny kernel (tt2_gemm_args a_ln_* / kv_* / pe_* / emit_*).
 struct SkinnyFuse {
   const bf16* br; const float* gamma; const float* beta; bf16* h_out; float eps;   // LN prologue (gamma != 0)
-  bf16* kv; const int32_t* kv_t; int kv_col0; int64_t kv_bstride, kv_ld;           // KV scatter (kv != 0)
+  void* kv; const int32_t* kv_t; int kv_col0; int64_t kv_bstride, kv_ld;           // KV scatter (kv != 0)
   const float* pe; const float* pe_alpha; const int32_t* pe_t;                     // + alpha * pe[t][n]
-  float* emit_mel; float* emit_stop; bf16* emit_prev; int32_t* emit_t; uint32_t* emit_seed;
+  float* emit_mel; float* emit_stop; void* emit_prev; int32_t* emit_t; uint32_t* emit_seed;
   int32_t* emit_done; int emit_nmels, emit_tmax;                                   // frame emit (heads)
 };
 
 constexpr int SK_LN_LD = 512 + 8;   // bf16 per LDS row of the normalised A (16-B pad)
 
-template <int NCH, bool LN, int MR>
-__global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t ldx, const bf16* W, int64_t ldw,
+// element type of the skinny path: bf16 (the engine's dtype) or f16 (the fp16 decode step)
+template <typename TE> struct SkT;
+template <> struct SkT<bf16> {
+  typedef bf16x8 V;
+  static TT2_DEV f32x4 mma(V a, V b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+};
+template <> struct SkT<f16> {
+  typedef f16x8 V;
+  static TT2_DEV f32x4 mma(V a, V b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+};
+
+template <typename TE, int NCH, bool LN, int MR>
+__global__ __launch_bounds__(NT) void gemm_skinny_kernel(const TE* X, int64_t ldx, const TE* W, int64_t ldw,
                                                          EpiParams E, int M, int N, int K, SkinnyFuse F,
                                                          float* slab, int kper) {
-  static_assert(!LN || MR == 2, "LN prologue: m <= 32");
+  static_assert(!LN || (MR == 2 && __is_same(TE, bf16)), "LN prologue: bf16, m <= 32");
+  typedef typename SkT<TE>::V V8;
   __shared__ float red[4][16 * MR][SK_COLS + 1];
   extern __shared__ __attribute__((aligned(16))) bf16 s_h[];   // [32][SK_LN_LD] when F.gamma (K == 512)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -639,16 +653,16 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t 
   const int pe_t = F.pe ? *F.pe_t : 0;
   const float pe_al = F.pe ? *F.pe_alpha : 0.f;
   const int em_t = F.emit_mel ? *F.emit_t : 0;
-  const bf16* wrow = W + (int64_t)(nok ? n : 0) * ldw;
+  const TE* wrow = W + (int64_t)(nok ? n : 0) * ldw;
   // MR blocks of 16 rows: block q covers rows 16 q + r
-  const bf16* xr[MR];
+  const TE* xr[MR];
   bool rok[MR];
 #pragma unroll
   for (int q = 0; q < MR; ++q) {
     rok[q] = 16 * q + r < M;
     xr[q] = X + (int64_t)(rok[q] ? 16 * q + r : 0) * ldx;
   }
-  union U { uint4 u; bf16x8 v; };
+  union U { uint4 u; V8 v; };
   const uint4 z4 = make_uint4(0, 0, 0, 0);
   f32x4 acc[MR];
 #pragma unroll
@@ -742,7 +756,7 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t 
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
-      for (int q = 0; q < MR; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[q][c].v, w[c].v, acc[q], 0, 0, 0);
+      for (int q = 0; q < MR; ++q) acc[q] = SkT<TE>::mma(a[q][c].v, w[c].v, acc[q]);
   }
   // acc layout: row 4*(lane>>4) + i, col lane & 15
 #pragma unroll
@@ -775,11 +789,11 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const bf16* X, int64_t 
       y += e_pe;
       st_any(E.c, (int64_t)m * E.ldc + nn, E.c_dt, y);
       if (F.kv && nn >= F.kv_col0)
-        F.kv[(int64_t)m * F.kv_bstride + (int64_t)kv_t * F.kv_ld + (nn - F.kv_col0)] = (bf16)y;
+        reinterpret_cast<TE*>(F.kv)[(int64_t)m * F.kv_bstride + (int64_t)kv_t * F.kv_ld + (nn - F.kv_col0)] = (TE)y;
       if (F.emit_mel && em_t < F.emit_tmax) {
         if (nn < F.emit_nmels) {
           F.emit_mel[((int64_t)m * F.emit_tmax + em_t) * F.emit_nmels + nn] = y;
-          F.emit_prev[(int64_t)m * F.emit_nmels + nn] = (bf16)y;
+          reinterpret_cast<TE*>(F.emit_prev)[(int64_t)m * F.emit_nmels + nn] = (TE)y;
         } else if (nn == F.emit_nmels) {
           F.emit_stop[(int64_t)m * F.emit_tmax + em_t] = y;
         }
@@ -1451,18 +1465,22 @@ static int gemm_plan(const tt2_gemm_args* a) {
   const int var = a->kernel_variant;
   const int64_t a_inner = a->trans_a ? a->m : a->k, b_inner = a->trans_b ? a->n : a->k;
   // skinny split-K exists only as raw partial slabs (main_only) for tt2_ln_combine
-  const bool skinny = a->dtype_in == TT2_BF16 && a->m <= 64 && !a->trans_a && !a->trans_b && a->k % 8 == 0 &&
+  const bool half_in = a->dtype_in == TT2_BF16 || a->dtype_in == TT2_F16;
+  const bool skinny = half_in && a->m <= 64 && !a->trans_a && !a->trans_b && a->k % 8 == 0 &&
                       a->a_conv_t == 0 && (a->splits <= 1 || a->main_only) && (var == 0 || var == 3);
   if (skinny && a->splits > 1 && (a->a_ln_gamma || a->kv_cache || a->pe_table || a->emit_mel ||
                                   a->k % (32 * a->splits) != 0))
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: skinny split-K slabs need k % (32 splits) == 0, no fusions"), -1;
   if ((a->a_ln_gamma || a->kv_cache) && !skinny)
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln / kv fusions need the skinny path (bf16, m <= 64, NT)"), -1;
-  if (a->a_ln_gamma && (a->k != 512 || a->lda != a->k || a->m > 32 || !a->a_ln_branch || !a->a_ln_beta ||
+  if (a->dtype_in == TT2_F16 && !skinny)
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: f16 operands only on the skinny decode path (m <= 64, NT)"), -1;
+  if (a->a_ln_gamma && (a->dtype_in != TT2_BF16 || a->k != 512 || a->lda != a->k || a->m > 32 || !a->a_ln_branch ||
+                        !a->a_ln_beta ||
                         !a->a_ln_out))
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ln needs k == lda == 512, m <= 32, branch, beta and out"), -1;
-  if (a->kv_cache && (!a->kv_t || a->dtype_out != TT2_BF16))
-    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: kv scatter needs kv_t and a bf16 output"), -1;
+  if (a->kv_cache && (!a->kv_t || a->dtype_out != a->dtype_in))
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: kv scatter needs kv_t and an output of the input dtype"), -1;
   if ((a->pe_table || a->emit_mel) && !skinny)
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: pe / emit epilogues need the skinny path (bf16, m <= 64, NT)"), -1;
   if (a->pe_table && (!a->pe_alpha || !a->pe_t))
@@ -1497,7 +1515,7 @@ extern "C" int tt2_gemm_plan(const tt2_gemm_args* a) { return gemm_plan(a); }
 
 // Validate one GEMM request and build its operand / epilogue descriptors.
 static int gemm_prep(const tt2_gemm_args* a, OpDesc& A, OpDesc& B, EpiParams& ep) {
-  const int esz = a->dtype_in == TT2_BF16 ? 2 : 4;
+  const int esz = a->dtype_in == TT2_F32 ? 4 : 2;
   const int E = 16 / esz;
   auto misaligned = [&](const void* p, int64_t ld) {
     return (reinterpret_cast<uintptr_t>(p) % 16) != 0 || (ld * esz) % 16 != 0;
@@ -1537,7 +1555,8 @@ static int gemm_prep(const tt2_gemm_args* a, OpDesc& A, OpDesc& B, EpiParams& ep
       const int esz = dt == TT2_BF16 ? 2 : 4;
       return reinterpret_cast<uintptr_t>(p) % 16 == 0 && (ld * esz) % 16 == 0 && (8 * esz) % 16 == 0;
     };
-    ep.vec = ok(a->c, a->ldc, a->dtype_out) && ok(a->res, a->ldr, a->res_dtype) &&
+    ep.vec = a->dtype_out != TT2_F16 && a->res_dtype != TT2_F16 && a->gate_dtype != TT2_F16 &&
+             ok(a->c, a->ldc, a->dtype_out) && ok(a->res, a->ldr, a->res_dtype) &&
              ok(a->gate, a->ldg, a->gate_dtype) && (reinterpret_cast<uintptr_t>(a->bias) % 16 == 0);
   }
   return TT2_OK;
@@ -1556,32 +1575,34 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   if (plan < 0) return TT2_E_INVALID;   // message already set
   if (plan == 3) {   // skinny-M weight-streaming path (decode step)
     SkinnyFuse F{reinterpret_cast<const bf16*>(a->a_ln_branch), a->a_ln_gamma, a->a_ln_beta,
-                 reinterpret_cast<bf16*>(a->a_ln_out), a->a_ln_eps, reinterpret_cast<bf16*>(a->kv_cache), a->kv_t,
+                 reinterpret_cast<bf16*>(a->a_ln_out), a->a_ln_eps, a->kv_cache, a->kv_t,
                  a->kv_col0, a->kv_bstride, a->kv_ld, a->pe_table, a->pe_alpha, a->pe_t, a->emit_mel, a->emit_stop,
-                 reinterpret_cast<bf16*>(a->emit_prev), a->emit_t, a->emit_seed, a->emit_done, a->emit_nmels,
-                 a->emit_tmax};
+                 a->emit_prev, a->emit_t, a->emit_seed, a->emit_done, a->emit_nmels, a->emit_tmax};
     const size_t lds = a->a_ln_gamma ? 32 * SK_LN_LD * sizeof(bf16) : 0;
     // split-K (splits > 1, main_only): raw partial slabs [splits][m][n] f32 in the workspace
     const int sp = a->splits > 1 ? a->splits : 1;
     const int kper = sp > 1 ? ((a->k + sp - 1) / sp + 31) / 32 * 32 : a->k;
     float* slab = sp > 1 ? reinterpret_cast<float*>(a->workspace) : nullptr;
     const dim3 grid((a->n + SK_COLS - 1) / SK_COLS, sp > 1 ? (a->k + kper - 1) / kper : 1);
-    const bf16* X = reinterpret_cast<const bf16*>(a->a);
-    const bf16* Wt = reinterpret_cast<const bf16*>(a->b);
     // per-wave K slice = NCH x 32: one pass for K <= 4 * NCH * 32
     const int nch = kper <= 128 ? 1 : kper <= 256 ? 2 : kper <= 512 ? 4 : kper <= 1024 ? 8 : 16;
-#define TT2_SK(NCH, LN, MR) hipLaunchKernelGGL((gemm_skinny_kernel<NCH, LN, MR>), grid, dim3(NT), lds, stream, X, \
-                                               a->lda, Wt, a->ldb, ep, a->m, a->n, a->k, F, slab, kper)
-#define TT2_SK_M(MR)                      \
-  if (nch == 1) TT2_SK(1, false, MR);     \
-  else if (nch == 2) TT2_SK(2, false, MR); \
-  else if (nch == 4) TT2_SK(4, false, MR); \
-  else if (nch == 8) TT2_SK(8, false, MR); \
-  else if (MR == 2) TT2_SK(16, false, 2);  \
-  else TT2_SK(8, false, 4);   /* 64 rows: two passes of 8 chunks (16 would spill) */
-    if (a->a_ln_gamma) TT2_SK(4, true, 2);   // k == 512, m <= 32 (checked by the plan)
-    else if (a->m <= 32) { TT2_SK_M(2) }
-    else { TT2_SK_M(4) }
+#define TT2_SK(TE, NCH, LN, MR)                                                                              \
+  hipLaunchKernelGGL((gemm_skinny_kernel<TE, NCH, LN, MR>), grid, dim3(NT), lds, stream,                    \
+                     reinterpret_cast<const TE*>(a->a), a->lda, reinterpret_cast<const TE*>(a->b), a->ldb, ep, \
+                     a->m, a->n, a->k, F, slab, kper)
+#define TT2_SK_M(TE, MR)                      \
+  if (nch == 1) TT2_SK(TE, 1, false, MR);     \
+  else if (nch == 2) TT2_SK(TE, 2, false, MR); \
+  else if (nch == 4) TT2_SK(TE, 4, false, MR); \
+  else if (nch == 8) TT2_SK(TE, 8, false, MR); \
+  else if (MR == 2) TT2_SK(TE, 16, false, 2);  \
+  else TT2_SK(TE, 8, false, 4);   /* 64 rows: two passes of 8 chunks (16 would spill) */
+    if (a->a_ln_gamma) TT2_SK(bf16, 4, true, 2);   // bf16, k == 512, m <= 32 (checked by the plan)
+    else if (a->dtype_in == TT2_F16) {
+      if (a->m <= 32) { TT2_SK_M(f16, 2) } else { TT2_SK_M(f16, 4) }
+    } else {
+      if (a->m <= 32) { TT2_SK_M(bf16, 2) } else { TT2_SK_M(bf16, 4) }
+    }
 #undef TT2_SK_M
 #undef TT2_SK
     return tt2_check_launch(hipGetLastError(), "tt2_gemm(skinny)");

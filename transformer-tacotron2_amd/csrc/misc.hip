@@ -19,10 +19,12 @@ int grid_for(int64_t total, int per = NT) {
 }
 
 TT2_DEV float ldf(const void* p, int64_t i, int dt) {
+  if (dt == TT2_F16) return (float)reinterpret_cast<const f16*>(p)[i];
   return dt == TT2_BF16 ? (float)reinterpret_cast<const bf16*>(p)[i] : reinterpret_cast<const float*>(p)[i];
 }
 TT2_DEV void stf(void* p, int64_t i, int dt, float v) {
-  if (dt == TT2_BF16) reinterpret_cast<bf16*>(p)[i] = (bf16)v;
+  if (dt == TT2_F16) reinterpret_cast<f16*>(p)[i] = (f16)v;
+  else if (dt == TT2_BF16) reinterpret_cast<bf16*>(p)[i] = (bf16)v;
   else reinterpret_cast<float*>(p)[i] = v;
 }
 

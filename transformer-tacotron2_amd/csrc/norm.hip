@@ -30,6 +30,11 @@ template <> TT2_DEV void ld8(const bf16* p, float (&v)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
 }
+template <> TT2_DEV void ld8(const f16* p, float (&v)[8]) {
+  f16x8 x = *reinterpret_cast<const f16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+}
 template <> TT2_DEV void ld8(const float* p, float (&v)[8]) {
   f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
 #pragma unroll
@@ -41,6 +46,12 @@ template <> TT2_DEV void st8(bf16* p, const float (&v)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) x[j] = (bf16)v[j];
   *reinterpret_cast<bf16x8*>(p) = x;
+}
+template <> TT2_DEV void st8(f16* p, const float (&v)[8]) {
+  f16x8 x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = (f16)v[j];
+  *reinterpret_cast<f16x8*>(p) = x;
 }
 template <> TT2_DEV void st8(float* p, const float (&v)[8]) {
   *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
@@ -95,9 +106,9 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(LnArgs a) {
 // 512 columns of a row, where part holds the raw partial sums of a skinny split-K
 // projection ([S][M][512] f32).  One wave per row, every load (x, the S slabs, bias,
 // gamma, beta) issued before the first reduction: one memory round trip.
-template <int S>
-__global__ __launch_bounds__(NT) void ln_combine_kernel(const bf16* x, const float* part, const float* bias,
-                                                        const float* gamma, const float* beta, bf16* y, int M,
+template <int S, typename T>
+__global__ __launch_bounds__(NT) void ln_combine_kernel(const T* x, const float* part, const float* bias,
+                                                        const float* gamma, const float* beta, T* y, int M,
                                                         float eps) {
   constexpr int C = 512;
   const int lane = threadIdx.x & 63;
@@ -552,21 +563,28 @@ extern "C" int tt2_layernorm_fwd(const tt2_ln_args* p, hipStream_t s) {
 
 extern "C" int tt2_ln_combine(const void* x, const float* part, int32_t splits, const float* bias,
                               const float* gamma, const float* beta, void* y, int32_t m, int32_t c, float eps,
-                              hipStream_t s) {
+                              int32_t dtype, hipStream_t s) {
   if (c != 512) return tt2_set_error(TT2_E_INVALID, "tt2_ln_combine: c must be 512");
   if (!x || !part || !bias || !gamma || !beta || !y) return tt2_set_error(TT2_E_INVALID, "tt2_ln_combine: null");
+  if (dtype != TT2_DT_BF16 && dtype != TT2_DT_F16) return tt2_set_error(TT2_E_INVALID, "tt2_ln_combine: bf16 / f16");
   if (m <= 0) return TT2_OK;
   const dim3 g((m + 3) / 4);
-  const bf16* X = reinterpret_cast<const bf16*>(x);
-  bf16* Y = reinterpret_cast<bf16*>(y);
+#define TT2_LNC(S)                                                                                             \
+  if (dtype == TT2_DT_F16)                                                                                     \
+    hipLaunchKernelGGL((ln_combine_kernel<S, f16>), g, dim3(NT), 0, s, (const f16*)x, part, bias, gamma, beta,  \
+                       (f16*)y, m, eps);                                                                       \
+  else                                                                                                         \
+    hipLaunchKernelGGL((ln_combine_kernel<S, bf16>), g, dim3(NT), 0, s, (const bf16*)x, part, bias, gamma, beta, \
+                       (bf16*)y, m, eps);
   switch (splits) {
-    case 1: hipLaunchKernelGGL(ln_combine_kernel<1>, g, dim3(NT), 0, s, X, part, bias, gamma, beta, Y, m, eps); break;
-    case 2: hipLaunchKernelGGL(ln_combine_kernel<2>, g, dim3(NT), 0, s, X, part, bias, gamma, beta, Y, m, eps); break;
-    case 4: hipLaunchKernelGGL(ln_combine_kernel<4>, g, dim3(NT), 0, s, X, part, bias, gamma, beta, Y, m, eps); break;
-    case 8: hipLaunchKernelGGL(ln_combine_kernel<8>, g, dim3(NT), 0, s, X, part, bias, gamma, beta, Y, m, eps); break;
-    case 16: hipLaunchKernelGGL(ln_combine_kernel<16>, g, dim3(NT), 0, s, X, part, bias, gamma, beta, Y, m, eps); break;
+    case 1: TT2_LNC(1) break;
+    case 2: TT2_LNC(2) break;
+    case 4: TT2_LNC(4) break;
+    case 8: TT2_LNC(8) break;
+    case 16: TT2_LNC(16) break;
     default: return tt2_set_error(TT2_E_INVALID, "tt2_ln_combine: splits must be 1, 2, 4, 8 or 16");
   }
+#undef TT2_LNC
   return tt2_check_launch(hipGetLastError(), "tt2_ln_combine");
 }
 

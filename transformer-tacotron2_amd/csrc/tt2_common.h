@@ -15,15 +15,19 @@ typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16;   // the fp16 decode path
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 #define TT2_DEV __device__ __forceinline__
 
 // ---------------------------------------------------------------- conversions
 TT2_DEV float to_f32(float x) { return x; }
 TT2_DEV float to_f32(bf16 x) { return (float)x; }
+TT2_DEV float to_f32(f16 x) { return (float)x; }
 template <typename T> TT2_DEV T from_f32(float x);
 template <> TT2_DEV float from_f32<float>(float x) { return x; }
 template <> TT2_DEV bf16 from_f32<bf16>(float x) { return (bf16)x; }
+template <> TT2_DEV f16 from_f32<f16>(float x) { return (f16)x; }
 
 // 16-byte chunk of T: 8 bf16 or 4 f32.
 template <typename T> struct Chunk { static constexpr int N = 16 / sizeof(T); };
@@ -146,5 +150,5 @@ TT2_DEV float max16(float v) {
   return v;
 }
 
-enum { TT2_F32 = 0, TT2_BF16 = 1 };
+enum { TT2_F32 = 0, TT2_BF16 = 1, TT2_F16 = 2 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("TT2_LIB") or os.path.join(_HERE, "libtt2.so")   # TT2
 
 DT_F32 = 0
 DT_BF16 = 1
+DT_F16 = 2
 ACT_NONE, ACT_RELU, ACT_TANH = 0, 1, 2
 
 vp = C.c_void_p
@@ -115,6 +116,8 @@ def dt(t: torch.Tensor) -> int:
         return DT_BF16
     if t.dtype == torch.float32:
         return DT_F32
+    if t.dtype == torch.float16:
+        return DT_F16
     raise TT2Error(f"unsupported dtype {t.dtype}")
 
 
@@ -205,7 +208,7 @@ SIGNATURES.update({
     "tt2_overlap_add": ([vp, i64, vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, i64, vp], C.c_int),
     "tt2_mel_rows": ([vp, i64, vp, vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, C.c_int32, vp],
                      C.c_int),
-    "tt2_ln_combine": ([vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp], C.c_int),
+    "tt2_ln_combine": ([vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_float, C.c_int32, vp], C.c_int),
     "tt2_batchnorm_workspace_size": ([P_(BnArgs)], sz),
     "tt2_batchnorm_fwd": ([P_(BnArgs), vp], C.c_int),
     "tt2_batchnorm_bwd": ([P_(BnArgs), vp], C.c_int),

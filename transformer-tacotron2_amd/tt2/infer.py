@@ -41,7 +41,11 @@ class _Slab:
 
 class Decoder:
     def __init__(self, engine: TTSEngine, batch: int, text_len: int, t_max: int, prenet_dropout: bool = False,
-                 seed: int = 0):
+                 seed: int = 0, dtype: torch.dtype | None = None):
+        """dtype: the decode step's storage type -- the engine's (bf16 / f32) by default, or
+        torch.float16 on a bf16 engine: the step then runs on an f16 copy of
+        the weights (refreshed from the f32 master at every encode()), an f16 KV cache and the
+        encoder memory's K/V cast to f16; the encoder and post-net stay in the engine's dtype."""
         self.e = e = engine
         c = e.cfg
         self.B, self.Tx, self.Tmax = batch, text_len, t_max
@@ -49,7 +53,11 @@ class Decoder:
             raise ValueError(f"t_max {t_max} exceeds the positional table ({c.max_len})")
         self.prenet_dropout = prenet_dropout
         self.seed0 = seed
-        dev, cd = e.dev, e.cd
+        dev = e.dev
+        cd = dtype or e.cd
+        self.dd = cd
+        if cd == torch.float16 and (e.cd != torch.bfloat16 or batch > 64):
+            raise ValueError("f16 decode needs a bf16 engine and batch <= 64 (the skinny decode kernels)")
         d, F = c.d_model, c.d_ffn
         B = batch
         self.A = e.arena(batch, text_len, t_max)   # encoder + post-net buffers (lazy)
@@ -70,7 +78,8 @@ class Decoder:
         self.emit_done = torch.zeros(1, dtype=torch.int32, device=dev)   # heads-GEMM arrival counter
         # bf16: the scaled PE rides in the pre-net projection's epilogue and the frame emit
         # in the heads GEMM's (skinny-path epilogues; 2 launches fewer per step)
-        self.fused_io = cd == torch.bfloat16 and batch <= 64
+        half = cd in (torch.bfloat16, torch.float16)
+        self.fused_io = half and batch <= 64
         self.graph = None
         # bf16 decode-step schedules: 0 no fusion, 1 KV-cache scatter in the QKV epilogue,
         # 2 also the LayerNorms as GEMM prologues (every workgroup recomputes the 32-row
@@ -78,9 +87,23 @@ class Decoder:
         # residual + LayerNorm combine kernel folds (tools/decode_ab.py measures them).
         # The skinny-path fusions need batch <= 64 (the LN prologues <= 32); larger batches
         # run unfused.
-        self.fuse = 3 if cd == torch.bfloat16 and batch <= 64 else 0
+        self.fuse = 3 if half and batch <= 64 else 0
         self.split_o, self.split_f = 4, 8
         self.slab = _Slab(torch.zeros(16 * max(B, 32) * d, dtype=torch.float32, device=dev))
+        if cd == torch.float16:
+            self.w16 = torch.zeros(e.lay.numel, dtype=torch.float16, device=dev)
+            self.mkv16 = torch.zeros(B * text_len, c.n_dec * 2 * d, dtype=torch.float16, device=dev)
+
+    def W(self, name):
+        """Weight view in the decode step's dtype."""
+        if self.dd == torch.float16:
+            return self.e.lay.view(self.w16, name)
+        return self.e.W(name)
+
+    @property
+    def mkv(self):
+        """Encoder memory K/V of all decoder layers [B * Tx, 6144] in the step's dtype."""
+        return self.mkv16 if self.dd == torch.float16 else self.A["mkv"]
 
     # ----------------------------------------------------------------- one step
     def step(self):
@@ -93,25 +116,25 @@ class Decoder:
         d1 = Drop(self.seed, SITE_INFER_FC1, pd) if pd > 0 else NO_DROP
         d2 = Drop(self.seed, SITE_INFER_FC2, pd) if pd > 0 else NO_DROP
         lin = e._lin
-        lin(self.prev, e.W("dec.fc1.w"), self.p1, B, c.dec_prenet, c.n_mels, bias=e.P("dec.fc1.b"), act=ACT_RELU,
+        lin(self.prev, self.W("dec.fc1.w"), self.p1, B, c.dec_prenet, c.n_mels, bias=e.P("dec.fc1.b"), act=ACT_RELU,
             drop=d1)
-        lin(self.p1, e.W("dec.fc2.w"), self.p2, B, c.dec_prenet, c.dec_prenet, bias=e.P("dec.fc2.b"), act=ACT_RELU,
+        lin(self.p1, self.W("dec.fc2.w"), self.p2, B, c.dec_prenet, c.dec_prenet, bias=e.P("dec.fc2.b"), act=ACT_RELU,
             drop=d2)
         if self.fused_io:
             # x0 = proj(p2) + alpha * pe[t], the scaled PE in the projection's epilogue
-            lin(self.p2, e.W("dec.proj.w"), self.x0, B, d, c.dec_prenet, bias=e.P("dec.proj.b"),
+            lin(self.p2, self.W("dec.proj.w"), self.x0, B, d, c.dec_prenet, bias=e.P("dec.proj.b"),
                 pe=(e.pe, e.P("dec.alpha"), self.t))
         else:
-            lin(self.p2, e.W("dec.proj.w"), self.proj, B, d, c.dec_prenet, bias=e.P("dec.proj.b"))
+            lin(self.p2, self.W("dec.proj.w"), self.proj, B, d, c.dec_prenet, bias=e.P("dec.proj.b"))
             ops.posenc_fwd(self.proj, e.P("dec.alpha"), e.pe, self.x0, B, 1, t_ptr=self.t)
-        mkv = A["mkv"]
+        mkv = self.mkv
         kvld = c.n_dec * 2 * d
         eps = c.ln_eps
         # Each post-LN is fused into the GEMM that consumes it (the skinny kernel
         # normalises its A rows and publishes the LN output for the residual path), and
         # the K/V columns of the QKV projection go straight into the KV cache: 8 kernels
         # per layer instead of 12.
-        if e.cd == torch.bfloat16 and self.fuse == 3:
+        if self.dd == torch.float16 or (e.cd == torch.bfloat16 and self.fuse == 3):
             return self._step_layers_split(B, d, F, H, scale)
         if e.cd != torch.bfloat16 or self.fuse < 2:
             return self._step_layers_unfused(lin, B, d, F, H, scale, kv_fused=e.cd == torch.bfloat16 and self.fuse == 1)
@@ -122,27 +145,27 @@ class Decoder:
             cache = self.cache[l]
             kv = (cache, self.t, d, self.Tmax * 2 * d, 2 * d)
             if ln_prev is None:
-                lin(x, e.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"), kv=kv)
+                lin(x, self.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"), kv=kv)
             else:
-                lin(x, e.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"), kv=kv, a_ln=ln_prev + (eps,))
+                lin(x, self.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"), kv=kv, a_ln=ln_prev + (eps,))
                 x = ln_prev[3]
             ops.attn_decode(self.qkv, cache, cache[:, :, d:], self.att, 3 * d, self.Tmax * 2 * d, 2 * d,
                             self.Tmax * 2 * d, 2 * d, d, B, H, self.Tmax, t_ptr=self.t, scale=scale)
-            lin(self.att, e.W(p + "o.w"), self.o, B, d, d, bias=e.P(p + "o.b"))
+            lin(self.att, self.W(p + "o.w"), self.o, B, d, d, bias=e.P(p + "o.b"))
             # h1 = LN1(x + o), fused into the cross-attention query projection
-            lin(x, e.W(p + "cq.w"), self.cq, B, d, d, bias=e.P(p + "cq.b"),
+            lin(x, self.W(p + "cq.w"), self.cq, B, d, d, bias=e.P(p + "cq.b"),
                 a_ln=(self.o, e.P(p + "ln1.g"), e.P(p + "ln1.b"), self.h1, eps))
             ko = 2 * d * l
             ops.attn_decode(self.cq, mkv[:, ko:], mkv[:, ko + d:], self.catt, d, self.Tx * kvld, kvld,
                             self.Tx * kvld, kvld, d, B, H, self.Tx, key_len=A["text_len"], scale=scale)
-            lin(self.catt, e.W(p + "co.w"), self.co, B, d, d, bias=e.P(p + "co.b"))
+            lin(self.catt, self.W(p + "co.w"), self.co, B, d, d, bias=e.P(p + "co.b"))
             # h2 = LN2(h1 + co), fused into FFN1
-            lin(self.h1, e.W(p + "ffn1.w"), self.f1, B, F, d, bias=e.P(p + "ffn1.b"), act=ACT_RELU,
+            lin(self.h1, self.W(p + "ffn1.w"), self.f1, B, F, d, bias=e.P(p + "ffn1.b"), act=ACT_RELU,
                 a_ln=(self.co, e.P(p + "ln2.g"), e.P(p + "ln2.b"), self.h2, eps))
-            lin(self.f1, e.W(p + "ffn2.w"), self.f2, B, d, F, bias=e.P(p + "ffn2.b"))
+            lin(self.f1, self.W(p + "ffn2.w"), self.f2, B, d, F, bias=e.P(p + "ffn2.b"))
             # LN3(h2 + f2) is fused into the next consumer (next layer's QKV, or the heads)
             x, ln_prev = self.h2, (self.f2, e.P(p + "ln3.g"), e.P(p + "ln3.b"), xs[l % 2])
-        lin(x, e.W("heads.w"), self.heads, B, c.n_mels + 1, d, bias=e.P("heads.b"), ldo=96,
+        lin(x, self.W("heads.w"), self.heads, B, c.n_mels + 1, d, bias=e.P("heads.b"), ldo=96,
             a_ln=ln_prev + (eps,), emit=self._emit_args())
 
     def _step_layers_split(self, B, d, F, H, scale):
@@ -154,7 +177,7 @@ class Decoder:
         e, c, A = self.e, self.e.cfg, self.A
         lin = e._lin
         x = self.x0
-        mkv = A["mkv"]
+        mkv = self.mkv
         kvld = c.n_dec * 2 * d
         eps = c.ln_eps
         slab = self.slab
@@ -165,22 +188,22 @@ class Decoder:
         for l in range(c.n_dec):
             p = f"dec{l}."
             cache = self.cache[l]
-            lin(x, e.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"),
+            lin(x, self.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"),
                 kv=(cache, self.t, d, self.Tmax * 2 * d, 2 * d))
             ops.attn_decode(self.qkv, cache, cache[:, :, d:], self.att, 3 * d, self.Tmax * 2 * d, 2 * d,
                             self.Tmax * 2 * d, 2 * d, d, B, H, self.Tmax, t_ptr=self.t, scale=scale)
-            split(self.att, e.W(p + "o.w"), d, d, self.split_o)
+            split(self.att, self.W(p + "o.w"), d, d, self.split_o)
             ops.ln_combine(x, slab.t, self.split_o, e.P(p + "o.b"), e.P(p + "ln1.g"), e.P(p + "ln1.b"), self.h1, B,
                            eps)
-            lin(self.h1, e.W(p + "cq.w"), self.cq, B, d, d, bias=e.P(p + "cq.b"))
+            lin(self.h1, self.W(p + "cq.w"), self.cq, B, d, d, bias=e.P(p + "cq.b"))
             ko = 2 * d * l
             ops.attn_decode(self.cq, mkv[:, ko:], mkv[:, ko + d:], self.catt, d, self.Tx * kvld, kvld,
                             self.Tx * kvld, kvld, d, B, H, self.Tx, key_len=A["text_len"], scale=scale)
-            split(self.catt, e.W(p + "co.w"), d, d, self.split_o)
+            split(self.catt, self.W(p + "co.w"), d, d, self.split_o)
             ops.ln_combine(self.h1, slab.t, self.split_o, e.P(p + "co.b"), e.P(p + "ln2.g"), e.P(p + "ln2.b"),
                            self.h2, B, eps)
-            lin(self.h2, e.W(p + "ffn1.w"), self.f1, B, F, d, bias=e.P(p + "ffn1.b"), act=ACT_RELU)
-            split(self.f1, e.W(p + "ffn2.w"), d, F, self.split_f)
+            lin(self.h2, self.W(p + "ffn1.w"), self.f1, B, F, d, bias=e.P(p + "ffn1.b"), act=ACT_RELU)
+            split(self.f1, self.W(p + "ffn2.w"), d, F, self.split_f)
             xn = self.xa if x is not self.xa else self.xb
             ops.ln_combine(self.h2, slab.t, self.split_f, e.P(p + "ffn2.b"), e.P(p + "ln3.g"), e.P(p + "ln3.b"),
                            xn, B, eps)
@@ -196,10 +219,10 @@ class Decoder:
     def _heads(self, x):
         c, e = self.e.cfg, self.e
         if self.fused_io:
-            e._lin(x, e.W("heads.w"), self.heads, self.B, c.n_mels + 1, c.d_model, bias=e.P("heads.b"), ldo=96,
+            e._lin(x, self.W("heads.w"), self.heads, self.B, c.n_mels + 1, c.d_model, bias=e.P("heads.b"), ldo=96,
                    emit=self._emit_args())
         else:
-            e._lin(x, e.W("heads.w"), self.heads, self.B, c.n_mels + 1, c.d_model, bias=e.P("heads.b"), ldo=96)
+            e._lin(x, self.W("heads.w"), self.heads, self.B, c.n_mels + 1, c.d_model, bias=e.P("heads.b"), ldo=96)
             self._emit()
 
     def _emit(self):
@@ -212,29 +235,29 @@ class Decoder:
         separate kernel too unless kv_fused (bf16 skinny-GEMM epilogue scatter)."""
         e, c, A = self.e, self.e.cfg, self.A
         x, xn = self.x0, self.xa
-        mkv = A["mkv"]
+        mkv = self.mkv
         kvld = c.n_dec * 2 * d
         for l in range(c.n_dec):
             p = f"dec{l}."
             cache = self.cache[l]
             if kv_fused:
-                lin(x, e.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"),
+                lin(x, self.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"),
                     kv=(cache, self.t, d, self.Tmax * 2 * d, 2 * d))
             else:
-                lin(x, e.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"))
+                lin(x, self.W(p + "qkv.w"), self.qkv, B, 3 * d, d, bias=e.P(p + "qkv.b"))
                 ops.kv_append(self.qkv[:, d:], 3 * d, cache, self.Tmax * 2 * d, 2 * d, 2 * d, B, self.t)
             ops.attn_decode(self.qkv, cache, cache[:, :, d:], self.att, 3 * d, self.Tmax * 2 * d, 2 * d,
                             self.Tmax * 2 * d, 2 * d, d, B, H, self.Tmax, t_ptr=self.t, scale=scale)
-            lin(self.att, e.W(p + "o.w"), self.o, B, d, d, bias=e.P(p + "o.b"))
+            lin(self.att, self.W(p + "o.w"), self.o, B, d, d, bias=e.P(p + "o.b"))
             ops.layernorm_fwd(x, self.o, e.P(p + "ln1.g"), e.P(p + "ln1.b"), self.h1, None, None, B, c.ln_eps)
-            lin(self.h1, e.W(p + "cq.w"), self.cq, B, d, d, bias=e.P(p + "cq.b"))
+            lin(self.h1, self.W(p + "cq.w"), self.cq, B, d, d, bias=e.P(p + "cq.b"))
             ko = 2 * d * l
             ops.attn_decode(self.cq, mkv[:, ko:], mkv[:, ko + d:], self.catt, d, self.Tx * kvld, kvld,
                             self.Tx * kvld, kvld, d, B, H, self.Tx, key_len=A["text_len"], scale=scale)
-            lin(self.catt, e.W(p + "co.w"), self.co, B, d, d, bias=e.P(p + "co.b"))
+            lin(self.catt, self.W(p + "co.w"), self.co, B, d, d, bias=e.P(p + "co.b"))
             ops.layernorm_fwd(self.h1, self.co, e.P(p + "ln2.g"), e.P(p + "ln2.b"), self.h2, None, None, B, c.ln_eps)
-            lin(self.h2, e.W(p + "ffn1.w"), self.f1, B, F, d, bias=e.P(p + "ffn1.b"), act=ACT_RELU)
-            lin(self.f1, e.W(p + "ffn2.w"), self.f2, B, d, F, bias=e.P(p + "ffn2.b"))
+            lin(self.h2, self.W(p + "ffn1.w"), self.f1, B, F, d, bias=e.P(p + "ffn1.b"), act=ACT_RELU)
+            lin(self.f1, self.W(p + "ffn2.w"), self.f2, B, d, F, bias=e.P(p + "ffn2.b"))
             ops.layernorm_fwd(self.h2, self.f2, e.P(p + "ln3.g"), e.P(p + "ln3.b"), xn, None, None, B, c.ln_eps)
             x, xn = xn, (self.xb if xn is self.xa else self.xa)
         self._heads(x)
@@ -253,6 +276,10 @@ class Decoder:
         A["text_len"].copy_(text_len.to(torch.int32))
         e.forward_encoder(A)
         e.training = was
+        if self.dd == torch.float16:
+            self.w16.copy_(e.params)
+            kvld = self.mkv16.shape[1]
+            ops.cast2d(A["mkv"], kvld, self.mkv16, kvld, self.mkv16.shape[0], kvld)
 
     def capture(self):
         """Record one decode step as a hipGraph (run after encode(); the warm-up

@@ -288,7 +288,8 @@ def layernorm_fwd(x, branch, gamma, beta, y, mean, rstd, m, eps=1e-5, drop: Drop
 def ln_combine(x, part, splits, bias, gamma, beta, y, m, eps=1e-5):
     """y = LN(x + bias + sum_s part[s]) (decode step; part = a skinny split-K GEMM's slabs)."""
     check(lib().tt2_ln_combine(x.data_ptr(), part.data_ptr(), splits, bias.data_ptr(), gamma.data_ptr(),
-                               beta.data_ptr(), y.data_ptr(), m, x.shape[-1], eps, stream_ptr()), "tt2_ln_combine")
+                               beta.data_ptr(), y.data_ptr(), m, x.shape[-1], eps, dt(x), stream_ptr()),
+          "tt2_ln_combine")
 
 
 def layernorm_bwd(dy, x, branch, gamma, mean, rstd, dx, dbranch, dgamma, dbeta, m, drop: Drop = NO_DROP,
