@@ -12,7 +12,7 @@
  *  - Calls are stream-ordered on the caller's stream and reentrant.
  *  - Return 0 (TT2_OK) or a negative TT2_E_* code; tt2_last_error() returns a
  *    thread-local message for the last failure on this thread.
- *  - dtype fields: TT2_DT_F32 = 0, TT2_DT_BF16 = 1.  Activations are
+ *  - dtype fields: TT2_DT_F32 = 0, TT2_DT_BF16 = 1, TT2_DT_F16 = 2 (decode step only).  Activations are
  *    channels-last row-major [rows, channels]; rows = batch * time.
  *  - Dropout: keep(idx) = hash(seed, site, idx) >= thr; thr = 0
  *    disables it.  seed points to a device uint32.
