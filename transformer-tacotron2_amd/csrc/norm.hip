@@ -355,14 +355,16 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
   }
 }
 
-// grid ceil(C/16): 16 columns x 16 chunk groups per block.  Exact two-pass combine of
+// grid ceil(C/4): 4 columns x 64 chunk groups per block (C = 512 -> 128 blocks, each
+// lane combining ~R/64 chunks with its loads unrolled 4 deep).  Exact two-pass combine of
 // the chunk moments (no per-chunk division): mean = sum n_c mean_c / n, then
 // M2 = sum M2_c + n_c (mean_c - mean)^2, accumulated in double.
+constexpr int BNF_COLS = 4, BNF_GROUPS = 64;
 __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
-  __shared__ double red[16][17];
-  __shared__ double smean[16];
-  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+  __shared__ double red[BNF_GROUPS][BNF_COLS + 1];
+  __shared__ double smean[BNF_COLS];
+  const int cl = threadIdx.x % BNF_COLS, g = threadIdx.x / BNF_COLS;
+  const int c = blockIdx.x * BNF_COLS + cl;
   if (!a.training) {
     if (g == 0 && c < a.C) {
       a.mean[c] = a.run_mean[c];
@@ -371,32 +373,52 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
     return;
   }
   const bool ok = c < a.C;
+  const int cc = ok ? c : 0;
+  auto nrows = [&](int r) { return (double)min(a.rows_per, a.M - r * a.rows_per); };
   double acc = 0.0;
-  if (ok)
-    for (int r = g; r < a.R; r += 16)
-      acc += (double)min(a.rows_per, a.M - r * a.rows_per) * a.part[((int64_t)r * 2 + 0) * a.C + c];
+  int r = g;
+  for (; r + 3 * BNF_GROUPS < a.R; r += 4 * BNF_GROUPS) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = a.part[((int64_t)(r + u * BNF_GROUPS) * 2 + 0) * a.C + cc];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += nrows(r + u * BNF_GROUPS) * v[u];
+  }
+  for (; r < a.R; r += BNF_GROUPS) acc += nrows(r) * a.part[((int64_t)r * 2 + 0) * a.C + cc];
   red[g][cl] = acc;
   __syncthreads();
   if (g == 0) {
     double t = 0.0;
-    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    for (int k = 0; k < BNF_GROUPS; ++k) t += red[k][cl];
     smean[cl] = t / a.M;
   }
   __syncthreads();
   const double mu = smean[cl];
   acc = 0.0;
-  if (ok)
-    for (int r = g; r < a.R; r += 16) {
-      const double nb = min(a.rows_per, a.M - r * a.rows_per);
-      const double d = a.part[((int64_t)r * 2 + 0) * a.C + c] - mu;
-      acc += a.part[((int64_t)r * 2 + 1) * a.C + c] + nb * d * d;
+  r = g;
+  for (; r + 3 * BNF_GROUPS < a.R; r += 4 * BNF_GROUPS) {
+    float m1[4], m2[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      m1[u] = a.part[((int64_t)(r + u * BNF_GROUPS) * 2 + 0) * a.C + cc];
+      m2[u] = a.part[((int64_t)(r + u * BNF_GROUPS) * 2 + 1) * a.C + cc];
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double d = m1[u] - mu;
+      acc += m2[u] + nrows(r + u * BNF_GROUPS) * d * d;
+    }
+  }
+  for (; r < a.R; r += BNF_GROUPS) {
+    const double d = a.part[((int64_t)r * 2 + 0) * a.C + cc] - mu;
+    acc += a.part[((int64_t)r * 2 + 1) * a.C + cc] + nrows(r) * d * d;
+  }
   __syncthreads();
   red[g][cl] = acc;
   __syncthreads();
   if (g != 0 || !ok) return;
   double m2 = 0.0;
-  for (int k = 0; k < 16; ++k) m2 += red[k][cl];
+  for (int k = 0; k < BNF_GROUPS; ++k) m2 += red[k][cl];
   const double n = a.M;
   const double var = m2 / n;
   a.mean[c] = (float)mu;
@@ -495,21 +517,32 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
 }
 
 __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(BnArgs a) {
-  __shared__ float red[2][16][17];
-  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+  __shared__ float red[2][BNF_GROUPS][BNF_COLS + 1];
+  const int cl = threadIdx.x % BNF_COLS, g = threadIdx.x / BNF_COLS;
+  const int c = blockIdx.x * BNF_COLS + cl;
+  const int cc = c < a.C ? c : 0;
   float s1 = 0.f, s2 = 0.f;
-  if (c < a.C)
-    for (int r = g; r < a.R; r += 16) {
-      s1 += a.part[((int64_t)r * 2 + 0) * a.C + c];
-      s2 += a.part[((int64_t)r * 2 + 1) * a.C + c];
+  int r = g;
+  for (; r + 3 * BNF_GROUPS < a.R; r += 4 * BNF_GROUPS) {
+    float v1[4], v2[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v1[u] = a.part[((int64_t)(r + u * BNF_GROUPS) * 2 + 0) * a.C + cc];
+      v2[u] = a.part[((int64_t)(r + u * BNF_GROUPS) * 2 + 1) * a.C + cc];
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { s1 += v1[u]; s2 += v2[u]; }
+  }
+  for (; r < a.R; r += BNF_GROUPS) {
+    s1 += a.part[((int64_t)r * 2 + 0) * a.C + cc];
+    s2 += a.part[((int64_t)r * 2 + 1) * a.C + cc];
+  }
   red[0][g][cl] = s1;
   red[1][g][cl] = s2;
   __syncthreads();
   if (g != 0 || c >= a.C) return;
   float t1 = 0.f, t2 = 0.f;
-  for (int k = 0; k < 16; ++k) { t1 += red[0][k][cl]; t2 += red[1][k][cl]; }
+  for (int k = 0; k < BNF_GROUPS; ++k) { t1 += red[0][k][cl]; t2 += red[1][k][cl]; }
   a.dbeta[c] = t1;
   a.dgamma[c] = t2;
 }
@@ -670,7 +703,7 @@ extern "C" int tt2_batchnorm_fwd(const tt2_bn_args* p, hipStream_t s) {
     if (bf) hipLaunchKernelGGL(bn_stats_kernel<bf16>, dim3(a.R), dim3(NT), 0, s, a);
     else hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(a.R), dim3(NT), 0, s, a);
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + 15) / 16), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
   const int g = grid_for((int64_t)p->m * p->c / 8);
   if (bf) hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(g), dim3(NT), 0, s, a);
   else hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(g), dim3(NT), 0, s, a);
@@ -691,7 +724,7 @@ extern "C" int tt2_batchnorm_bwd(const tt2_bn_args* p, hipStream_t s) {
   else if (dbf) hipLaunchKernelGGL((KER<float, bf16>), grid, dim3(NT), 0, s, a);                \
   else hipLaunchKernelGGL((KER<float, float>), grid, dim3(NT), 0, s, a);
   TT2_BN_DISPATCH(bn_bwd_stats_kernel, dim3(a.R))
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + 15) / 16), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
   const int ga = grid_for((int64_t)p->m * p->c / 8);
   TT2_BN_DISPATCH(bn_bwd_apply_kernel, dim3(ga))
 #undef TT2_BN_DISPATCH
