@@ -31,27 +31,38 @@ TT2_DEV void stf(void* p, int64_t i, int dt, float v) {
 // dst[c] = beta * dst[c] + sum_r src[r * ld + c]   (fixed order)
 // block = 16 columns x 16 row groups (short dependent chains); LDS combine in a fixed order.
 constexpr int RR_COLS = 16;
+// block = CW columns x (NT / CW) row groups, CW = min(16, cols rounded up to a power of
+// two): narrow reductions (the Adam norm's 1024 x 1 partials) use every lane.  Each lane
+// sums its rows two at a time; the group sums combine in a fixed order (two levels).
 __global__ __launch_bounds__(NT) void reduce_rows_kernel(const float* src, int rows, int cols, int64_t ld, float* dst,
-                                                         float beta) {
-  __shared__ float red[16][RR_COLS + 1];
-  const int cl = threadIdx.x & (RR_COLS - 1), g = threadIdx.x / RR_COLS;
-  const int c = blockIdx.x * RR_COLS + cl;
+                                                         float beta, int cw) {
+  __shared__ float red[NT];
+  const int G = NT / cw;
+  const int cl = threadIdx.x % cw, g = threadIdx.x / cw;
+  const int c = blockIdx.x * cw + cl;
   float s0 = 0.f, s1 = 0.f;
   if (c < cols) {
     int r = g;
-    for (; r + 16 < rows; r += 32) {
+    for (; r + G < rows; r += 2 * G) {
       s0 += src[(int64_t)r * ld + c];
-      s1 += src[(int64_t)(r + 16) * ld + c];
+      s1 += src[(int64_t)(r + G) * ld + c];
     }
     if (r < rows) s0 += src[(int64_t)r * ld + c];
   }
-  red[g][cl] = s0 + s1;
+  red[threadIdx.x] = s0 + s1;
+  __syncthreads();
+  // level 1: 16 partial sums per column over strided groups; level 2: lane g == 0
+  const int P = G < 16 ? G : 16;
+  float t1 = 0.f;
+  if (g < P)
+    for (int k = g; k < G; k += P) t1 += red[k * cw + cl];
+  __syncthreads();
+  if (g < P) red[g * cw + cl] = t1;
   __syncthreads();
   if (g == 0 && c < cols) {
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) s += red[k][cl];
-    dst[c] = beta != 0.f ? beta * dst[c] + s : s;
+    float t = 0.f;
+    for (int k = 0; k < P; ++k) t += red[k * cw + cl];
+    dst[c] = beta != 0.f ? beta * dst[c] + t : t;
   }
 }
 
@@ -275,14 +286,25 @@ __global__ __launch_bounds__(NT) void loss_kernel(const float* heads, int64_t hl
   }
 }
 
+// one wave: lane l sums partial rows l, l + 64, ... (loads issued together), then lane 0
+// adds the 64 lane sums in lane order (fixed order: reproducible)
 __global__ void loss_finalize_kernel(const float* part, int nblocks, const int32_t* mel_len, int B, int Tlen, int NM,
                                      float* out) {
-  if (threadIdx.x != 0) return;
+  __shared__ float red[3][64];
+  const int l = threadIdx.x;
+  float a[3] = {0.f, 0.f, 0.f};
+  for (int i = l; i < nblocks; i += 64) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(part + i * 4);
+    a[0] += v[0]; a[1] += v[1]; a[2] += v[2];
+  }
+  red[0][l] = a[0]; red[1][l] = a[1]; red[2][l] = a[2];
+  __syncthreads();
+  if (l != 0) return;
   int nvalid = 0;
   for (int b = 0; b < B; ++b) nvalid += min(max(mel_len[b], 0), Tlen);
   float s[3] = {0.f, 0.f, 0.f};
   for (int k = 0; k < 3; ++k)
-    for (int i = 0; i < nblocks; ++i) s[k] += part[i * 4 + k];
+    for (int i = 0; i < 64; ++i) s[k] += red[k][i];
   const float n = nvalid > 0 ? (float)nvalid : 1.f;
   out[1] = s[0] / (n * NM);
   out[2] = s[1] / (n * NM);
@@ -402,9 +424,10 @@ __global__ void step_bump_kernel(int32_t* step, uint32_t* seed) {
 // =============================================================== C ABI
 extern "C" int tt2_reduce_rows(const tt2_reduce_args* p, hipStream_t s) {
   if (p->cols <= 0) return TT2_OK;
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((p->cols + RR_COLS - 1) / RR_COLS), dim3(NT), 0, s, p->src, p->rows,
-                     p->cols,
-                     p->ld, p->dst, p->beta);
+  int cw = 1;
+  while (cw < p->cols && cw < RR_COLS) cw <<= 1;
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((p->cols + cw - 1) / cw), dim3(NT), 0, s, p->src, p->rows, p->cols,
+                     p->ld, p->dst, p->beta, cw);
   return tt2_check_launch(hipGetLastError(), "tt2_reduce_rows");
 }
 
@@ -428,7 +451,7 @@ extern "C" int tt2_colsum(const void* x, int dtype, int64_t ld, int m, int n, fl
     hipLaunchKernelGGL(colsum_partial_kernel<float>, g, dim3(NT), 0, s, (const float*)x, ld, m, n, rows_per, vec,
                        part);
   hipLaunchKernelGGL(reduce_rows_kernel, dim3((n + RR_COLS - 1) / RR_COLS), dim3(NT), 0, s, part, R, n, (int64_t)n,
-                     dst, beta);
+                     dst, beta, RR_COLS);
   return tt2_check_launch(hipGetLastError(), "tt2_colsum");
 }
 
@@ -485,7 +508,7 @@ extern "C" int tt2_posenc_bwd(const tt2_pe_args* p, hipStream_t s) {
     hipLaunchKernelGGL(pe_bwd_kernel<float>, dim3(TT2_PE_BWD_BLOCKS), dim3(NT), 0, s, (const float*)p->dout, p->pe,
                        (float*)p->dx, part, p->m, p->c, p->t, d);
   hipLaunchKernelGGL(reduce_rows_kernel, dim3(1), dim3(NT), 0, s, part, TT2_PE_BWD_BLOCKS, 1, (int64_t)1,
-                     p->dalpha, 0.f);
+                     p->dalpha, 0.f, 1);
   return tt2_check_launch(hipGetLastError(), "tt2_posenc_bwd");
 }
 
@@ -555,7 +578,7 @@ extern "C" int tt2_adam_step(const tt2_adam_args* p, hipStream_t s) {
     float* total = part + TT2_ADAM_NORM_BLOCKS;
     hipLaunchKernelGGL(sumsq_kernel, dim3(TT2_ADAM_NORM_BLOCKS), dim3(NT), 0, s, p->grads, p->n, part);
     hipLaunchKernelGGL(reduce_rows_kernel, dim3(1), dim3(NT), 0, s, part, TT2_ADAM_NORM_BLOCKS, 1, (int64_t)1, total,
-                       0.f);
+                       0.f, 1);
     a.sumsq = total;
   }
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(p->n / 4)), dim3(NT), 0, s, a);
