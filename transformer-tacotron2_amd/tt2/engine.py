@@ -190,6 +190,8 @@ class TTSEngine:
                  seed: int = 0):
         self.cfg = c = cfg or TTSConfig()
         assert c.d_model == 512 and c.head_dim == 64, "kernels are built for d_model 512, head_dim 64"
+        self._heads_pad = None   # bf16 backward: heads GEMMs padded to 88 rows (see backward)
+        self.pad_heads = True
         self._wq = None   # weight-gradient requests queued for one grouped launch (see _defer_wgrads)
         self.cd = dtype
         self.dev = torch.device(device)
@@ -496,9 +498,24 @@ class TTSEngine:
         nh = c.n_mels + 1
         ops.cast2d(A["g_heads"], A.heads_ld, A["gh_cd"], A.heads_ld, Md, nh)
         x_top = A[f"dx{c.n_dec}"]
-        self._wgrad(A["gh_cd"], x_top, self.G("heads.w"), nh, d, Md, ldy=A.heads_ld, gb=self.G("heads.b"))
         gx, gx2 = A["g_xa"], A["g_xb"]
-        self._dgrad(A["gh_cd"], self.W("heads.w"), gx, Md, d, nh, ldy=A.heads_ld)
+        if cd == torch.bfloat16 and self.pad_heads:
+            # the 81 head rows padded to 88 (gh_cd columns 81.. are zero) so both products take
+            # the LDS-DMA kernels instead of the register-staged one (odd inner dimension)
+            nhp = 88
+            if self._heads_pad is None:
+                self._heads_pad = (torch.zeros(nhp, d, dtype=torch.float32, device=self.dev),
+                                   torch.zeros(nhp, dtype=torch.float32, device=self.dev),
+                                   torch.zeros(nhp, d, dtype=cd, device=self.dev))
+            gw_p, gb_p, w_p = self._heads_pad
+            self._wgrad(A["gh_cd"], x_top, gw_p, nhp, d, Md, ldy=A.heads_ld, gb=gb_p)
+            ops.cast2d(gw_p, d, self.G("heads.w"), d, nh, d)
+            ops.cast2d(gb_p, nhp, self.G("heads.b"), nh, 1, nh)
+            ops.cast2d(self.W("heads.w"), d, w_p, d, nh, d)
+            self._dgrad(A["gh_cd"], w_p, gx, Md, d, nhp, ldy=A.heads_ld)
+        else:
+            self._wgrad(A["gh_cd"], x_top, self.G("heads.w"), nh, d, Md, ldy=A.heads_ld, gb=self.G("heads.b"))
+            self._dgrad(A["gh_cd"], self.W("heads.w"), gx, Md, d, nh, ldy=A.heads_ld)
         self._ready("heads.w")
         # ---------------- decoder layers
         mkv = A["mkv"]
