@@ -102,3 +102,16 @@ def test_batchnorm_train_fwd_bwd(dtype, m, c, act, res):
     assert rel(dy, yr.grad) < tol_b
     assert rel(dg, gr.grad) < tol_b
     assert rel(db, br.grad) < tol_b
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cout,cin", [(512, 512), (80, 512), (512, 80), (100, 70)])
+def test_conv_weight_flip(dtype, cout, cin):
+    """wd[ci][tap'][co] = w[co][K-1-tap'][ci] (the conv dgrad weight, internal [Cout][tap][Cin])."""
+    from tt2 import ops
+    K = 5
+    w = torch.randn(cout, K, cin, device="cuda").to(dtype)
+    wd = torch.empty(cin, K * cout, device="cuda", dtype=dtype)
+    ops.conv_weight_flip(w, wd, cout, cin, K)
+    ref = w.flip(1).permute(2, 1, 0).reshape(cin, K * cout)
+    assert torch.equal(wd, ref)

@@ -313,15 +313,24 @@ __global__ void loss_finalize_kernel(const float* part, int nblocks, const int32
 }
 
 // ------------------------------------------------------------ weight repack
-// conv dgrad weight: wd[ci][tap'][co] = w[co][K-1-tap'][ci]
+// conv dgrad weight: wd[ci][tap'][co] = w[co][K-1-tap'][ci] -- per tap a [Cout x Cin] ->
+// [Cin x Cout] transpose through a 64 x 64 LDS tile: reads coalesced along ci, writes along co.
 template <typename T>
-__global__ void conv_wflip_kernel(const T* w, T* wd, int Cout, int Cin, int K) {
-  const int64_t total = (int64_t)Cout * Cin * K;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
-    const int ci = (int)(i / ((int64_t)K * Cout));
-    const int rem = (int)(i % ((int64_t)K * Cout));
-    const int tp = rem / Cout, co = rem % Cout;
-    wd[i] = w[((int64_t)co * K + (K - 1 - tp)) * Cin + ci];
+__global__ __launch_bounds__(NT) void conv_wflip_kernel(const T* w, T* wd, int Cout, int Cin, int K) {
+  __shared__ T tile[64][65];
+  const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64, tap = blockIdx.z;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int r = ty; r < 64; r += NT / 64) {
+    const int co = co0 + r, ci = ci0 + tx;
+    if (co < Cout && ci < Cin) tile[r][tx] = w[((int64_t)co * K + tap) * Cin + ci];
+  }
+  __syncthreads();
+  const int tp = K - 1 - tap;
+#pragma unroll 4
+  for (int r = ty; r < 64; r += NT / 64) {
+    const int ci = ci0 + r, co = co0 + tx;
+    if (co < Cout && ci < Cin) wd[((int64_t)ci * K + tp) * Cout + co] = tile[tx][r];
   }
 }
 
@@ -550,11 +559,12 @@ extern "C" int tt2_tts_loss(const tt2_loss_args* p, hipStream_t s) {
 }
 
 extern "C" int tt2_conv_weight_flip(const void* w, void* wd, int cout, int cin, int k, int dtype, hipStream_t s) {
-  const int g = grid_for((int64_t)cout * cin * k);
+  if (cout <= 0 || cin <= 0 || k <= 0) return TT2_OK;
+  const dim3 g((cin + 63) / 64, (cout + 63) / 64, k);
   if (dtype == TT2_DT_BF16)
-    hipLaunchKernelGGL(conv_wflip_kernel<bf16>, dim3(g), dim3(NT), 0, s, (const bf16*)w, (bf16*)wd, cout, cin, k);
+    hipLaunchKernelGGL(conv_wflip_kernel<bf16>, g, dim3(NT), 0, s, (const bf16*)w, (bf16*)wd, cout, cin, k);
   else
-    hipLaunchKernelGGL(conv_wflip_kernel<float>, dim3(g), dim3(NT), 0, s, (const float*)w, (float*)wd, cout, cin, k);
+    hipLaunchKernelGGL(conv_wflip_kernel<float>, g, dim3(NT), 0, s, (const float*)w, (float*)wd, cout, cin, k);
   return tt2_check_launch(hipGetLastError(), "tt2_conv_weight_flip");
 }
 
