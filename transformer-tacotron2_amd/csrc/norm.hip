@@ -72,18 +72,41 @@ struct LnArgs {
   DropDesc drop;
 };
 
+template <typename T> TT2_DEV void unpack8(const uint4 (&u)[sizeof(T) / 2], float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    union { uint4 q; bf16x8 b; } c;
+    c.q = u[0];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)c.b[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = __uint_as_float((&u[0].x)[j]); v[4 + j] = __uint_as_float((&u[1].x)[j]); }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void ln_fwd_kernel(LnArgs a) {
+  constexpr int NV = sizeof(T) / 2;   // 16-B vectors per 8 elements
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= a.M) return;
   const int c0 = lane * 8;
   const int64_t off = (int64_t)row * a.C + c0;
+  // every load of the row first (x, branch, gamma, beta, the dropout seed): one round trip
+  // (a branch-dependent load behind the x unpack used to cost a second one)
+  const bool has_br = a.branch != nullptr;
+  const uint4* X = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.x) + off);
+  const uint4* BR = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(has_br ? a.branch : a.x) + off);
+  uint4 xr[NV], brr[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) { xr[v] = X[v]; brr[v] = BR[v]; }
+  const f32x4 g0 = *reinterpret_cast<const f32x4*>(a.gamma + c0), g1 = *reinterpret_cast<const f32x4*>(a.gamma + c0 + 4);
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.beta + c0), b1 = *reinterpret_cast<const f32x4*>(a.beta + c0 + 4);
+  const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
   float s[8], br[8];
-  ld8(reinterpret_cast<const T*>(a.x) + off, s);
-  if (a.branch) {
-    ld8(reinterpret_cast<const T*>(a.branch) + off, br);
-    const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
+  unpack8<T>(xr, s);
+  if (has_br) {
+    unpack8<T>(brr, br);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[j] += a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)(off + j), br[j]) : br[j];
   }
@@ -97,7 +120,10 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(LnArgs a) {
   const float rstd = rsqrtf(wave_sum(sq) / a.C + a.eps);
   float y[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) y[j] = (s[j] - mean) * rstd * a.gamma[c0 + j] + a.beta[c0 + j];
+  for (int j = 0; j < 4; ++j) {
+    y[j] = (s[j] - mean) * rstd * g0[j] + b0[j];
+    y[4 + j] = (s[4 + j] - mean) * rstd * g1[j] + b1[j];
+  }
   st8(reinterpret_cast<T*>(a.y) + off, y);
   if (lane == 0 && a.mean) { a.mean[row] = mean; a.rstd[row] = rstd; }
 }
@@ -168,17 +194,6 @@ TT2_DEV void ln_row_load(LnRow<T>& r, const LnArgs& a, int row, int c0) {
   r.rstd = a.rstd[row];
 }
 
-template <typename T> TT2_DEV void unpack8(const uint4 (&u)[sizeof(T) / 2], float (&v)[8]) {
-  if constexpr (sizeof(T) == 2) {
-    union { uint4 q; bf16x8 b; } c;
-    c.q = u[0];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (float)c.b[j];
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { v[j] = __uint_as_float((&u[0].x)[j]); v[4 + j] = __uint_as_float((&u[1].x)[j]); }
-  }
-}
 
 template <typename T>
 __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
