@@ -18,7 +18,7 @@
 // Backward (no atomics, bitwise reproducible): attn_bwd_dq walks key tiles per
 // query block (dQ), attn_bwd_dkdv walks query tiles per key block (dK, dV);
 // both recompute P from the saved LSE.  delta = rowsum(dO * O) comes from
-// attn_bwd_prep.
+// attn_bwd_prep (f32 / v1 path) or from the v3 dQ kernel, which runs first.
 #include <math.h>
 
 #include <type_traits>
@@ -722,11 +722,22 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
   bf16* dQ = reinterpret_cast<bf16*>(a.dq) + (int64_t)b * a.Tq * a.dq_ld + h * D;
 
   const bool qok = qv < a.Tq;
-  bf16x8 fq[4], fdo[4];
+  bf16x8 fq[4], fdo[4], fo[4];
   own_frags(fq, Q, qv, hi);
   own_frags(fdo, dO, qv, hi);
+  // delta = rowsum(dO * O) of this lane's query row, computed here (the two lane halves hold
+  // 32 dims each) and published for the dK / dV kernel that runs next on the stream
+  const RowBuf Ob = row_buf(reinterpret_cast<const bf16*>(a.o) + (int64_t)b * a.Tq * a.o_ld + h * D, a.o_ld, a.Tq);
+  own_frags(fo, Ob, qv, hi);
   const float lse = qok ? a.lse[(int64_t)bh * a.Tq + qv] : INFINITY;
-  const float dl = qok ? a.delta[(int64_t)bh * a.Tq + qv] : 0.f;
+  float dsum = 0.f;
+#pragma unroll
+  for (int st = 0; st < 4; ++st)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dsum += (float)fdo[st][j] * (float)fo[st][j];
+  dsum += __shfl_xor(dsum, 32, 64);
+  const float dl = qok ? dsum : 0.f;
+  if (qok && hi == 0) a.delta[(int64_t)bh * a.Tq + qv] = dsum;
   const float c = a.scale * LOG2E;
   f32x16 dq[2];
   zero16(dq[0]);
@@ -985,8 +996,9 @@ extern "C" int tt2_attn_bwd(const tt2_attn_args* p, hipStream_t s) {
   const int BH = p->batch * p->heads;
   dim3 gprep((p->batch * p->tq + 3) / 4);
   if (p->dtype == TT2_DT_BF16) {
-    hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16>, gprep, dim3(NT), 0, s, a);
     const int nq = v3_waves(p, p->tq, false), nk = v3_waves(p, p->tk, false);
+    // the v3 dQ kernel computes delta = rowsum(dO * O) itself (and stores it for dK / dV)
+    if (nq == 0) hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16>, gprep, dim3(NT), 0, s, a);
     if (nq == 4) hipLaunchKernelGGL(attn_bwd_dq3_kernel<4>, dim3(BH, (p->tq + 127) / 128), dim3(256), 0, s, a);
     else if (nq == 2) hipLaunchKernelGGL(attn_bwd_dq3_kernel<2>, dim3(BH, (p->tq + 63) / 64), dim3(128), 0, s, a);
     else hipLaunchKernelGGL(attn_bwd_dq_kernel<bf16>, dim3((p->tq + BQ - 1) / BQ, BH), dim3(NT), 0, s, a);
