@@ -182,7 +182,7 @@ int tt2_decode_emit(const float* heads, int64_t heads_ld, int batch, int n_mels,
 #define TT2_COLSUM_ROWS 128
 #define TT2_BN_ROWS_PER_CHUNK 64
 #define TT2_PE_BWD_BLOCKS 1024
-#define TT2_LOSS_BLOCKS 256
+#define TT2_LOSS_BLOCKS 1024
 #define TT2_ADAM_NORM_BLOCKS 1024
 
 /* dst[c] = beta*dst[c] + sum_r src[r*ld + c] (fixed summation order) */
