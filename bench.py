@@ -78,9 +78,43 @@ def cpu_baseline(budget_s: float = 20.0):
         if time.perf_counter() - t0 > budget_s / 2 or n >= 8:
             break
     dt = (time.perf_counter() - t0) / n
+    # cfg1: one LJSpeech-size utterance (100 phonemes -> 400 frames), eval forward
+    model.eval()
+    g = torch.Generator().manual_seed(0)
+    t1 = torch.randint(1, 80, (1, 100), generator=g)
+    m1 = torch.randn(1, 400, NMEL, generator=g)
+    l1, lm1 = torch.tensor([100]), torch.tensor([400])
+    with torch.no_grad():
+        model(t1, l1, m1, lm1)
+        c0 = time.perf_counter()
+        for _ in range(5):
+            model(t1, l1, m1, lm1)
+        dc = (time.perf_counter() - c0) / 5
     return {"value": round(2 * TY / dt, 2), "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"CPU oracle fp32 train step (fwd+loss+bwd+Adam), B=2 x (128 phonemes, 800x80 mel), "
-                      f"{n} timed steps after 1 warm-up, {threads} torch threads of {cores} visible cores"}
+                      f"{n} timed steps after 1 warm-up, {threads} torch threads of {cores} visible cores",
+            "cfg1_forward": {"value": round(400 / dc, 1), "unit": "frames/s",
+                             "sample": "CPU oracle fp32 eval forward, B=1, 100 phonemes -> 400 frames, 5 runs"}}
+
+
+def gpu_cfg1(model):
+    """cfg1 on the GPU engine (bf16 eval forward, eager launches) for comparison."""
+    g = torch.Generator().manual_seed(0)
+    t1 = torch.randint(1, 80, (1, 100), generator=g).cuda()
+    m1 = torch.randn(1, 400, NMEL, generator=g).cuda()
+    l1, lm1 = torch.tensor([100]).cuda(), torch.tensor([400]).cuda()
+    was = model.engine.training
+    model.eval()
+    model(t1, l1, m1, lm1)
+    torch.cuda.synchronize()
+    c0 = time.perf_counter()
+    for _ in range(20):
+        model(t1, l1, m1, lm1)
+    torch.cuda.synchronize()
+    dc = (time.perf_counter() - c0) / 20
+    model.train(was)
+    return {"value": round(400 / dc, 1), "unit": "frames/s", "ms": round(dc * 1e3, 3),
+            "sample": "bf16 eval forward on the GPU, B=1, 100 phonemes -> 400 frames, eager launches"}
 
 
 DEC_B, DEC_T = 32, 800
@@ -317,6 +351,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[bench] cpu baseline (oracle on host cores)")
         cpu = cpu_baseline()
+        cpu["cfg1_forward"]["gpu"] = gpu_cfg1(model)
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
