@@ -152,6 +152,9 @@ typedef struct tt2_attn_args {
                         2 v3 with 2-wave workgroups, 3 v3 with 4-wave workgroups (bf16 only) */
 } tt2_attn_args;
 
+/* Alignment diagnostics: probs[b*H + h][q][j] (f32) of a forward already run with these
+ * args, recomputed from q, k and the saved lse (exactly 0 where masked). */
+int tt2_attn_probs(const tt2_attn_args* a, float* probs, hipStream_t stream);
 int tt2_attn_fwd(const tt2_attn_args* a, hipStream_t stream);
 int tt2_attn_bwd(const tt2_attn_args* a, hipStream_t stream);
 

@@ -153,3 +153,23 @@ def test_backward_bf16_grads_close_to_oracle():
         # BN-normalised convs (post-net, encoder pre-net) amplify bf16 rounding to ~25 %
         if k.startswith(("mel_", "stop_", "decoder.layers.5")):
             assert rel(gm[k], og[k].grad) < 0.12, (k, rel(gm[k], og[k].grad))
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 5e-2)])
+def test_alignments_match_oracle(dtype, tol):
+    """model.alignments(l): the encoder-decoder attention probabilities recomputed from the
+    saved LSE equal the oracle's nn.MultiheadAttention-style weights (masked keys exactly 0)."""
+    oracle, model = build(dtype, seed=5)
+    text, tl, mel, ml = make_batch()
+    oracle.eval()
+    model.eval()
+    _, _, _, attn = oracle(text, tl, mel, ml, return_attn=True)
+    model(text, tl.int(), mel, ml.int())
+    for l in (0, 5):
+        ref = attn["dec_cross"][l]
+        got = model.alignments(l).cpu()
+        assert got.shape == ref.shape
+        assert rel(got, ref) < tol
+        assert got[1, :, :, int(tl[1]):].abs().max().item() == 0.0
+    f = TransformerTTS.diagonal_focus(model.alignments(-1), tl, ml)
+    assert f.shape == (2,) and ((f > 0) & (f <= 1.0001)).all()

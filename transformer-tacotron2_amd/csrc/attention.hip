@@ -969,6 +969,46 @@ int v3_waves(const tt2_attn_args* p, int rows, bool fwd) {
   return !fwd || wg4 >= 512 ? 4 : 2;
 }
 
+// ------------------------------------------------------------ diagnostics
+// Attention probabilities of a forward already run (alignment diagnostics, SURVEY 8(f)
+// row 3): P[bh][q][j] = exp2(s * scale * log2e - lse[bh][q]) from the saved log2-LSE,
+// 0 where masked.  One workgroup per (batch*head, query row); off the training path.
+template <typename T>
+__global__ __launch_bounds__(NT) void attn_probs_kernel(AttnArgs a, float* probs) {
+  __shared__ float sq[D];
+  const int bh = blockIdx.y, qi = blockIdx.x;
+  const int b = bh / a.H, h = bh % a.H;
+  const T* Q = reinterpret_cast<const T*>(a.q) + ((int64_t)b * a.Tq + qi) * a.q_ld + h * D;
+  if (threadIdx.x < D) sq[threadIdx.x] = to_f32(Q[threadIdx.x]);
+  __syncthreads();
+  const float lse = a.lse[(int64_t)bh * a.Tq + qi];
+  const int klim = key_limit(a, b);
+  const float c = a.scale * LOG2E;
+  float* out = probs + ((int64_t)bh * a.Tq + qi) * a.Tk;
+  for (int j = threadIdx.x; j < a.Tk; j += NT) {
+    float v = 0.f;
+    if (j < klim && (!a.causal || j <= qi)) {
+      const T* Kr = reinterpret_cast<const T*>(a.k) + ((int64_t)b * a.Tk + j) * a.k_ld + h * D;
+      float dot = 0.f;
+#pragma unroll 8
+      for (int d = 0; d < D; ++d) dot += sq[d] * to_f32(Kr[d]);
+      v = exp2f(dot * c - lse);
+    }
+    out[j] = v;
+  }
+}
+
+extern "C" int tt2_attn_probs(const tt2_attn_args* p, float* probs, hipStream_t s) {
+  if (int rc = validate(p)) return rc;
+  if (!p->lse || !probs) return tt2_set_error(TT2_E_INVALID, "tt2_attn_probs: lse / probs required");
+  if (p->batch * p->tq * p->tk == 0) return TT2_OK;
+  AttnArgs a = to_args(p);
+  const dim3 g(p->tq, p->batch * p->heads);
+  if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(attn_probs_kernel<bf16>, g, dim3(NT), 0, s, a, probs);
+  else hipLaunchKernelGGL(attn_probs_kernel<float>, g, dim3(NT), 0, s, a, probs);
+  return tt2_check_launch(hipGetLastError(), "tt2_attn_probs");
+}
+
 extern "C" int tt2_attn_fwd(const tt2_attn_args* p, hipStream_t s) {
   if (int rc = validate(p)) return rc;
   if (!p->o_out || !p->lse) return tt2_set_error(TT2_E_INVALID, "tt2_attn_fwd: out/lse required");

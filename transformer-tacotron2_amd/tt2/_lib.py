@@ -137,6 +137,7 @@ class AttnArgs(C.Structure):
 
 
 SIGNATURES.update({
+    "tt2_attn_probs": ([C.POINTER(AttnArgs), vp, vp], C.c_int),
     "tt2_attn_fwd": ([C.POINTER(AttnArgs), vp], C.c_int),
     "tt2_attn_bwd": ([C.POINTER(AttnArgs), vp], C.c_int),
 })

@@ -12,6 +12,8 @@ PyTorch-op fallback (a missing library or GPU raises).
 """
 from __future__ import annotations
 
+import math
+
 import torch
 
 from .config import TTSConfig
@@ -162,6 +164,33 @@ class TransformerTTS:
             self._decoders[key] = dec
         dev = self.engine.dev
         return dec.run(text.to(dev), text_len.to(dev), max_len, stop_threshold, use_graph)
+
+    # ------------------------------------------------------------ diagnostics
+    def alignments(self, layer: int = -1) -> torch.Tensor:
+        """Encoder-decoder attention of decoder layer `layer` from the last forward:
+        [B, H, Ty, Tx] f32 (rows sum to 1 over the valid phonemes).
+        Recomputed on the GPU from the saved query, memory keys and log-sum-exp."""
+        if self._last is None:
+            raise RuntimeError("alignments() needs a forward first")
+        e, A, c = self.engine, self._last, self.cfg
+        l = layer % c.n_dec
+        d, H = c.d_model, c.n_heads
+        kvld = c.n_dec * 2 * d
+        probs = torch.empty(A.B, H, A.Ty, A.Tx, dtype=torch.float32, device=e.dev)
+        from . import ops
+        ops.attn_probs(A[f"dcq{l}"], A["mkv"][:, 2 * d * l:], A[f"dclse{l}"], probs, d, kvld, A.B, H, A.Ty, A.Tx,
+                       key_len=A["text_len"], scale=1.0 / math.sqrt(c.head_dim))
+        return probs
+
+    @staticmethod
+    def diagonal_focus(align: torch.Tensor, text_len: torch.Tensor, mel_len: torch.Tensor) -> torch.Tensor:
+        """Per-utterance focus rate: mean over valid frames of the max attention weight
+        (averaged over heads) -- near 1 for a sharp monotonic alignment."""
+        a = align.mean(1)
+        B, Ty, _ = a.shape
+        valid = torch.arange(Ty, device=a.device)[None, :] < mel_len.to(a.device)[:, None]
+        mx = a.amax(-1)
+        return (mx * valid).sum(1) / valid.sum(1).clamp_min(1)
 
     # ------------------------------------------------------------ training
     def configure_optimizer(self, **kw):

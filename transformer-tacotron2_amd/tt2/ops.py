@@ -251,6 +251,14 @@ def attn_fwd(q, k, v, out, lse, q_ld, k_ld, v_ld, o_ld, batch, heads, tq, tk, ke
     return out
 
 
+def attn_probs(q, k, lse, probs, q_ld, k_ld, batch, heads, tq, tk, key_len=None, causal=False, scale=0.125):
+    """Attention probabilities [B*H, Tq, Tk] f32 of a forward already run (alignment diagnostics)."""
+    a = _attn_common(q, k, k, q_ld, k_ld, k_ld, batch, heads, tq, tk, key_len, causal, scale)
+    a.lse = lse.data_ptr()
+    check(lib().tt2_attn_probs(C.byref(a), probs.data_ptr(), stream_ptr()), "tt2_attn_probs")
+    return probs
+
+
 def attn_bwd(q, k, v, o, dout, lse, delta, dq, dk, dv, q_ld, k_ld, v_ld, o_ld, do_ld, dq_ld, dk_ld, dv_ld,
              batch, heads, tq, tk, key_len=None, causal=False, scale=0.125):
     L = lib()
