@@ -334,13 +334,15 @@ TT2_DEV void ld8_any(const void* p, int64_t off, int dt, float (&o)[8]) {
 // Chunk epilogue: 8 consecutive outputs of row m starting at column n0.  Full,
 // aligned chunks (E.vec) take 16-B loads/stores with every option tested once
 // per chunk; edge chunks fall back to the per-element path.
-TT2_DEV void epi_store8(const EpiParams& E, uint32_t seed, int m, int n0, int N, const float (&v)[8]) {
+// pre_b: alpha and bias were already applied to v (v7's prefetched bias; E.vec, full chunk)
+TT2_DEV void epi_store8(const EpiParams& E, uint32_t seed, int m, int n0, int N, const float (&v)[8],
+                        bool pre_b = false) {
   const int64_t off = (int64_t)m * E.ldc + n0;
   if (E.vec && n0 + 8 <= N) {
     float o[8], t[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = v[j] * E.alpha;
-    if (E.bias) {
+    for (int j = 0; j < 8; ++j) o[j] = pre_b ? v[j] : v[j] * E.alpha;
+    if (E.bias && !pre_b) {
       const f32x4 a = *reinterpret_cast<const f32x4*>(E.bias + n0), b = *reinterpret_cast<const f32x4*>(E.bias + n0 + 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) { o[j] += a[j]; o[4 + j] += b[j]; }
@@ -1306,6 +1308,21 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
   // ------------------------------------------------------------------ MFMA waves
   const int wm = wave >> 1, wn = wave & 1;
   const bool do_ks = !AK && E.ksum && (tile % ntn) == 0 && wn == 0;
+  // forward layout: this lane's two 8-column bias chunks, loaded before the K loop (the
+  // MFMA waves issue no other global loads, so they land meanwhile) instead of one
+  // dependent round trip in the epilogue
+  const int ql = lane >> 4;
+  const bool pre_b = AK && BKC && !ws && E.bias && E.vec;
+  f32x4 pbias[2][2];
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) {
+    const int n = n0 + wn * 64 + 16 * (2 * pr + (ql & 1)) + 8 * (ql >> 1);
+    pbias[pr][0] = pbias[pr][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (pre_b && n + 8 <= N) {
+      pbias[pr][0] = *reinterpret_cast<const f32x4*>(E.bias + n);
+      pbias[pr][1] = *reinterpret_cast<const f32x4*>(E.bias + n + 4);
+    }
+  }
   float ks[4] = {0.f, 0.f, 0.f, 0.f};
   f32x4 acc[4][4];
 #pragma unroll
@@ -1359,7 +1376,7 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
   // lane (q = lane >> 4) holds C[m][n0 + wn*64 + 16 j + 4 q + r] in acc[i][j][r]; swapping
   // column blocks (2p, 2p+1) between row pairs q, q^1 leaves 8 consecutive columns per lane
   const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
-  const int q = lane >> 4;
+  const int q = ql;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm * 64 + 16 * i + (lane & 15);
@@ -1384,6 +1401,14 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
           for (int j = 0; j < 8; ++j)
             if (n + j < N) w[j] = v[j];
         }
+      } else if (pre_b && n + 8 <= N) {
+        const f32x4 b0 = pbias[pr][0], b1 = pbias[pr][1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = v[j] * E.alpha + b0[j];
+          v[4 + j] = v[4 + j] * E.alpha + b1[j];
+        }
+        epi_store8(E, seed, m, n, N, v, true);
       } else {
         epi_store8(E, seed, m, n, N, v);
       }
