@@ -17,11 +17,14 @@ torch.manual_seed(0)
 model = TransformerTTS(TTSConfig(), dtype=torch.bfloat16)
 model.eval()
 g = torch.Generator().manual_seed(1)
-text = torch.randint(1, 80, (bench.DEC_B, bench.TX), generator=g).cuda()
-tl = torch.full((bench.DEC_B,), bench.TX, dtype=torch.int32, device="cuda")
-CFGS = [(1, 4, 8), (2, 4, 8), (3, 4, 8), (3, 2, 4), (3, 4, 16)]
+DB = int(os.environ.get("DEC_B", bench.DEC_B))        # DEC_B=64 DEC_DT=f16: the cfg5 shape
+DDT = torch.float16 if os.environ.get("DEC_DT") == "f16" else None
+text = torch.randint(1, 80, (DB, bench.TX), generator=g).cuda()
+tl = torch.full((DB,), bench.TX, dtype=torch.int32, device="cuda")
+CFGS = [(3, 4, 8), (3, 8, 8), (3, 8, 16), (3, 4, 16), (3, 2, 4)] if DB > 32 else \
+    [(1, 4, 8), (2, 4, 8), (3, 4, 8), (3, 2, 4), (3, 4, 16)]
 for fuse, so, sf in CFGS + CFGS:
-    dec = Decoder(model.engine, bench.DEC_B, bench.TX, bench.DEC_T)
+    dec = Decoder(model.engine, DB, bench.TX, bench.DEC_T, dtype=DDT)
     dec.fuse, dec.split_o, dec.split_f = fuse, so, sf
     dec.encode(text, tl)
     dec.capture()
