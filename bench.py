@@ -49,6 +49,40 @@ def synth_batch(rank: int, B: int = B_PER_GPU, dev="cuda"):
     return text.to(dev), tl.to(dev), mel.to(dev), ml.to(dev)
 
 
+def ragged_batch(rank: int, B: int = B_PER_GPU, dev="cuda"):
+    """cfg2's ragged variant: per-utterance lengths ~ U[0.5, 1] x max, seeded,
+    padded to the same [B, 128] / [B, 800] shape (pad ids 0, zero mel frames)."""
+    g = torch.Generator().manual_seed(1000 + rank)
+    text, _, mel, _ = synth_batch(rank, B, dev="cpu")
+    tl = (TX * (0.5 + 0.5 * torch.rand(B, generator=g))).round().clamp(1, TX).to(torch.int32)
+    ml = (TY * (0.5 + 0.5 * torch.rand(B, generator=g))).round().clamp(1, TY).to(torch.int32)
+    for b in range(B):
+        text[b, tl[b]:] = 0
+        mel[b, ml[b]:] = 0
+    return text.to(dev), tl.to(dev), mel.to(dev), ml.to(dev)
+
+
+def ragged_bench(step_fn, rank: int, steps: int):
+    """Times the same captured step on the ragged cfg2 batch; value counts valid frames only
+    (padding is computed and masked, as the boundary specifies)."""
+    text, tl, mel, ml = ragged_batch(rank)
+    for _ in range(2):
+        step_fn(text, tl, mel, ml)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step_fn(text, tl, mel, ml)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    valid = int(ml.sum().item())
+    return {"value": round(valid * steps / dt, 1), "unit": "frames/s (valid frames)",
+            "padded_frames_per_s": round(B_PER_GPU * TY * steps / dt, 1),
+            "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps, "loss": round(loss[0].item(), 5),
+            "config": {"workload": "cfg2 ragged variant: lengths ~ U[0.5,1] x max (seed 1000+rank), "
+                                   "padded to 128 / 800", "valid_frames": valid,
+                       "valid_text": int(tl.sum().item())}}
+
+
 def cpu_baseline(budget_s: float = 20.0):
     """The CPU oracle (pure PyTorch fp32) training step on a bounded sample
     (B=2 utterances of the same 128/800 shape), timed on the host cores."""
@@ -262,6 +296,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the cfg3 / cfg5 decode measurements")
     ap.add_argument("--no-longform", action="store_true", help="skip the cfg5 long-form decode measurement")
+    ap.add_argument("--no-ragged", action="store_true", help="skip the cfg2 ragged-length variant")
     ap.add_argument("--force-dp", action="store_true", help="dev: run the DP path (bucketed RCCL all-reduce, "
                     "segmented graph) even at world size 1")
     args = ap.parse_args()
@@ -306,15 +341,15 @@ def main():
         model.train_step(text, tl, mel, ml, sync_grads=sync_fn)
     torch.cuda.synchronize()
     if args.no_graph:
-        def step():
-            return model.train_step(text, tl, mel, ml, sync_grads=sync_fn)
+        def run(*batch):
+            return model.train_step(*batch, sync_grads=sync_fn)
     else:
         run = model.capture_train_step(B_PER_GPU, TX, TY, sync_grads=sync_fn)
         for _ in range(2):
             run(text, tl, mel, ml)
 
-        def step():
-            return run(text, tl, mel, ml)
+    def step():
+        return run(text, tl, mel, ml)
     torch.cuda.synchronize()
     log(f"[bench] timing {args.steps} steps")
     if world > 1:
@@ -336,6 +371,11 @@ def main():
     value = frames / dt
     log(f"[bench] {dt / args.steps * 1e3:.2f} ms/step, loss {lval:.4f}")
 
+    rag = None
+    if rank == 0 and world == 1 and not args.no_ragged:
+        log("[bench] cfg2 ragged variant")
+        rag = ragged_bench(run, rank, max(5, args.steps // 2))
+        log(f"[bench] ragged {rag['value']:.0f} valid frames/s ({rag['ms_per_step']} ms/step)")
     rl = roofline(model, text, tl, mel, ml) if rank == 0 else None
     dec = None
     if rank == 0 and world == 1 and not args.no_decode:
@@ -363,6 +403,7 @@ def main():
                        "graph": not args.no_graph},
             "loss": round(lval, 5),
             "roofline": rl,
+            "train_ragged": rag,
             "cpu_baseline": cpu,
             "decode": dec,
             "decode_longform": lf,

@@ -220,10 +220,20 @@ typedef struct tt2_ln_args {
   float drop_scale;
   float* dbias;   /* bwd, optional: grad_beta*dbias + column sums of the branch gradient
                      (= the bias gradient of the linear layer that produced `branch`) */
+  int32_t defer_finalize;   /* bwd: leave the per-workgroup column partials in `workspace`
+                               and do not write dgamma/dbeta/dbias yet: a later
+                               tt2_layernorm_bwd (finalize_prev) or
+                               tt2_layernorm_bwd_finalize completes them */
+  const struct tt2_ln_args* finalize_prev;   /* bwd, optional: a deferred earlier call
+                               (same c) whose dgamma/dbeta/dbias this launch completes in its
+                               spare lanes; its workspace must not have been reused since */
 } tt2_ln_args;
 int tt2_layernorm_fwd(const tt2_ln_args* a, hipStream_t stream);
 size_t tt2_layernorm_bwd_workspace_size(const tt2_ln_args* a);
 int tt2_layernorm_bwd(const tt2_ln_args* a, hipStream_t stream);
+/* Completes a deferred tt2_layernorm_bwd (defer_finalize = 1): dgamma/dbeta/dbias from the
+ * partials it left in a->workspace.  Same fixed summation order as a chained finalize. */
+int tt2_layernorm_bwd_finalize(const tt2_ln_args* a, hipStream_t stream);
 /* Decode-step residual combine + LayerNorm (x / y of dtype bf16 or f16, c = 512):
  *   y[m, :] = LN(x[m, :] + bias + sum_{s < splits} part[s][m][:]) * gamma + beta
  * part: the raw f32 partial slabs [splits][m][c] of a skinny split-K projection (tt2_gemm

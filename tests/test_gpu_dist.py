@@ -29,8 +29,11 @@ def nccl_group():
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1)
-    yield
-    dist.destroy_process_group()
+    try:
+        yield
+    finally:
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
 
 
 def _model():

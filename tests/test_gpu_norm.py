@@ -60,6 +60,54 @@ def test_layernorm_fwd_bwd_dbias(dtype, m, p):
     assert rel(dbias, brr.grad.sum(0)) < tol_b
 
 
+@pytest.mark.parametrize("m1,m2", [(12800, 12800), (2048, 12800), (12800, 37), (5, 2048)])
+def test_layernorm_bwd_chained_finalize(m1, m2):
+    """A deferred LayerNorm backward (defer=True) completed inside the next one's launch
+    (prev=) or by layernorm_bwd_finalize equals the immediate finalize (f32 sums in another
+    fixed order: 1e-5), and a grad_beta accumulation is carried through the chain."""
+    C = 512
+    g = torch.Generator().manual_seed(m1 + m2)
+    calls = []
+    for m in (m1, m2):
+        x, br, dy = (torch.randn(m, C, generator=g).bfloat16().cuda() for _ in range(3))
+        gamma = (1 + 0.1 * torch.randn(C, generator=g)).cuda()
+        beta = torch.zeros(C, device="cuda")
+        y = torch.empty_like(x)
+        mean, rstd = torch.empty(m, device="cuda"), torch.empty(m, device="cuda")
+        ops.layernorm_fwd(x, br, gamma, beta, y, mean, rstd, m)
+        calls.append((dy, x, br, gamma, mean, rstd, m))
+
+    def run(mode):
+        outs = []
+        parts = [torch.empty(ops.layernorm_bwd_workspace_size(1 << 30, C), dtype=torch.uint8, device="cuda")
+                 for _ in range(2)]
+        prev = None
+        for i, (dy, x, br, gamma, mean, rstd, m) in enumerate(calls):
+            dx, dbr = torch.empty_like(x), torch.empty_like(x)
+            dg, db, dbias = (torch.full((C,), 0.5, device="cuda") for _ in range(3))
+            kw = {}
+            if mode != "plain" and i == 0:
+                kw = dict(part=parts[0], defer=True)
+            a = ops.layernorm_bwd(dy, x, br, gamma, mean, rstd, dx, dbr, dg, db, m, dbias=dbias,
+                                  prev=prev if mode == "chain" else None, **kw)
+            if mode == "standalone" and i == 0:
+                ops.layernorm_bwd_finalize(a)
+            prev = a
+            outs.append((dx, dbr, dg, db, dbias))
+        torch.cuda.synchronize()
+        return outs
+
+    ref, chain, alone = run("plain"), run("chain"), run("standalone")
+    for got in (chain, alone):
+        for (rx, rb, rg, rbe, rbi), (gx, gb, gg, gbe, gbi) in zip(ref, got):
+            assert torch.equal(rx, gx) and torch.equal(rb, gb)
+            for r, v in ((rg, gg), (rbe, gbe), (rbi, gbi)):
+                assert rel(v, r) < 1e-5
+    # chained and standalone completions share one summation order: bitwise equal
+    for a_, b_ in zip(chain[0][2:], alone[0][2:]):
+        assert torch.equal(a_, b_)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("m,c,act,res", [(1000, 512, 1, False), (333, 80, 0, True), (64, 512, 2, False)])
 def test_batchnorm_train_fwd_bwd(dtype, m, c, act, res):

@@ -59,6 +59,14 @@ template <> TT2_DEV void st8(float* p, const float (&v)[8]) {
 }
 
 // --------------------------------------------------------------- LayerNorm
+// A deferred LayerNorm-backward finalize: column sums of part[nb][3][C] into (dg, db, dd).
+struct LnFin {
+  const float* part;
+  float* dg; float* db; float* dd;
+  float gb;
+  int nb;   // 0 = nothing to finalize
+};
+
 struct LnArgs {
   const void* x; const void* branch; const void* dy;
   void* y; void* dx; void* dbranch;
@@ -70,6 +78,7 @@ struct LnArgs {
   int M, C;
   float eps;
   DropDesc drop;
+  LnFin fin;   // bwd: an earlier deferred call's finalize, done in this launch's spare waves
 };
 
 template <typename T> TT2_DEV void unpack8(const uint4 (&u)[sizeof(T) / 2], float (&v)[8]) {
@@ -195,6 +204,31 @@ TT2_DEV void ln_row_load(LnRow<T>& r, const LnArgs& a, int row, int c0) {
 }
 
 
+// One wave sums output o (= which * C + c) of a deferred finalize over the nb partial rows
+// (4 loads in flight per lane, then a DPP wave sum): a fixed order, shared by the chained
+// and the standalone finalize.
+TT2_DEV void ln_fin_col(const LnFin& f, int C, int o, int lane) {
+  const int which = o / C, c = o - which * C;
+  float* dst = which == 0 ? f.dg : (which == 1 ? f.db : f.dd);
+  if (!dst) return;
+  const float* src = f.part + (int64_t)which * C + c;
+  const int64_t rs = 3 * (int64_t)C;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int r = lane;
+  for (; r + 192 < f.nb; r += 256) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] += src[(r + 64 * u) * rs];
+  }
+  for (; r < f.nb; r += 64) acc[0] += src[r * rs];
+  const float v = wave_sum((acc[0] + acc[1]) + (acc[2] + acc[3]));
+  if (lane == 0) dst[c] = f.gb != 0.f ? f.gb * dst[c] + v : v;
+}
+
+__global__ __launch_bounds__(LNB_NT) void ln_fin_kernel(LnFin f, int C) {
+  const int o = blockIdx.x * (LNB_NT / 64) + (threadIdx.x >> 6);
+  if (o < 3 * C) ln_fin_col(f, C, o, threadIdx.x & 63);
+}
+
 template <typename T>
 __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
   __shared__ float red[3][4][512];
@@ -268,6 +302,13 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
     const int which = i / a.C, c = i % a.C;
     a.part[((int64_t)blockIdx.x * 3 + which) * a.C + c] =
         red[which][0][c] + red[which][1][c] + red[which][2][c] + red[which][3][c];
+  }
+  if (a.fin.nb) {   // the previous LayerNorm's column sums, spread over every workgroup's waves
+    const int per = (3 * a.C + gridDim.x - 1) / gridDim.x;
+    for (int i = w; i < per; i += LNB_NT / 64) {
+      const int o = blockIdx.x * per + i;
+      if (o < 3 * a.C) ln_fin_col(a.fin, a.C, o, lane);
+    }
   }
 }
 
@@ -641,6 +682,11 @@ static int ln_bwd_blocks(int m) {
   return min(cap, (m + 15) / 16);
 }
 
+static LnFin ln_fin_of(const tt2_ln_args* q) {
+  return LnFin{reinterpret_cast<const float*>(q->workspace), q->dgamma, q->dbeta, q->dbias, q->grad_beta,
+               ln_bwd_blocks(q->m)};
+}
+
 extern "C" size_t tt2_layernorm_bwd_workspace_size(const tt2_ln_args* p) {
   return (size_t)ln_bwd_blocks(p->m) * 3 * p->c * sizeof(float);
 }
@@ -657,12 +703,32 @@ extern "C" int tt2_layernorm_bwd(const tt2_ln_args* p, hipStream_t s) {
   a.dgamma = p->dgamma; a.dbeta = p->dbeta; a.dbias = p->dbias; a.grad_beta = p->grad_beta;
   a.M = p->m; a.C = p->c; a.eps = p->eps;
   a.drop = DropDesc{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
-  if (p->m == 0) return TT2_OK;
+  if (const tt2_ln_args* q = p->finalize_prev) {
+    if (!q->defer_finalize || q->c != p->c || !q->workspace)
+      return tt2_set_error(TT2_E_INVALID, "tt2_layernorm_bwd: finalize_prev must be a deferred call with the same c");
+    if (q->workspace == p->workspace && q->m > 0)
+      return tt2_set_error(TT2_E_INVALID, "tt2_layernorm_bwd: finalize_prev's workspace is overwritten by this call");
+    if (q->m > 0) a.fin = ln_fin_of(q);
+  }
+  if (p->m == 0) {   // nothing of our own; still complete the chained finalize
+    if (a.fin.nb) hipLaunchKernelGGL(ln_fin_kernel, dim3((3 * p->c + 7) / 8), dim3(LNB_NT), 0, s, a.fin, p->c);
+    return tt2_check_launch(hipGetLastError(), "tt2_layernorm_bwd");
+  }
   const int nb = ln_bwd_blocks(p->m);
   if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(ln_bwd_kernel<bf16>, dim3(nb), dim3(LNB_NT), 0, s, a);
   else hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nb), dim3(LNB_NT), 0, s, a);
-  hipLaunchKernelGGL(ln_bwd_finalize, dim3(p->c / 16, 3), dim3(256), 0, s, a, nb);
+  if (!p->defer_finalize) {
+    a.fin = LnFin{};
+    hipLaunchKernelGGL(ln_bwd_finalize, dim3(p->c / 16, 3), dim3(256), 0, s, a, nb);
+  }
   return tt2_check_launch(hipGetLastError(), "tt2_layernorm_bwd");
+}
+
+extern "C" int tt2_layernorm_bwd_finalize(const tt2_ln_args* p, hipStream_t s) {
+  if (!p->defer_finalize || !p->workspace) return tt2_set_error(TT2_E_INVALID, "tt2_layernorm_bwd_finalize: not a deferred call");
+  if (p->m == 0) return TT2_OK;
+  hipLaunchKernelGGL(ln_fin_kernel, dim3((3 * p->c + 7) / 8), dim3(LNB_NT), 0, s, ln_fin_of(p), p->c);
+  return tt2_check_launch(hipGetLastError(), "tt2_layernorm_bwd_finalize");
 }
 
 // rows per statistics chunk: at most TT2_BN_ROWS_PER_CHUNK, fewer for short inputs

@@ -154,6 +154,7 @@ class LnArgs(C.Structure):
         ("workspace", vp), ("ws_bytes", sz), ("drop_seed", vp),
         ("m", i32), ("c", i32), ("dtype", i32), ("eps", f32), ("grad_beta", f32),
         ("drop_site", u32), ("drop_thr", u32), ("drop_scale", f32), ("dbias", vp),
+        ("defer_finalize", i32), ("finalize_prev", vp),
     ]
 
 
@@ -203,6 +204,7 @@ SIGNATURES.update({
     "tt2_layernorm_fwd": ([P_(LnArgs), vp], C.c_int),
     "tt2_layernorm_bwd_workspace_size": ([P_(LnArgs)], sz),
     "tt2_layernorm_bwd": ([P_(LnArgs), vp], C.c_int),
+    "tt2_layernorm_bwd_finalize": ([P_(LnArgs), vp], C.c_int),
     "tt2_reflect_pad": ([vp, i64, vp, C.c_int32, C.c_int32, vp, i64, C.c_int32, vp], C.c_int),
     "tt2_spec_magnitude": ([vp, i64, C.c_int32, C.c_int32, vp, i64, vp], C.c_int),
     "tt2_spec_rephase": ([vp, i64, vp, i64, C.c_int32, C.c_int32, vp, i64, vp], C.c_int),

@@ -15,6 +15,7 @@ exact-f32 MFMA).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -192,6 +193,10 @@ class TTSEngine:
         assert c.d_model == 512 and c.head_dim == 64, "kernels are built for d_model 512, head_dim 64"
         self._heads_pad = None   # bf16 backward: heads GEMMs padded to 88 rows (see backward)
         self.pad_heads = True
+        # backward: a LayerNorm's column-sum finalize rides in the next LayerNorm's launch
+        # (two dedicated partials buffers alternate; see _ln_defer)
+        self.ln_chain = os.environ.get("TT2_LN_CHAIN", "1") != "0"
+        self._ln_parts = None
         self._wq = None   # weight-gradient requests queued for one grouped launch (see _defer_wgrads)
         self.cd = dtype
         self.dev = torch.device(device)
@@ -299,6 +304,18 @@ class TTSEngine:
                  a_ksum=gb if fused else None)
         if gb is not None and not fused:
             self._bias(dy, ldy or n_out, m, n_out, gb)
+
+    def _ln_defer(self, slot: int, m: int, prev=None) -> dict:
+        """Keyword arguments that defer a LayerNorm backward's finalize into partials buffer
+        `slot` (0/1, alternating along a chain) and complete `prev`'s in the same launch.
+        Chains stop at each layer's last LayerNorm (not deferred), so every layer's
+        gradients are final when its DP bucket may be launched."""
+        if not self.ln_chain:
+            return {}
+        if self._ln_parts is None:
+            nbytes = ops.layernorm_bwd_workspace_size(1 << 30, self.cfg.d_model)
+            self._ln_parts = [torch.empty(nbytes, dtype=torch.uint8, device=self.dev) for _ in range(2)]
+        return {"part": self._ln_parts[slot], "defer": True, "prev": prev}
 
     def _defer_wgrads(self):
         self._wq = []
@@ -527,9 +544,10 @@ class TTSEngine:
             h1, h2 = A[f"dh1{l}"], A[f"dh2{l}"]
             self._defer_wgrads()
             # LN3 + FFN
-            ops.layernorm_bwd(gx, h2, A[f"df2{l}"], self.P(p + "ln3.g"), A[f"dln3m{l}"], A[f"dln3r{l}"], A["g_res"],
-                              A["g_br3"], self.G(p + "ln3.g"), self.G(p + "ln3.b"), Md,
-                              drop=self.drop(base + 3, c.dropout), ws=self.ws, dbias=self.G(p + "ffn2.b"))
+            ln3 = ops.layernorm_bwd(gx, h2, A[f"df2{l}"], self.P(p + "ln3.g"), A[f"dln3m{l}"], A[f"dln3r{l}"],
+                                    A["g_res"], A["g_br3"], self.G(p + "ln3.g"), self.G(p + "ln3.b"), Md,
+                                    drop=self.drop(base + 3, c.dropout), ws=self.ws, dbias=self.G(p + "ffn2.b"),
+                                    **self._ln_defer(0, Md))
             self._wgrad(A["g_br3"], A[f"df1{l}"], self.G(p + "ffn2.w"), d, F, Md)
             self._dgrad(A["g_br3"], self.W(p + "ffn2.w"), A["g_f1"], Md, F, d, gate=A[f"df1{l}"],
                         gate_scale=gs(c.dropout))
@@ -537,9 +555,10 @@ class TTSEngine:
             self._dgrad(A["g_f1"], self.W(p + "ffn1.w"), gx2, Md, d, F, res=A["g_res"])
             gx, gx2 = gx2, gx
             # LN2 + cross attention
-            ops.layernorm_bwd(gx, h1, A[f"dco{l}"], self.P(p + "ln2.g"), A[f"dln2m{l}"], A[f"dln2r{l}"], A["g_res"],
-                              A["g_br2"], self.G(p + "ln2.g"), self.G(p + "ln2.b"), Md,
-                              drop=self.drop(base + 1, c.dropout), ws=self.ws, dbias=self.G(p + "co.b"))
+            ln2 = ops.layernorm_bwd(gx, h1, A[f"dco{l}"], self.P(p + "ln2.g"), A[f"dln2m{l}"], A[f"dln2r{l}"],
+                                    A["g_res"], A["g_br2"], self.G(p + "ln2.g"), self.G(p + "ln2.b"), Md,
+                                    drop=self.drop(base + 1, c.dropout), ws=self.ws, dbias=self.G(p + "co.b"),
+                                    **self._ln_defer(1, Md, ln3))
             self._wgrad(A["g_br2"], A[f"dcatt{l}"], self.G(p + "co.w"), d, d, Md)
             self._dgrad(A["g_br2"], self.W(p + "co.w"), A["g_att"], Md, d, d)
             ko = 2 * d * l
@@ -553,7 +572,7 @@ class TTSEngine:
             # LN1 + self attention
             ops.layernorm_bwd(gx, x_in, A[f"do{l}"], self.P(p + "ln1.g"), A[f"dln1m{l}"], A[f"dln1r{l}"],
                               A["g_res"], A["g_br"], self.G(p + "ln1.g"), self.G(p + "ln1.b"), Md,
-                              drop=self.drop(base, c.dropout), ws=self.ws, dbias=self.G(p + "o.b"))
+                              drop=self.drop(base, c.dropout), ws=self.ws, dbias=self.G(p + "o.b"), prev=ln2)
             self._wgrad(A["g_br"], A[f"datt{l}"], self.G(p + "o.w"), d, d, Md)
             self._dgrad(A["g_br"], self.W(p + "o.w"), A["g_att"], Md, d, d)
             qkv, gq = A[f"dqkv{l}"], A["g_qkv"]
@@ -596,9 +615,10 @@ class TTSEngine:
             p, base = f"enc{l}.", SITE_ENC_LAYER + 4 * l
             x_in, h1 = A[f"ex{l}"], A[f"eh1{l}"]
             self._defer_wgrads()
-            ops.layernorm_bwd(gxe, h1, A[f"ef2{l}"], self.P(p + "ln2.g"), A[f"eln2m{l}"], A[f"eln2r{l}"], gres, gbr2,
-                              self.G(p + "ln2.g"), self.G(p + "ln2.b"), Me, drop=self.drop(base + 2, c.dropout),
-                              ws=self.ws, dbias=self.G(p + "ffn2.b"))
+            ln2 = ops.layernorm_bwd(gxe, h1, A[f"ef2{l}"], self.P(p + "ln2.g"), A[f"eln2m{l}"], A[f"eln2r{l}"],
+                                    gres, gbr2, self.G(p + "ln2.g"), self.G(p + "ln2.b"), Me,
+                                    drop=self.drop(base + 2, c.dropout), ws=self.ws, dbias=self.G(p + "ffn2.b"),
+                                    **self._ln_defer(0, Me))
             self._wgrad(gbr2, A[f"ef1{l}"], self.G(p + "ffn2.w"), d, F, Me)
             self._dgrad(gbr2, self.W(p + "ffn2.w"), gf1, Me, F, d, gate=A[f"ef1{l}"], gate_scale=gs(c.dropout))
             self._wgrad(gf1, h1, self.G(p + "ffn1.w"), F, d, Me, gb=self.G(p + "ffn1.b"))
@@ -606,7 +626,7 @@ class TTSEngine:
             gxe, gxe2 = gxe2, gxe
             ops.layernorm_bwd(gxe, x_in, A[f"eo{l}"], self.P(p + "ln1.g"), A[f"eln1m{l}"], A[f"eln1r{l}"], gres, gbr,
                               self.G(p + "ln1.g"), self.G(p + "ln1.b"), Me, drop=self.drop(base, c.dropout),
-                              ws=self.ws, dbias=self.G(p + "o.b"))
+                              ws=self.ws, dbias=self.G(p + "o.b"), prev=ln2)
             self._wgrad(gbr, A[f"eatt{l}"], self.G(p + "o.w"), d, d, Me)
             self._dgrad(gbr, self.W(p + "o.w"), gatt, Me, d, d)
             qkv = A[f"eqkv{l}"]

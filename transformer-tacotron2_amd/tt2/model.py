@@ -231,10 +231,12 @@ class TransformerTTS:
         s.wait_stream(torch.cuda.current_stream())
         g2 = torch.cuda.CUDAGraph() if sync_grads is not None else None
         segs = []   # [(graph, bucket indices launched right after its replay)]
+        # captures are thread-local: RCCL's watchdog thread polls its work events during
+        # capture, which a global-mode capture treats as a prohibited call (capture invalidated)
         torch.cuda.synchronize()
         with torch.cuda.stream(s):
             cur = [torch.cuda.CUDAGraph()]
-            cur[0].capture_begin()
+            cur[0].capture_begin(capture_error_mode="thread_local")
             if sync is not None and hasattr(sync, "take_ready"):
                 # cut the forward+backward graph wherever a gradient bucket becomes final,
                 # so the replay can start that bucket's all-reduce while the rest of the
@@ -249,7 +251,7 @@ class TransformerTTS:
                         cur[0].capture_end()
                         segs.append((cur[0], idx))
                         cur[0] = torch.cuda.CUDAGraph()
-                        cur[0].capture_begin()
+                        cur[0].capture_begin(capture_error_mode="thread_local")
                 e.grad_ready_hook = cut
             e.forward(A)
             e.loss(A)
@@ -262,7 +264,7 @@ class TransformerTTS:
             if sync is not None and hasattr(sync, "take_ready"):
                 sync.reset()
             if g2 is not None:
-                with torch.cuda.graph(g2, stream=s):
+                with torch.cuda.graph(g2, stream=s, capture_error_mode="thread_local"):
                     e.optimizer_step()
         torch.cuda.current_stream().wait_stream(s)
         e.grad_ready_hook = hook

@@ -301,9 +301,14 @@ def ln_combine(x, part, splits, bias, gamma, beta, y, m, eps=1e-5):
 
 
 def layernorm_bwd(dy, x, branch, gamma, mean, rstd, dx, dbranch, dgamma, dbeta, m, drop: Drop = NO_DROP,
-                  ws: Workspace | None = None, dbias=None):
+                  ws: Workspace | None = None, dbias=None, part=None, defer=False, prev=None):
     """dx = d(LN)/ds, dbranch = drop-masked dx, gamma/beta grads, and optionally
-    dbias = column sums of dbranch (the producing linear layer's bias gradient)."""
+    dbias = column sums of dbranch (the producing linear layer's bias gradient).
+
+    defer=True leaves dgamma/dbeta/dbias as column partials in `part` (a dedicated uint8
+    buffer that nothing else may touch until they are finalized); a later call with
+    prev=<the returned args> completes them in its own launch, or layernorm_bwd_finalize
+    does.  Returns the call's LnArgs."""
     L = lib()
     a = _lib.LnArgs()
     a.dy, a.x, a.branch = dy.data_ptr(), x.data_ptr(), ptr(branch)
@@ -313,9 +318,28 @@ def layernorm_bwd(dy, x, branch, gamma, mean, rstd, dx, dbranch, dgamma, dbeta, 
     a.dgamma, a.dbeta = dgamma.data_ptr(), dbeta.data_ptr()
     a.m, a.c, a.dtype = m, x.shape[-1], dt(x)
     _drop_into(a, drop)
-    buf = (ws or _WS).get(L.tt2_layernorm_bwd_workspace_size(C.byref(a)))
+    need = L.tt2_layernorm_bwd_workspace_size(C.byref(a))
+    if defer and part is None:
+        raise ValueError("layernorm_bwd: defer needs a dedicated partials buffer")
+    buf = part if part is not None else (ws or _WS).get(need)
+    if buf.numel() < need:
+        raise ValueError(f"layernorm_bwd: partials buffer {buf.numel()} B < {need} B")
     a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
+    a.defer_finalize = int(defer)
+    a.finalize_prev = C.addressof(prev) if prev is not None and prev.defer_finalize else None
     check(L.tt2_layernorm_bwd(C.byref(a), stream_ptr()), "tt2_layernorm_bwd")
+    return a
+
+
+def layernorm_bwd_workspace_size(m: int, c: int) -> int:
+    a = _lib.LnArgs()
+    a.m, a.c = m, c
+    return lib().tt2_layernorm_bwd_workspace_size(C.byref(a))
+
+
+def layernorm_bwd_finalize(a):
+    """Completes a deferred layernorm_bwd (its returned LnArgs)."""
+    check(lib().tt2_layernorm_bwd_finalize(C.byref(a), stream_ptr()), "tt2_layernorm_bwd_finalize")
 
 
 def _bn(y, gamma, beta, mean, rstd, m, c, act, training, drop, eps, momentum, ws):
