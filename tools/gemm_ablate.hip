@@ -1,8 +1,10 @@
 // Standalone GEMM ablation harness (dev tool): builds gemm.hip with one of the
-// TT2_ABL_* switches and times the bf16 v2 kernel on the step's key shapes.
+// TT2_ABL_* switches and times the bf16 kernel (variant TT2_V, default v2) on the step's
+// key shapes.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I transformer-tacotron2_amd/csrc \
 //     -DTT2_ABL_NO_EPI tools/gemm_ablate.hip -o /tmp/abl_noepi
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "../transformer-tacotron2_amd/csrc/gemm.hip"
@@ -22,7 +24,7 @@ int main() {
     g.a = A; g.b = B; g.c = Cm; g.m = s.m; g.n = s.n; g.k = s.k;
     g.lda = s.ta ? s.m : s.k; g.ldb = s.tb ? s.n : s.k; g.ldc = s.n;
     g.trans_a = s.ta; g.trans_b = s.tb; g.dtype_in = 1; g.dtype_out = 1; g.alpha = 1.f; g.gate_scale = 1.f;
-    g.splits = 1; g.kernel_variant = 2;
+    g.splits = 1; g.kernel_variant = getenv("TT2_V") ? atoi(getenv("TT2_V")) : 2;
     for (int i = 0; i < 3; ++i) tt2_gemm(&g, 0);
     hipDeviceSynchronize();
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
