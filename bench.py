@@ -265,20 +265,27 @@ def longform_bench(model):
     dec.encode(text, tl)
     dec.capture()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    dec.encode(text, tl)
-    dec.reset()
-    # random weights give a meaningless stop head: the seeded caps stand in for the stop
-    # positions (the loop polls them every 32 frames exactly as it polls stop flags)
-    n = dec.decode_loop(LF_T, stop_threshold=None, limits=caps)
-    mel, out_len = dec.postnet(n, None, caps)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+
+    def one_run():
+        t0 = time.perf_counter()
+        dec.encode(text, tl)
+        dec.reset()
+        # random weights give a meaningless stop head: the seeded caps stand in for the stop
+        # positions (the loop polls them every 32 frames exactly as it polls stop flags)
+        n = dec.decode_loop(LF_T, stop_threshold=None, limits=caps)
+        _, out_len = dec.postnet(n, None, caps)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, n, out_len
+
+    one_run()   # untimed: first-touch of the 2000-step KV cache and workspaces
+    runs = [one_run() for _ in range(2)]
+    dt = sum(r[0] for r in runs) / len(runs)
+    n, out_len = runs[-1][1], runs[-1][2]
     model.train(was)
     frames = int(out_len.sum())
     algo = n * LF_STEP_BYTES + LF_KEY_BYTES * n * (n + 1) / 2
     return {"value": round(frames / dt, 1), "unit": "frames/s", "ms_per_run": round(dt * 1e3, 2),
-            "steps_run": n, "frames": frames, "ms_per_frame_step": round(dt / n * 1e3, 4),
+            "runs_ms": [round(r[0] * 1e3, 2) for r in runs], "steps_run": n, "frames": frames, "ms_per_frame_step": round(dt / n * 1e3, 4),
             "config": {"workload": "long-form AR decode: encoder + hipGraph decode steps until every utterance "
                                    "stops or reaches its cap + post-net", "batch": LF_B, "text_len": TX,
                        "t_max": LF_T, "caps": "U[1000, 2000] seeded",

@@ -291,7 +291,7 @@ class Decoder:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            with torch.cuda.graph(self.graph, stream=s, capture_error_mode="thread_local"):
+            with torch.cuda.graph(self.graph, stream=s, capture_error_mode=ops.CAPTURE_MODE):
                 self.step()
         torch.cuda.current_stream().wait_stream(s)
         self.reset()

@@ -16,6 +16,7 @@ import math
 
 import torch
 
+from . import ops
 from .config import TTSConfig
 from .engine import Arena, TTSEngine
 from .params import from_state_dict, grads_to_state_dict_names, to_state_dict
@@ -236,7 +237,7 @@ class TransformerTTS:
         torch.cuda.synchronize()
         with torch.cuda.stream(s):
             cur = [torch.cuda.CUDAGraph()]
-            cur[0].capture_begin(capture_error_mode="thread_local")
+            cur[0].capture_begin(capture_error_mode=ops.CAPTURE_MODE)
             if sync is not None and hasattr(sync, "take_ready"):
                 # cut the forward+backward graph wherever a gradient bucket becomes final,
                 # so the replay can start that bucket's all-reduce while the rest of the
@@ -251,7 +252,7 @@ class TransformerTTS:
                         cur[0].capture_end()
                         segs.append((cur[0], idx))
                         cur[0] = torch.cuda.CUDAGraph()
-                        cur[0].capture_begin(capture_error_mode="thread_local")
+                        cur[0].capture_begin(capture_error_mode=ops.CAPTURE_MODE)
                 e.grad_ready_hook = cut
             e.forward(A)
             e.loss(A)
@@ -264,7 +265,7 @@ class TransformerTTS:
             if sync is not None and hasattr(sync, "take_ready"):
                 sync.reset()
             if g2 is not None:
-                with torch.cuda.graph(g2, stream=s, capture_error_mode="thread_local"):
+                with torch.cuda.graph(g2, stream=s, capture_error_mode=ops.CAPTURE_MODE):
                     e.optimizer_step()
         torch.cuda.current_stream().wait_stream(s)
         e.grad_ready_hook = hook

@@ -13,6 +13,11 @@ import torch
 from . import _lib
 from ._lib import GemmArgs, check, dt, lib, ptr, stream_ptr
 
+# hipGraph capture mode of the training-step and decode-step graphs.  thread_local: RCCL's
+# watchdog thread polls its work events during a capture, which a global-mode capture
+# treats as a prohibited call (env TT2_CAPTURE_MODE: an A/B switch).
+CAPTURE_MODE = os.environ.get("TT2_CAPTURE_MODE", "thread_local")
+
 
 def drop_thr(p: float) -> int:
     """floor(p * 2^32) -- identical to the oracle's threshold."""
