@@ -338,7 +338,7 @@ def main():
             os.environ.setdefault("MASTER_PORT", "29533")
             dist.init_process_group("nccl", rank=0, world_size=1)
         broadcast_params(model)
-        sync = attach(model)
+        sync = attach(model, bucket_bytes=int(float(os.environ.get("TT2_BUCKET_MB", "25")) * (1 << 20)))
     model.train()
     text, tl, mel, ml = synth_batch(rank)
     sync_fn = sync.finish if sync is not None else None
