@@ -213,12 +213,16 @@ def gemm_kernel_name(plan: int, ta: int, tb: int) -> str:
 def roofline(model, text, tl, mel, ml):
     """Live per-launch timing of the dominant kernel family in one eager step."""
     from tt2 import ops
+    # rank 0 only: the DP gradient hook must not fire (its all-reduces would have no peers)
+    eng = model.engine
+    hook, eng.grad_ready_hook = eng.grad_ready_hook, None
     ops.PROBE = probe = ops.LaunchProbe()
     try:
         model.train_step(text, tl, mel, ml)
         summ = probe.summary()
     finally:
         ops.PROBE = None
+        eng.grad_ready_hook = hook
     # dominant = the GEMM variant with the most device time
     key, (n, flops, secs, abytes) = max(summ.items(), key=lambda kv: kv[1][2])
     secs = probe.replay_time(key)      # same launches, back-to-back timing
@@ -313,7 +317,7 @@ def main():
     from tt2.model import TransformerTTS
 
     rank, world, local = init_from_env()
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % torch.cuda.device_count())   # ranks > GPUs: a 1-GPU gloo rehearsal
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}")
     torch.manual_seed(0)

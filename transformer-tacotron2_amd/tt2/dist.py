@@ -83,7 +83,8 @@ def init_from_env(backend: str | None = None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # TT2_DIST_BACKEND=gloo: rehearse the multi-rank control flow on one GPU
+            backend = os.environ.get("TT2_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
