@@ -239,10 +239,17 @@ def roofline(model, text, tl, mel, ml):
         t = json.load(open(os.path.join(prof, tfiles[-1])))
         if t.get("kernel", "") == kname:
             traffic, tsrc = round(t["hbm_bytes_per_launch"]), "profiles/" + tfiles[-1]
+    busy, bsrc = None, None   # SQ_VALU_MFMA_BUSY_CYCLES pass (tools/summarize_mfma.py)
+    bfiles = sorted(f for f in os.listdir(prof) if f.endswith("_mfma_busy.json")) if os.path.isdir(prof) else []
+    if bfiles:
+        for name, v in json.load(open(os.path.join(prof, bfiles[-1])))["kernels"].items():
+            if kname + "(" in name:
+                busy, bsrc = round(v["busy_fraction"], 4), "profiles/" + bfiles[-1]
     return {
         "kernel": kname,
         "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_source": tsrc,
+        "mfma_busy_under_profiler": busy, "mfma_busy_source": bsrc,
         "algo_bytes_per_launch": round(abytes / n), "launches_per_step": n, "flops_per_launch": flops / n,
         "avg_launch_us": round(secs / n * 1e6, 2),
         "all_gemms": {"launches": sum(v[0] for v in summ.values()), "ms_per_step": round(tot_t * 1e3, 3),
