@@ -112,6 +112,13 @@ typedef struct tt2_gemm_args {
   uint32_t* emit_seed;
   int32_t* emit_done;
   int32_t emit_nmels, emit_tmax;
+  /* frame emit, stop handling: emit_stop_bias (optional f32 [m][emit_tmax]) is added to the stop
+   * logit before it is stored (per-utterance length injection); emit_stop_len (optional int32 [m])
+   * records t + 1 at the first frame whose stop logit >= emit_stop_thr (entries the caller set to
+   * INT32_MAX mean "still running"). */
+  const float* emit_stop_bias;
+  int32_t* emit_stop_len;
+  float emit_stop_thr;
 } tt2_gemm_args;
 
 size_t tt2_gemm_workspace_size(const tt2_gemm_args* a);
@@ -171,15 +178,88 @@ typedef struct tt2_attn_decode_args {
   const int32_t* t_ptr;
   int32_t batch, heads, head_dim, tk, dtype;
   float scale;
+  /* optional early exit: when stop_len != NULL, batch element b is finished once
+   * *step >= stop_len[b] (step defaults to t_ptr); its output row is 0 and no key is read */
+  const int32_t* stop_len;
+  const int32_t* step;
 } tt2_attn_decode_args;
 int tt2_attn_decode(const tt2_attn_decode_args* a, hipStream_t stream);
 /* cache[b*c_bstride + (*t_ptr)*c_ld + c] = src[b*src_ld + c], c < n */
 int tt2_kv_append(const void* src, int64_t src_ld, void* cache, int64_t c_bstride, int64_t c_ld, int n, int batch,
                   const int32_t* t_ptr, int dtype, hipStream_t stream);
-/* heads [batch, heads_ld] f32 -> mel_seq[b, t, :], stop_seq[b, t], prev[b, :] (prev_dtype);
+/* heads [batch, heads_ld] f32 -> mel_seq[b, t, :], stop_seq[b, t] (+ stop_bias[b, t] if given),
+ * prev[b, :] (prev_dtype); stop_len[b] = t + 1 at the first stop logit >= stop_thr (if given);
  * then *t_ptr += 1 and *seed += 1 (seed may be NULL) */
 int tt2_decode_emit(const float* heads, int64_t heads_ld, int batch, int n_mels, int t_max, float* mel_seq,
-                    float* stop_seq, void* prev, int prev_dtype, int32_t* t_ptr, uint32_t* seed, hipStream_t stream);
+                    float* stop_seq, void* prev, int prev_dtype, int32_t* t_ptr, uint32_t* seed,
+                    const float* stop_bias, int32_t* stop_len, float stop_thr, hipStream_t stream);
+
+/* ------------------------------------------------------------ decode step / graph
+ * The whole autoregressive decode step (the loop body of
+ * modeling_speecht5.py:2215-2267 with a KV cache): pre-net on the previous frame (optional
+ * always-on dropout, sites 128 / 129, seed = *seed, bumped every step) -> scaled PE at the
+ * device step t -> n_layers x [self-attention with KV-cache append, cross-attention over the
+ * encoder memory K/V, FFN, post-LNs] -> mel / stop heads -> frame emit, t += 1.  The library
+ * composes the launches itself, so a non-Python host (C++, a JNI / cgo binding) can drive
+ * inference; tt2_decode_graph_create captures one step as a hipGraph that the library owns,
+ * and tt2_decode_graph_launch replays it n times.
+ *
+ * Early exit: an utterance finishes at the first frame whose stop logit (+ stop_bias) reaches
+ * stop_logit (stop_len[b] = that frame + 1); afterwards its attention reads no keys.  The
+ * caller polls stop_len between launches (stop_logit = +inf: forced length).  Frames emitted after
+ * an utterance's stop are zero, so a batched post-net sees each utterance zero-padded at its length.
+ *
+ * Weights are in the step dtype (bf16 / f16 / f32, [out, in] row-major as in the checkpoint);
+ * biases, LayerNorm parameters, alpha and the PE table are f32.  All buffers are caller-owned;
+ * the workspace (tt2_decode_workspace_size bytes) holds the KV cache and step activations. */
+#define TT2_MAX_DEC_LAYERS 16
+typedef struct tt2_dec_layer {
+  const void* qkv_w; const float* qkv_b;     /* self-attention in_proj [3d, d] */
+  const void* o_w; const float* o_b;         /* self-attention out_proj [d, d] */
+  const float* ln1_g; const float* ln1_b;
+  const void* cq_w; const float* cq_b;       /* cross-attention query rows of in_proj [d, d] */
+  const void* co_w; const float* co_b;       /* cross-attention out_proj [d, d] */
+  const float* ln2_g; const float* ln2_b;
+  const void* ffn1_w; const float* ffn1_b;   /* [F, d] */
+  const void* ffn2_w; const float* ffn2_b;   /* [d, F] */
+  const float* ln3_g; const float* ln3_b;
+} tt2_dec_layer;
+
+typedef struct tt2_decode_desc {
+  int32_t batch, text_len, t_max, n_layers, d_model, n_heads, d_ffn, n_mels, prenet_dim;
+  int32_t dtype;        /* step storage type: TT2_DT_BF16, TT2_DT_F16 (batch <= 64) or TT2_DT_F32 */
+  int32_t schedule;     /* 0 auto, 1 plain (one launch per op), 2 split-K (16-bit, batch <= 64) */
+  float ln_eps;
+  float prenet_dropout; /* 0 = off (Tacotron2 keeps it on at inference) */
+  float stop_logit;     /* logit(stop_threshold); +inf never stops */
+  const void* fc1_w; const float* fc1_b;     /* pre-net [P, n_mels], [P, P], proj [d, P] */
+  const void* fc2_w; const float* fc2_b;
+  const void* proj_w; const float* proj_b;
+  const float* alpha;                        /* decoder PE scale (device scalar) */
+  const float* pe_table;                     /* [>= t_max][d] */
+  tt2_dec_layer layers[TT2_MAX_DEC_LAYERS];
+  const void* heads_w; const float* heads_b; /* [n_mels + 1, d]: mel rows, then the stop row */
+  const void* mem_kv;        /* [batch * text_len, n_layers * 2d]: layer l's K at column 2dl, V at 2dl + d */
+  const int32_t* text_lens;  /* [batch] phonemes per utterance */
+  float* mel_seq;            /* out [batch][t_max][n_mels] (pre-post-net frames) */
+  float* stop_seq;           /* out [batch][t_max] */
+  int32_t* stop_len;         /* out [batch]; INT32_MAX while running */
+  const float* stop_bias;    /* optional [batch][t_max] */
+  int32_t* step;             /* device step counter */
+  uint32_t* seed;            /* device dropout seed */
+  void* workspace; size_t ws_bytes;
+} tt2_decode_desc;
+typedef struct tt2_decode_graph* tt2_decode_graph_t;
+
+size_t tt2_decode_workspace_size(const tt2_decode_desc* d);
+/* step = 0, seed = seed0, previous frame = 0 (the go frame), stop_len = INT32_MAX */
+int tt2_decode_reset(const tt2_decode_desc* d, uint32_t seed0, hipStream_t stream);
+/* one step as eager launches */
+int tt2_decode_step(const tt2_decode_desc* d, hipStream_t stream);
+int tt2_decode_graph_create(const tt2_decode_desc* d, hipStream_t stream, tt2_decode_graph_t* out);
+/* n_steps replays; frames past t_max are not emitted */
+int tt2_decode_graph_launch(tt2_decode_graph_t g, int32_t n_steps, hipStream_t stream);
+int tt2_decode_graph_destroy(tt2_decode_graph_t g);
 
 /* ------------------------------------------------------------- reductions */
 #define TT2_COLSUM_ROWS 128
@@ -310,6 +390,8 @@ typedef struct tt2_loss_args {
   int32_t batch, t, n_mels, grad_dtype;
   float pos_weight;
   float grad_scale;  /* multiplies every gradient (1/world_size under data parallelism) */
+  int32_t separate_grads;  /* 1: g_heads' mel columns hold only d/d(mel_before) (no residual
+                              d/d(mel_after) term folded in): the autograd boundary's layout */
 } tt2_loss_args;
 size_t tt2_loss_workspace_size(void);
 int tt2_tts_loss(const tt2_loss_args* a, hipStream_t stream);

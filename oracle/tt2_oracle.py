@@ -185,7 +185,9 @@ class MHA(nn.Module):
         q = q.view(B, Tq, h, dh).transpose(1, 2)
         k = k.view(B, Tk, h, dh).transpose(1, 2)
         v = v.view(B, Tk, h, dh).transpose(1, 2)
-        s = (q @ k.transpose(-1, -2)) / math.sqrt(dh)
+        # scores and softmax in f32 (a no-op for the f32 oracle; under torch.autocast it mirrors
+        # AMP's f32 softmax, so the autocast oracle is a standard bf16 mixed-precision reference)
+        s = (q @ k.transpose(-1, -2)).float() / math.sqrt(dh)
         allowed = torch.ones(B, 1, Tq, Tk, dtype=torch.bool)
         if key_len is not None:
             allowed = allowed & (torch.arange(Tk)[None, None, None, :] < key_len.view(B, 1, 1, 1))
@@ -319,8 +321,8 @@ class Decoder(nn.Module):
         self.pos_drop = HashDropout(c.dropout, SITE_DEC_PE)
         self.layers = nn.ModuleList([DecoderLayer(c, l) for l in range(c.n_dec)])
 
-    def forward(self, dec_in, mem, text_len, mel_len):
-        x = self.pos_drop(self.pos(self.prenet(dec_in)))
+    def forward(self, dec_in, mem, text_len, mel_len, prenet_out=None):
+        x = self.pos_drop(self.pos(self.prenet(dec_in) if prenet_out is None else prenet_out))
         ps, pc = [], []
         for layer in self.layers:
             x, a, b = layer(x, mem, text_len, mel_len)
@@ -385,11 +387,31 @@ class TransformerTTSOracle(nn.Module):
     def loss(self, outputs, mel, mel_len):
         return tts_loss(outputs[0], outputs[1], outputs[2], mel, mel_len, self.cfg.stop_pos_weight)
 
+    def infer_prenet(self, frames, seed0: int):
+        """Decoder pre-net at inference with Tacotron2's always-on dropout (sites 128 / 129):
+        frame j of the prefix (the input of decode step j) draws its masks with seed
+        seed0 + j over the flat [B, 256] index, as the GPU decode step does."""
+        c, pn = self.cfg, self.decoder.prenet
+        B, T, _ = frames.shape
+        p = c.prenet_dropout
+        keep = lambda site, j: torch.from_numpy(  # noqa: E731
+            dropout_keep(seed0 + j, site, B * c.dec_prenet, p)).reshape(B, c.dec_prenet).float() / (1.0 - p)
+        outs = []
+        for j in range(T):
+            h = F.relu(pn.fc1(frames[:, j])) * keep(SITE_INFER_FC1, j)
+            h = F.relu(pn.fc2(h)) * keep(SITE_INFER_FC2, j)
+            outs.append(pn.proj(h))
+        return torch.stack(outs, 1)
+
     @torch.no_grad()
-    def infer(self, text, text_len, max_len: int, stop_threshold: float = 0.5, force_len: bool = False):
+    def infer(self, text, text_len, max_len: int, stop_threshold: float = 0.5, force_len: bool = False,
+              prenet_dropout_seed: int | None = None, stop_bias=None):
         """Greedy AR decode (loop shape of modeling_speecht5.py:2215-2267),
         recomputing the full prefix each step.  Returns (mel_after, out_len,
-        mel_before, stop_logits)."""
+        mel_before, stop_logits).  prenet_dropout_seed: Tacotron2's always-on pre-net
+        dropout (see infer_prenet); stop_bias [B, max_len]: added to the stop logits
+        (per-utterance length injection).  An utterance's out_len is its
+        first frame with sigmoid(stop) >= threshold, + 1."""
         B = text.size(0)
         c = self.cfg
         mem, _ = self.encoder(text, text_len)
@@ -399,10 +421,13 @@ class TransformerTTSOracle(nn.Module):
         done = torch.zeros(B, dtype=torch.bool)
         full_len = torch.full((B,), max_len, dtype=torch.long)
         for t in range(max_len):
-            x, _, _ = self.decoder(frames, mem, text_len, full_len)
+            pre = None if prenet_dropout_seed is None else self.infer_prenet(frames, prenet_dropout_seed)
+            x, _, _ = self.decoder(frames, mem, text_len, full_len, prenet_out=pre)
             last = x[:, -1]
             f = self.mel_linear(last)
             s = self.stop_linear(last).squeeze(-1)
+            if stop_bias is not None:
+                s = s + stop_bias[:, t]
             befores.append(f)
             stops.append(s)
             frames = torch.cat([frames, f[:, None]], dim=1)

@@ -44,3 +44,13 @@ def test_roofline_detaches_dp_hook(monkeypatch):
     assert ops.PROBE is None
     assert r["kernel"] == "gemm7_kernel<true, true>" and r["launches_per_step"] == 2
     assert abs(r["achieved"] - 2000.0) < 1e-6 and r["bound"] == "mfma"
+
+
+def test_longform_algo_bytes_counts_running_utterances_only():
+    """cfg5's roofline bytes: weights once per step, each utterance's cross K/V and t + 1 self
+    K/V rows only while it runs (its attention exits after its stop)."""
+    import torch
+    lens = torch.tensor([1, 3])
+    got = bench.longform_algo_bytes(lens, 3)
+    want = 3 * bench.LF_W_BYTES + 4 * bench.LF_CROSS_BYTES + bench.LF_KEY_BYTES * (1 + (1 + 2 + 3))
+    assert abs(got - want) < 1e-6 * want

@@ -1,0 +1,88 @@
+"""bf16 parity of the benchmarked precision (all rows; 8(c)).
+
+The fp32 oracle is the reference; a second reference -- the same oracle under
+torch.autocast("cpu", dtype=torch.bfloat16), i.e. standard bf16 mixed precision with f32
+softmax / accumulation -- measures how far bf16 arithmetic alone moves each output and
+each parameter gradient.  The GPU bf16 step (LJSpeech shape 128 / 800, B = 2, one ragged
+utterance, dropout on) must sit within 1.5x of that deviation (+ 2e-3 absolute, for
+quantities that bf16 rounding barely moves) for the forward outputs, the loss terms and
+EVERY parameter gradient.  The per-quantity deviations are written to
+gpurun_out/bf16_parity.json."""
+import copy
+import json
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from tt2.config import TTSConfig  # noqa: E402
+from tt2.model import TransformerTTS  # noqa: E402
+from tt2_oracle import OracleConfig, TransformerTTSOracle, init_deterministic  # noqa: E402
+
+RATIO, FLOOR = 1.5, 2e-3
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _run_oracle(oracle, batch, autocast):
+    text, tl, mel, ml = batch
+    oracle.set_seed(7)
+    oracle.zero_grad(set_to_none=True)
+    with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
+        out = oracle(text, tl, mel, ml)
+        total, parts = oracle.loss(out[:3], mel, ml)
+    total.float().backward()
+    outs = {"mel_before": out[0].float(), "mel_after": out[1].float(), "stop": out[2].float(),
+            "loss": torch.stack([total.float()] + [parts[k].float() for k in ("mel_before", "mel_after", "stop")])}
+    grads = {k: p.grad.float() for k, p in oracle.named_parameters() if p.grad is not None}
+    return outs, grads
+
+
+def test_bf16_step_within_autocast_deviation():
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    base = init_deterministic(TransformerTTSOracle(OracleConfig()), 0).train()
+    model = TransformerTTS(TTSConfig(), dtype=torch.bfloat16).train()
+    model.load_state_dict(base.state_dict())
+    g = torch.Generator().manual_seed(2)
+    B, Tx, Ty = 2, 128, 800
+    text = torch.randint(1, 80, (B, Tx), generator=g)
+    tl, ml = torch.tensor([128, 97]), torch.tensor([800, 611])
+    text[1, 97:] = 0
+    mel = torch.randn(B, Ty, 80, generator=g)
+    mel[1, 611:] = 0
+    batch = (text, tl, mel, ml)
+    ref_out, ref_g = _run_oracle(copy.deepcopy(base), batch, autocast=False)
+    ac_out, ac_g = _run_oracle(copy.deepcopy(base), batch, autocast=True)
+
+    model.set_seed(7)
+    mb, ma, ms, _ = model(text, tl, mel, ml)
+    total, parts = model.loss()
+    model.backward()
+    gpu_out = {"mel_before": mb, "mel_after": ma, "stop": ms,
+               "loss": torch.stack([total] + [parts[k] for k in ("mel_before", "mel_after", "stop")])}
+    gpu_g = model.grads_state_dict()
+
+    rows, bad = {}, []
+    for k in ref_out:
+        d_ac, d_gpu = rel(ac_out[k], ref_out[k]), rel(gpu_out[k], ref_out[k])
+        rows["out." + k] = (d_gpu, d_ac)
+    for k, r in ref_g.items():
+        if r.abs().max() == 0:          # conv biases in front of training-mode BN: exactly 0
+            assert gpu_g[k].abs().max().item() < 1e-6, k
+            continue
+        rows["grad." + k] = (rel(gpu_g[k], r), rel(ac_g[k], r))
+    for k, (d_gpu, d_ac) in rows.items():
+        if d_gpu > RATIO * d_ac + FLOOR:
+            bad.append((k, d_gpu, d_ac))
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/bf16_parity.json", "w") as f:
+        json.dump({"ratio": RATIO, "floor": FLOOR, "rows": {k: {"gpu": a, "autocast": b} for k, (a, b) in rows.items()},
+                   "violations": bad}, f, indent=1)
+    worst = max(rows.items(), key=lambda kv: kv[1][0] / (kv[1][1] + 1e-12))
+    print(f"{len(rows)} quantities; worst gpu/autocast: {worst}")
+    assert not bad, f"{len(bad)} quantities beyond {RATIO}x the autocast deviation: {bad[:8]}"

@@ -12,7 +12,7 @@ import torch.distributed as dist
 pytestmark = pytest.mark.gpu
 
 from tt2.config import TTSConfig  # noqa: E402
-from tt2.dist import attach  # noqa: E402
+from tt2.dist import GradSync, attach  # noqa: E402
 from tt2.model import TransformerTTS  # noqa: E402
 
 
@@ -66,3 +66,57 @@ def test_segmented_dp_graph_matches_single_graph(nccl_group):
         assert torch.equal(la, lb)
     torch.cuda.synchronize()
     assert torch.equal(ref.engine.params, dp.engine.params)
+
+
+class SnapshotSync(GradSync):
+    """GradSync that snapshots each bucket on the compute stream at the moment its
+    all-reduce is launched (what RCCL would read) and, in finish(), compares every snapshot
+    with the final gradients.  A kernel that writes into a bucket after it was handed to
+    RCCL -- a missing or misplaced grad_ready call, or a deferred LayerNorm finalize landing
+    in an already-launched bucket -- shows up as a mismatch even on one rank, where the
+    all-reduce itself is the identity."""
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        self.snaps, self.bad, self.steps = [], [], 0
+
+    def _launch(self, lo, hi):
+        self.snaps.append((lo, hi, self.flat[lo:hi].clone()))
+        super()._launch(lo, hi)
+
+    def finish(self):
+        super().finish()
+        assert sorted((lo, hi) for lo, hi, _ in self.snaps) == sorted(self.buckets)
+        for lo, hi, s in self.snaps:
+            if not torch.equal(s, self.flat[lo:hi]):
+                self.bad.append((lo, hi))
+        self.snaps = []
+        self.steps += 1
+
+
+@pytest.mark.parametrize("bucket_mb", [4, 25])
+def test_buckets_final_when_launched_cfg2(nccl_group, bucket_mb):
+    """At the cfg2 shape (B = 16, 128 phonemes, 800 frames, dropout on): every gradient
+    bucket is final when its all-reduce is launched, eagerly (hook during the backward)
+    and in the segmented captured step (launches between graph segments)."""
+    g = torch.Generator().manual_seed(4)
+    B, Tx, Ty = 16, 128, 800
+    text = torch.randint(1, 80, (B, Tx), generator=g).cuda()
+    tl = torch.full((B,), Tx, dtype=torch.int32).cuda()
+    mel = torch.randn(B, Ty, 80, generator=g).cuda()
+    ml = torch.full((B,), Ty, dtype=torch.int32).cuda()
+    m = _model()
+    eng = m.engine
+    sync = SnapshotSync(eng.grads, bucket_mb << 20)
+    eng.grad_scale = 1.0 / sync.world
+    eng.grad_ready_hook = sync.ready
+    assert len(sync.buckets) >= 3
+    for _ in range(2):
+        m.train_step(text, tl, mel, ml, sync_grads=sync.finish)
+    torch.cuda.synchronize()
+    assert sync.steps == 2 and sync.bad == [], f"eager: buckets written after launch {sync.bad}"
+    run = m.capture_train_step(B, Tx, Ty, sync_grads=sync.finish)
+    for _ in range(2):
+        run(text, tl, mel, ml)
+    torch.cuda.synchronize()
+    assert sync.steps == 4 and sync.bad == [], f"captured: buckets written after launch {sync.bad}"

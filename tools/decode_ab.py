@@ -1,4 +1,4 @@
-"""Decode throughput A/B (dev tool, GPU): fused vs unfused decode step, cfg3 shape."""
+"""Decode throughput A/B (dev tool, GPU): libtt2 split vs plain decode schedule, cfg3 shape."""
 import os
 import sys
 import time
@@ -10,7 +10,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 from tt2.config import TTSConfig  # noqa: E402
-from tt2.infer import Decoder  # noqa: E402
+from tt2.infer import SCHEDULE_PLAIN, SCHEDULE_SPLIT, Decoder  # noqa: E402
 from tt2.model import TransformerTTS  # noqa: E402
 
 torch.manual_seed(0)
@@ -21,13 +21,10 @@ DB = int(os.environ.get("DEC_B", bench.DEC_B))        # DEC_B=64 DEC_DT=f16: the
 DDT = torch.float16 if os.environ.get("DEC_DT") == "f16" else None
 text = torch.randint(1, 80, (DB, bench.TX), generator=g).cuda()
 tl = torch.full((DB,), bench.TX, dtype=torch.int32, device="cuda")
-CFGS = [(3, 4, 8), (3, 8, 8), (3, 8, 16), (3, 4, 16), (3, 2, 4)] if DB > 32 else \
-    [(1, 4, 8), (2, 4, 8), (3, 4, 8), (3, 2, 4), (3, 4, 16)]
-for fuse, so, sf in CFGS + CFGS:
-    dec = Decoder(model.engine, DB, bench.TX, bench.DEC_T, dtype=DDT)
-    dec.fuse, dec.split_o, dec.split_f = fuse, so, sf
+for sched in (SCHEDULE_SPLIT, SCHEDULE_PLAIN) * 2:
+    dec = Decoder(model.engine, DB, bench.TX, bench.DEC_T, dtype=DDT, schedule=sched)
     dec.encode(text, tl)
-    dec.capture()
+    dec.capture(None)
     dec.reset()
     dec.decode_loop(32)
     torch.cuda.synchronize()
@@ -36,4 +33,4 @@ for fuse, so, sf in CFGS + CFGS:
     dec.decode_loop(400, stop_threshold=None)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print(f"fuse={fuse} split_o={so} split_f={sf}: {dt / 400 * 1e6:.1f} us/step", flush=True)
+    print(f"schedule={sched}: {dt / 400 * 1e6:.1f} us/step", flush=True)

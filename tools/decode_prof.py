@@ -21,7 +21,7 @@ text = torch.randint(1, 80, (bench.DEC_B, bench.TX), generator=g).cuda()
 tl = torch.full((bench.DEC_B,), bench.TX, dtype=torch.int32, device="cuda")
 dec = Decoder(model.engine, bench.DEC_B, bench.TX, bench.DEC_T)
 dec.encode(text, tl)
-dec.capture()
+dec.capture(None)
 dec.reset()
 dec.decode_loop(40, stop_threshold=None)
 torch.cuda.synchronize()

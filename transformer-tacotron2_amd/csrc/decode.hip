@@ -46,6 +46,8 @@ struct DecArgs {
   int64_t q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld;
   const int32_t* key_len;   // per-batch number of keys (cross attention) or null
   const int32_t* t_ptr;     // self attention: keys = *t_ptr + 1
+  const int32_t* stop_len;  // optional [B]: utterance b is finished once *step >= stop_len[b]
+  const int32_t* step;
   int tk, H;
   float scale;
 };
@@ -57,6 +59,11 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
   const int dc = lane & 7, kg = lane >> 3;   // 8-dim chunk, key slot within an 8-key group
+  if (a.stop_len && *a.step >= a.stop_len[b]) {
+    // a finished utterance: its frames past the stop are discarded, so skip the key stream
+    if (threadIdx.x < D) reinterpret_cast<T*>(a.out)[(int64_t)b * a.o_ld + h * D + threadIdx.x] = from_f32<T>(0.f);
+    return;
+  }
   float qv[8];
   load8f(reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld + h * D + dc * 8, qv);
   int nk = a.tk;
@@ -152,17 +159,21 @@ __global__ void kv_append_kernel(const T* src, int64_t src_ld, T* cache, int64_t
 // heads [B, hld] f32 -> mel_seq[b][t][:], stop_seq[b][t], prev frame (T); then t += 1, seed += 1
 template <typename T>
 __global__ void decode_emit_kernel(const float* heads, int64_t hld, int B, int NM, int tmax, float* mel_seq,
-                                   float* stop_seq, T* prev, int32_t* t_ptr, uint32_t* seed) {
+                                   float* stop_seq, T* prev, int32_t* t_ptr, uint32_t* seed, const float* stop_bias,
+                                   int32_t* stop_len, float stop_thr) {
   const int t = *t_ptr;
   for (int i = threadIdx.x; i < B * (NM + 1); i += blockDim.x) {
     const int b = i / (NM + 1), c = i % (NM + 1);
     const float v = heads[(int64_t)b * hld + c];
     if (t < tmax) {
       if (c < NM) {
-        mel_seq[((int64_t)b * tmax + t) * NM + c] = v;
-        prev[(int64_t)b * NM + c] = from_f32<T>(v);
+        const float vm = (stop_len && stop_len[b] <= t) ? 0.f : v;   // zero frames after the stop
+        mel_seq[((int64_t)b * tmax + t) * NM + c] = vm;
+        prev[(int64_t)b * NM + c] = from_f32<T>(vm);
       } else {
-        stop_seq[(int64_t)b * tmax + t] = v;
+        const float vs = stop_bias ? v + stop_bias[(int64_t)b * tmax + t] : v;
+        stop_seq[(int64_t)b * tmax + t] = vs;
+        if (stop_len && vs >= stop_thr && stop_len[b] > t) stop_len[b] = t + 1;
       }
     }
   }
@@ -185,6 +196,9 @@ extern "C" int tt2_attn_decode(const tt2_attn_decode_args* p, hipStream_t s) {
   a.q = p->q; a.k = p->k; a.v = p->v; a.out = p->out;
   a.q_ld = p->q_ld; a.k_bstride = p->k_bstride; a.k_ld = p->k_ld; a.v_bstride = p->v_bstride; a.v_ld = p->v_ld;
   a.o_ld = p->o_ld; a.key_len = p->key_len; a.t_ptr = p->t_ptr; a.tk = p->tk; a.H = p->heads; a.scale = p->scale;
+  a.stop_len = p->stop_len;
+  a.step = p->step ? p->step : p->t_ptr;
+  if (a.stop_len && !a.step) return tt2_set_error(TT2_E_INVALID, "tt2_attn_decode: stop_len needs step or t_ptr");
   dim3 g(p->batch * p->heads);
   // 8 waves per (batch, head): each wave takes 1/8 of the keys, 32 keys per iteration
   if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL((attn_decode_kernel<bf16, 8>), g, dim3(8 * 64), 0, s, a);
@@ -208,12 +222,16 @@ extern "C" int tt2_kv_append(const void* src, int64_t src_ld, void* cache, int64
 
 extern "C" int tt2_decode_emit(const float* heads, int64_t heads_ld, int batch, int n_mels, int t_max,
                                float* mel_seq, float* stop_seq, void* prev, int prev_dtype, int32_t* t_ptr,
-                               uint32_t* seed, hipStream_t s) {
+                               uint32_t* seed, const float* stop_bias, int32_t* stop_len, float stop_thr,
+                               hipStream_t s) {
   if (prev_dtype == TT2_DT_BF16)
     hipLaunchKernelGGL(decode_emit_kernel<bf16>, dim3(1), dim3(NT), 0, s, heads, heads_ld, batch, n_mels, t_max,
-                       mel_seq, stop_seq, (bf16*)prev, t_ptr, seed);
+                       mel_seq, stop_seq, (bf16*)prev, t_ptr, seed, stop_bias, stop_len, stop_thr);
+  else if (prev_dtype == TT2_DT_F16)
+    hipLaunchKernelGGL(decode_emit_kernel<f16>, dim3(1), dim3(NT), 0, s, heads, heads_ld, batch, n_mels, t_max,
+                       mel_seq, stop_seq, (f16*)prev, t_ptr, seed, stop_bias, stop_len, stop_thr);
   else
     hipLaunchKernelGGL(decode_emit_kernel<float>, dim3(1), dim3(NT), 0, s, heads, heads_ld, batch, n_mels, t_max,
-                       mel_seq, stop_seq, (float*)prev, t_ptr, seed);
+                       mel_seq, stop_seq, (float*)prev, t_ptr, seed, stop_bias, stop_len, stop_thr);
   return tt2_check_launch(hipGetLastError(), "tt2_decode_emit");
 }

@@ -621,6 +621,7 @@ struct SkinnyFuse {
   const float* pe; const float* pe_alpha; const int32_t* pe_t;                     // + alpha * pe[t][n]
   float* emit_mel; float* emit_stop; void* emit_prev; int32_t* emit_t; uint32_t* emit_seed;
   int32_t* emit_done; int emit_nmels, emit_tmax;                                   // frame emit (heads)
+  const float* emit_stop_bias; int32_t* emit_stop_len; float emit_stop_thr;        // stop injection / tracking
 };
 
 constexpr int SK_LN_LD = 512 + 8;   // bf16 per LDS row of the normalised A (16-B pad)
@@ -794,10 +795,17 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const TE* X, int64_t ld
         reinterpret_cast<TE*>(F.kv)[(int64_t)m * F.kv_bstride + (int64_t)kv_t * F.kv_ld + (nn - F.kv_col0)] = (TE)y;
       if (F.emit_mel && em_t < F.emit_tmax) {
         if (nn < F.emit_nmels) {
-          F.emit_mel[((int64_t)m * F.emit_tmax + em_t) * F.emit_nmels + nn] = y;
-          reinterpret_cast<TE*>(F.emit_prev)[(int64_t)m * F.emit_nmels + nn] = (TE)y;
+          // frames after an utterance's stop are zero (its post-net then sees zero padding at
+          // its own length; this step's stop update is e + 1 > em_t, so no race on the read)
+          const float ym = (F.emit_stop_len && F.emit_stop_len[m] <= em_t) ? 0.f : y;
+          F.emit_mel[((int64_t)m * F.emit_tmax + em_t) * F.emit_nmels + nn] = ym;
+          reinterpret_cast<TE*>(F.emit_prev)[(int64_t)m * F.emit_nmels + nn] = (TE)ym;
         } else if (nn == F.emit_nmels) {
-          F.emit_stop[(int64_t)m * F.emit_tmax + em_t] = y;
+          // the stop logit (+ an injected per-utterance bias); the first frame at or above the
+          // threshold fixes the utterance's length (one thread owns row m's stop column)
+          const float ys = F.emit_stop_bias ? y + F.emit_stop_bias[(int64_t)m * F.emit_tmax + em_t] : y;
+          F.emit_stop[(int64_t)m * F.emit_tmax + em_t] = ys;
+          if (F.emit_stop_len && ys >= F.emit_stop_thr && F.emit_stop_len[m] > em_t) F.emit_stop_len[m] = em_t + 1;
         }
       }
     }
@@ -1602,7 +1610,8 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
     SkinnyFuse F{reinterpret_cast<const bf16*>(a->a_ln_branch), a->a_ln_gamma, a->a_ln_beta,
                  reinterpret_cast<bf16*>(a->a_ln_out), a->a_ln_eps, a->kv_cache, a->kv_t,
                  a->kv_col0, a->kv_bstride, a->kv_ld, a->pe_table, a->pe_alpha, a->pe_t, a->emit_mel, a->emit_stop,
-                 a->emit_prev, a->emit_t, a->emit_seed, a->emit_done, a->emit_nmels, a->emit_tmax};
+                 a->emit_prev, a->emit_t, a->emit_seed, a->emit_done, a->emit_nmels, a->emit_tmax,
+                 a->emit_stop_bias, a->emit_stop_len, a->emit_stop_thr};
     const size_t lds = a->a_ln_gamma ? 32 * SK_LN_LD * sizeof(bf16) : 0;
     // split-K (splits > 1, main_only): raw partial slabs [splits][m][n] f32 in the workspace
     const int sp = a->splits > 1 ? a->splits : 1;

@@ -233,7 +233,8 @@ __global__ void cast2d_kernel(const void* src, int sdt, int64_t sld, void* dst, 
 template <typename T>
 __global__ __launch_bounds__(NT) void loss_kernel(const float* heads, int64_t hld, const float* after,
                                                   const float* target, const int32_t* mel_len, int B, int Tlen,
-                                                  int NM, float pos_weight, float gscale, float* g_heads, T* g_after, float* part) {
+                                                  int NM, float pos_weight, float gscale, float* g_heads, T* g_after, float* part,
+                                                  int separate) {
   __shared__ float red[3][NT / 64];
   int nvalid = 0;
   for (int b = 0; b < B; ++b) nvalid += min(max(mel_len[b], 0), Tlen);
@@ -260,7 +261,7 @@ __global__ __launch_bounds__(NT) void loss_kernel(const float* heads, int64_t hl
         ga = 2.f * da * inv_nm;
       }
       g_after[j] = from_f32<T>(ga);
-      g += ga;  // mel_after = mel_before + postnet(mel_before): residual path
+      if (!separate) g += ga;  // mel_after = mel_before + postnet(mel_before): residual path
     } else if (c == NM) {
       const float x = heads[i];
       const float y = (t == len - 1) ? 1.f : 0.f;
@@ -548,11 +549,11 @@ extern "C" int tt2_tts_loss(const tt2_loss_args* p, hipStream_t s) {
   if (p->grad_dtype == TT2_DT_BF16)
     hipLaunchKernelGGL(loss_kernel<bf16>, dim3(TT2_LOSS_BLOCKS), dim3(NT), 0, s, p->heads, p->heads_ld,
                        p->mel_after, p->target, p->mel_len, p->batch, p->t, p->n_mels, p->pos_weight, p->grad_scale, p->g_heads,
-                       (bf16*)p->g_after, part);
+                       (bf16*)p->g_after, part, p->separate_grads);
   else
     hipLaunchKernelGGL(loss_kernel<float>, dim3(TT2_LOSS_BLOCKS), dim3(NT), 0, s, p->heads, p->heads_ld,
                        p->mel_after, p->target, p->mel_len, p->batch, p->t, p->n_mels, p->pos_weight, p->grad_scale, p->g_heads,
-                       (float*)p->g_after, part);
+                       (float*)p->g_after, part, p->separate_grads);
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), 0, s, part, TT2_LOSS_BLOCKS, p->mel_len, p->batch,
                      p->t, p->n_mels, p->loss_out);
   return tt2_check_launch(hipGetLastError(), "tt2_tts_loss");

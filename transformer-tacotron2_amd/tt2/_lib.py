@@ -46,6 +46,7 @@ class GemmArgs(C.Structure):
         ("pe_table", vp), ("pe_alpha", vp), ("pe_t", vp),
         ("emit_mel", vp), ("emit_stop", vp), ("emit_prev", vp), ("emit_t", vp), ("emit_seed", vp),
         ("emit_done", vp), ("emit_nmels", i32), ("emit_tmax", i32),
+        ("emit_stop_bias", vp), ("emit_stop_len", vp), ("emit_stop_thr", f32),
     ]
 
 
@@ -184,6 +185,7 @@ class LossArgs(C.Structure):
         ("heads", vp), ("mel_after", vp), ("target", vp), ("mel_len", vp), ("loss_out", vp), ("g_heads", vp),
         ("g_after", vp), ("workspace", vp), ("ws_bytes", sz), ("heads_ld", i64),
         ("batch", i32), ("t", i32), ("n_mels", i32), ("grad_dtype", i32), ("pos_weight", f32), ("grad_scale", f32),
+        ("separate_grads", i32),
     ]
 
 
@@ -238,11 +240,42 @@ class AttnDecodeArgs(C.Structure):
         ("key_len", vp), ("t_ptr", vp),
         ("batch", i32), ("heads", i32), ("head_dim", i32), ("tk", i32), ("dtype", i32),
         ("scale", f32),
+        ("stop_len", vp), ("step", vp),
+    ]
+
+
+MAX_DEC_LAYERS = 16
+
+
+class DecLayer(C.Structure):
+    _fields_ = [(n, vp) for n in (
+        "qkv_w", "qkv_b", "o_w", "o_b", "ln1_g", "ln1_b", "cq_w", "cq_b", "co_w", "co_b", "ln2_g", "ln2_b",
+        "ffn1_w", "ffn1_b", "ffn2_w", "ffn2_b", "ln3_g", "ln3_b")]
+
+
+class DecodeDesc(C.Structure):
+    _fields_ = [
+        ("batch", i32), ("text_len", i32), ("t_max", i32), ("n_layers", i32), ("d_model", i32), ("n_heads", i32),
+        ("d_ffn", i32), ("n_mels", i32), ("prenet_dim", i32), ("dtype", i32), ("schedule", i32),
+        ("ln_eps", f32), ("prenet_dropout", f32), ("stop_logit", f32),
+        ("fc1_w", vp), ("fc1_b", vp), ("fc2_w", vp), ("fc2_b", vp), ("proj_w", vp), ("proj_b", vp),
+        ("alpha", vp), ("pe_table", vp),
+        ("layers", DecLayer * MAX_DEC_LAYERS),
+        ("heads_w", vp), ("heads_b", vp),
+        ("mem_kv", vp), ("text_lens", vp),
+        ("mel_seq", vp), ("stop_seq", vp), ("stop_len", vp), ("stop_bias", vp), ("step", vp), ("seed", vp),
+        ("workspace", vp), ("ws_bytes", sz),
     ]
 
 
 SIGNATURES.update({
     "tt2_attn_decode": ([C.POINTER(AttnDecodeArgs), vp], C.c_int),
     "tt2_kv_append": ([vp, i64, vp, i64, i64, C.c_int, C.c_int, vp, C.c_int, vp], C.c_int),
-    "tt2_decode_emit": ([vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp], C.c_int),
+    "tt2_decode_emit": ([vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp, vp, f32, vp], C.c_int),
+    "tt2_decode_workspace_size": ([C.POINTER(DecodeDesc)], sz),
+    "tt2_decode_reset": ([C.POINTER(DecodeDesc), u32, vp], C.c_int),
+    "tt2_decode_step": ([C.POINTER(DecodeDesc), vp], C.c_int),
+    "tt2_decode_graph_create": ([C.POINTER(DecodeDesc), vp, C.POINTER(vp)], C.c_int),
+    "tt2_decode_graph_launch": ([vp, i32, vp], C.c_int),
+    "tt2_decode_graph_destroy": ([vp], C.c_int),
 })

@@ -420,9 +420,10 @@ def cast2d(src, src_ld, dst, dst_ld, m, n):
 
 
 def tts_loss(heads, heads_ld, mel_after, target, mel_len, loss_out, g_heads, g_after, batch, t, n_mels,
-             pos_weight=5.0, grad_scale=1.0, ws: Workspace | None = None):
+             pos_weight=5.0, grad_scale=1.0, ws: Workspace | None = None, separate_grads=False):
     L = lib()
     a = _lib.LossArgs()
+    a.separate_grads = int(separate_grads)
     a.heads, a.mel_after, a.target, a.mel_len = heads.data_ptr(), mel_after.data_ptr(), target.data_ptr(), \
         mel_len.data_ptr()
     a.loss_out, a.g_heads, a.g_after = loss_out.data_ptr(), g_heads.data_ptr(), g_after.data_ptr()
@@ -456,9 +457,10 @@ def step_bump(step, seed=None):
 
 
 def attn_decode(q, k, v, out, q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld, batch, heads, tk, key_len=None,
-                t_ptr=None, scale=0.125):
+                t_ptr=None, scale=0.125, stop_len=None, step=None):
     """One query row per batch element over a key cache (see tt2_attn_decode_args)."""
     a = _lib.AttnDecodeArgs()
+    a.stop_len, a.step = ptr(stop_len), ptr(step)
     a.q, a.k, a.v, a.out = q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
     a.q_ld, a.k_bstride, a.k_ld, a.v_bstride, a.v_ld, a.o_ld = q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld
     a.key_len, a.t_ptr = ptr(key_len), ptr(t_ptr)
@@ -471,7 +473,8 @@ def kv_append(src, src_ld, cache, c_bstride, c_ld, n, batch, t_ptr):
                               dt(src), stream_ptr()), "tt2_kv_append")
 
 
-def decode_emit(heads, heads_ld, batch, n_mels, t_max, mel_seq, stop_seq, prev, t_ptr, seed=None):
+def decode_emit(heads, heads_ld, batch, n_mels, t_max, mel_seq, stop_seq, prev, t_ptr, seed=None, stop_bias=None,
+                stop_len=None, stop_thr=float("inf")):
     check(lib().tt2_decode_emit(heads.data_ptr(), heads_ld, batch, n_mels, t_max, mel_seq.data_ptr(),
                                 stop_seq.data_ptr(), prev.data_ptr(), dt(prev), t_ptr.data_ptr(), ptr(seed),
-                                stream_ptr()), "tt2_decode_emit")
+                                ptr(stop_bias), ptr(stop_len), stop_thr, stream_ptr()), "tt2_decode_emit")
