@@ -77,6 +77,7 @@ class Arena:
 
     def __init__(self, c: TTSConfig, B: int, Tx: int, Ty: int, cd: torch.dtype, dev):
         self.B, self.Tx, self.Ty = B, Tx, Ty
+        self.gen = 0   # forward count (the autograd boundary checks its saved arena is intact)
         d, F, H = c.d_model, c.d_ffn, c.n_heads
         Me, Md = B * Tx, B * Ty
         self.Me, self.Md = Me, Md

@@ -1,20 +1,37 @@
 """TransformerTTS -- the drop-in model API of SURVEY 8(b) on the MI355X engine.
 
+A reference-shaped training script works unchanged (torch.nn.Module + autograd):
+
     model = TransformerTTS(cfg, dtype=torch.bfloat16)
     model.load_state_dict(sd)                      # SURVEY 8(b) checkpoint layout
-    mel_before, mel_after, stop_logits, _ = model(text, text_len, mel, mel_len)
-    total, parts = model.loss(outputs, mel, mel_len)
-    model.backward()                               # grads -> model.grads_state_dict()
-    model.train_step(text, text_len, mel, mel_len) # fwd + loss + bwd + Adam
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    out = model(text, text_len, mel, mel_len)      # (mel_before, mel_after, stop_logits, None)
+    total, parts = model.loss(out, mel, mel_len)   # honours its arguments
+    opt.zero_grad(); total.backward(); opt.step()
+
+and so does the engine's own fused fast path (no autograd, one hipGraph per step):
+
+    model.train_step(text, text_len, mel, mel_len) # fwd + loss + bwd + fused Adam/clip/Noam
+    model.loss(); model.backward()                 # loss / grads of the last forward
 
 Every compute step runs in libtt2's gfx950 kernels; there is no CPU or
-PyTorch-op fallback (a missing library or GPU raises).
+PyTorch-op fallback (a missing library or GPU raises).  The autograd boundary is two
+torch.autograd.Functions: the whole forward (its backward is the engine's hand-written
+backward, which writes the flat gradient buffer) and the fused loss kernel.
+
+parameters() are views of the engine's flat f32 master buffer in the INTERNAL layout
+(conv weights [Cout][tap][Cin], the six cross-attention K/V projections as one slot, mel +
+stop heads as one [81, 512] slot; names ``slots.<slot>``); state_dict() stays in the
+checkpoint layout.  An external optimizer updates the master weights in place; the bf16
+shadow the kernels read is refreshed at the next forward (version-counter check).
 """
 from __future__ import annotations
 
 import math
 
 import torch
+import torch.nn as nn
+from torch.autograd.function import once_differentiable
 
 from . import ops
 from .config import TTSConfig
@@ -22,25 +39,87 @@ from .engine import Arena, TTSEngine
 from .params import from_state_dict, grads_to_state_dict_names, to_state_dict
 
 
-class TransformerTTS:
+class _TTSForward(torch.autograd.Function):
+    """Teacher-forced forward as one autograd node; backward = the engine's backward from
+    the output gradients (it rewrites the flat gradient buffer; a copy is handed to
+    autograd, which accumulates it into each parameter's .grad)."""
+
+    @staticmethod
+    def forward(ctx, model, text, text_len, mel, mel_len, *params):
+        A = model._run_forward(text, text_len, mel, mel_len)
+        ctx.model, ctx.A, ctx.gen = model, A, A.gen
+        return model.outputs(A)[:3]
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g_before, g_after, g_stop):
+        model, A = ctx.model, ctx.A
+        if A.gen != ctx.gen:
+            raise RuntimeError("TransformerTTS: another forward of the same (B, Tx, Ty) shape overwrote the "
+                               "activations this backward needs; call backward before the next forward")
+        model._stage_output_grads(A, g_before, g_after, g_stop)
+        e = model.engine
+        e.backward(A)
+        if e.training:   # fresh dropout masks for the next step (the fused path bumps in its optimizer)
+            ops.step_bump(model._seed_steps, e.seed)
+        flat = e.grads.clone()
+        return (None,) * 5 + tuple(e.lay.view(flat, n) for n in model._slot_names)
+
+
+class _TTSLoss(torch.autograd.Function):
+    """The fused loss kernel (masked MSE x 2 + BCE(pos_weight)) on the GIVEN outputs and
+    targets; it writes d(total)/d(outputs) alongside the loss, backward scales them."""
+
+    @staticmethod
+    def forward(ctx, model, mel_before, mel_after, stop, mel, mel_len):
+        L, gb, ga, gs = model._run_loss(mel_before, mel_after, stop, mel, mel_len)
+        ctx.save_for_backward(gb, ga, gs)
+        parts = (L[1].clone(), L[2].clone(), L[3].clone())
+        ctx.mark_non_differentiable(*parts)
+        return (L[0].clone(),) + parts
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, g_total, *_):
+        gb, ga, gs = ctx.saved_tensors
+        return None, gb * g_total, ga * g_total, gs * g_total, None, None
+
+
+class TransformerTTS(nn.Module):
     def __init__(self, cfg: TTSConfig | None = None, dtype: torch.dtype = torch.bfloat16, device="cuda",
                  seed: int = 0):
+        super().__init__()
         self.cfg = cfg or TTSConfig()
-        self.engine = TTSEngine(self.cfg, dtype, device, seed)
+        self.engine = e = TTSEngine(self.cfg, dtype, device, seed)
         self._last: Arena | None = None
         self._graphs: dict = {}
+        self._loss_bufs: dict = {}
+        self._slot_names = list(e.lay.slots)
+        # parameters alias the flat master buffer (in-place optimizer updates land in it)
+        self.slots = nn.ParameterDict({n.replace(".", "__"): nn.Parameter(e.P(n)) for n in self._slot_names})
+        # the autograd Function's inputs and returned gradients follow the ParameterDict's order
+        key2slot = {n.replace(".", "__"): n for n in self._slot_names}
+        self._slot_names = [key2slot[k] for k in self.slots.keys()]
+        self._shadow_version = e.params._version
+        self._seed_steps = torch.zeros(1, dtype=torch.int32, device=e.dev)
+
+    def _apply(self, fn, recurse=True):
+        raise NotImplementedError("TransformerTTS parameters live in libtt2's flat buffers: choose device and "
+                                  "dtype at construction (TransformerTTS(cfg, dtype=..., device=...))")
 
     # ------------------------------------------------------------ modes
     def train(self, mode: bool = True):
+        super().train(mode)
         self.engine.training = mode
         return self
 
-    def eval(self):
-        return self.train(False)
-
-    @property
-    def training(self) -> bool:
-        return self.engine.training
+    def _sync_shadow(self):
+        """Refresh the bf16 weight shadow after an in-place update of the master weights
+        from outside the engine (an external optimizer, load, manual edits)."""
+        e = self.engine
+        if e.params._version != self._shadow_version:
+            e.sync_shadow()
+            self._shadow_version = e.params._version
 
     def set_seed(self, seed: int):
         """Per-step dropout seed (uint32), same meaning as the oracle's set_seed."""
@@ -51,9 +130,10 @@ class TransformerTTS:
         e = self.engine
         return to_state_dict(self.cfg, e.lay, e.params, e.slay, e.stats, e.nbt)
 
-    def load_state_dict(self, sd):
+    def load_state_dict(self, sd, strict: bool = True):
         P, S, nbt = from_state_dict(self.cfg, sd)
         self.engine.load_slots(P, S, nbt)
+        self._shadow_version = self.engine.params._version
 
     def save_checkpoint(self, path: str):
         """Training checkpoint: the SURVEY 8(b) state_dict, the Adam
@@ -111,15 +191,63 @@ class TransformerTTS:
                                  mel_len.to(dev, torch.int32))
         return A
 
-    def forward(self, text, text_len, mel, mel_len):
-        """Teacher-forced forward (shift-right with a zero go frame).  Returns
-        (mel_before [B,Ty,80], mel_after [B,Ty,80], stop_logits [B,Ty], None), f32."""
+    def _run_forward(self, text, text_len, mel, mel_len) -> Arena:
+        self._sync_shadow()
         A = self._stage(text, text_len, mel, mel_len)
+        A.gen += 1
         self.engine.forward(A)
         self._last = A
-        return self.outputs(A)
+        return A
 
-    __call__ = forward
+    def forward(self, text, text_len, mel, mel_len):
+        """Teacher-forced forward (shift-right with a zero go frame).  Returns
+        (mel_before [B,Ty,80], mel_after [B,Ty,80], stop_logits [B,Ty], None), f32.
+        With grad mode on, the outputs carry an autograd node whose backward runs the
+        engine's backward (so loss.backward() fills every parameter's .grad)."""
+        params = list(self.slots.values())
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            mb, ma, st = _TTSForward.apply(self, text, text_len, mel, mel_len, *params)
+            return mb, ma, st, None
+        return self.outputs(self._run_forward(text, text_len, mel, mel_len))
+
+    def _stage_output_grads(self, A: Arena, g_before, g_after, g_stop):
+        """d(loss)/d(outputs) -> the engine's backward inputs: g_heads (f32 [Md, 96]: mel
+        columns = d/d(mel_before) + d/d(mel_after), the post-net's residual path; column 80 =
+        d/d(stop)) and g_after (the post-net output gradient)."""
+        c = self.cfg
+        Md = A.Md
+        gh = A["g_heads"]
+        z = lambda: torch.zeros(Md, c.n_mels, device=gh.device)  # noqa: E731
+        gb = z() if g_before is None else g_before.reshape(Md, c.n_mels).float()
+        ga = z() if g_after is None else g_after.reshape(Md, c.n_mels).float()
+        gh[:, :c.n_mels].copy_(gb + ga)
+        gh[:, c.n_mels].copy_(torch.zeros(Md, device=gh.device) if g_stop is None else g_stop.reshape(Md))
+        A["g_after"].copy_(ga)
+
+    def _run_loss(self, mel_before, mel_after, stop, mel, mel_len):
+        """Loss kernel over the given tensors (staged into per-shape buffers); returns the
+        loss vector and d(total)/d(mel_before, mel_after, stop)."""
+        c, e = self.cfg, self.engine
+        B, Ty = mel.shape[0], mel.shape[1]
+        key = (B, Ty)
+        S = self._loss_bufs.get(key)
+        if S is None:
+            f = lambda *sh: torch.zeros(*sh, dtype=torch.float32, device=e.dev)  # noqa: E731
+            S = self._loss_bufs[key] = dict(heads=f(B * Ty, 96), after=f(B * Ty, c.n_mels), mel=f(B, Ty, c.n_mels),
+                                            mel_len=torch.zeros(B, dtype=torch.int32, device=e.dev), loss=f(4),
+                                            g_heads=f(B * Ty, 96), g_after=f(B * Ty, c.n_mels))
+        Md = B * Ty
+        S["heads"][:, :c.n_mels].copy_(mel_before.detach().reshape(Md, c.n_mels))
+        S["heads"][:, c.n_mels].copy_(stop.detach().reshape(Md))
+        S["after"].copy_(mel_after.detach().reshape(Md, c.n_mels))
+        S["mel"].copy_(mel)
+        S["mel_len"].copy_(mel_len)
+        ops.tts_loss(S["heads"], 96, S["after"], S["mel"], S["mel_len"], S["loss"], S["g_heads"], S["g_after"], B,
+                     Ty, c.n_mels, c.stop_pos_weight, 1.0, ws=e.ws, separate_grads=True)
+        gb = S["g_heads"][:, :c.n_mels].reshape(B, Ty, c.n_mels).clone()
+        gs = S["g_heads"][:, c.n_mels].reshape(B, Ty).clone()
+        ga = S["g_after"].reshape(B, Ty, c.n_mels).clone()
+        return S["loss"], gb, ga, gs
 
     def outputs(self, A: Arena):
         c = self.cfg
@@ -131,8 +259,18 @@ class TransformerTTS:
         return mel_before, mel_after, stop, None
 
     def loss(self, outputs=None, mel=None, mel_len=None):
-        """Loss of the last forward (targets are the mel it was given); returns
-        (total, {"mel_before", "mel_after", "stop"}) as device scalars."""
+        """loss(outputs, mel, mel_len): the TTS loss of the given outputs (mel_before,
+        mel_after, stop_logits, ...) against mel / mel_len, differentiable w.r.t. the outputs.
+        loss() with no outputs: the engine fast path -- the loss of the last forward against
+        the mel it was given (or mel / mel_len if passed), feeding backward().
+        Returns (total, {"mel_before", "mel_after", "stop"}) as device scalars."""
+        if outputs is not None:
+            if mel is None or mel_len is None:
+                raise ValueError("loss(outputs, mel, mel_len): mel and mel_len are required with outputs")
+            dev = self.engine.dev
+            total, lb, la, ls = _TTSLoss.apply(self, outputs[0], outputs[1], outputs[2],
+                                               mel.to(dev, torch.float32), mel_len.to(dev, torch.int32))
+            return total, {"mel_before": lb, "mel_after": la, "stop": ls}
         A = self._last
         if A is None:
             raise RuntimeError("loss() needs a forward() first")
@@ -156,6 +294,7 @@ class TransformerTTS:
         cross K/V).  Returns (mel_after [B, T, 80] f32, out_len [B]).
         stop_threshold=None forces max_len frames."""
         from .infer import Decoder
+        self._sync_shadow()
         B, Tx = text.shape
         key = (B, Tx, max_len, prenet_dropout)
         dec = self._decoders.get(key) if hasattr(self, "_decoders") else None
@@ -211,6 +350,7 @@ class TransformerTTS:
         [total, mse_before, mse_after, bce_stop] (no host sync)."""
         if self.engine.exp_avg is None:
             self.engine.init_optimizer()
+        self._sync_shadow()
         A = self._stage(text, text_len, mel, mel_len)
         self._step_body(A, sync_grads)
         self._last = A
