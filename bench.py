@@ -223,11 +223,14 @@ def roofline(model, text, tl, mel, ml):
     finally:
         ops.PROBE = None
         eng.grad_ready_hook = hook
+        if hasattr(probe, "close"):
+            probe.close()
     # dominant = the GEMM variant with the most device time
     key, (n, flops, secs, abytes) = max(summ.items(), key=lambda kv: kv[1][2])
-    # achieved uses the in-step durations (HIP events around each launch inside the step, so
-    # cache state and neighbours are the step's own); a back-to-back replay of the same
-    # launches (warm caches) is reported beside it for reference only
+    # achieved uses the in-step kernel durations (libtt2's launch probe: start / stop events
+    # recorded by the kernel dispatch itself, inside an eager step, so cache state and
+    # neighbours are the step's own); a back-to-back replay of the same launches (warm
+    # caches) is reported beside it for reference only
     replay = probe.replay_time(key)
     tot_t = sum(v[2] for v in summ.values())
     tot_f = sum(v[1] for v in summ.values())
@@ -254,7 +257,7 @@ def roofline(model, text, tl, mel, ml):
         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_source": tsrc,
         "mfma_busy_under_profiler": busy, "mfma_busy_source": bsrc,
         "algo_bytes_per_launch": round(abytes / n), "launches_per_step": n, "flops_per_launch": flops / n,
-        "avg_launch_us": round(secs / n * 1e6, 2), "timing": "in-step HIP events around each launch",
+        "avg_launch_us": round(secs / n * 1e6, 2), "timing": "in-step kernel dispatch events (tt2_probe_arm)",
         "replay_avg_launch_us": round(replay / n * 1e6, 2),
         "all_gemms": {"launches": sum(v[0] for v in summ.values()), "ms_per_step": round(tot_t * 1e3, 3),
                       "tflops": round(tot_f / tot_t / 1e12, 1)},

@@ -135,6 +135,15 @@ int tt2_gemm_plan(const tt2_gemm_args* a);
  * weight-gradient calls of the reference's autograd backward (see tt2_gemm). */
 int tt2_gemm_grouped(const tt2_gemm_args* probs, int32_t n, hipStream_t stream);
 
+/* Measurement probe (bench.py's live roofline): tt2_probe_arm() makes the next main GEMM
+ * kernel (v7 / grouped v7 / LDS-DMA 128x128) launched on this thread record its own
+ * start / stop timestamps (the kernel's execution, as rocprofv3 reports it) and returns the
+ * slot; tt2_probe_ms(slot) waits for it and returns the duration in ms (-1 if the armed
+ * launch did not happen); tt2_probe_reset() frees every slot. */
+int tt2_probe_arm(void);
+float tt2_probe_ms(int slot);
+void tt2_probe_reset(void);
+
 /* ---------------------------------------------------------------- attention
  * Scaled dot-product attention over heads of width 64, read in place from
  * projection outputs: head h of row (b, t) of Q is q[(b*tq + t)*q_ld + 64h].

@@ -27,6 +27,12 @@ int main(int argc, char** argv) {
   g.trans_a = ta; g.trans_b = tb; g.dtype_in = TT2_BF16; g.dtype_out = ta ? TT2_F32 : TT2_BF16;
   g.alpha = 1.f; g.gate_scale = 1.f; g.splits = sp; g.kernel_variant = var; g.main_only = 1;
   if (sp > 1) { g.ws_bytes = tt2_gemm_workspace_size(&g); hipMalloc(&W, g.ws_bytes); g.workspace = W; }
+  if (getenv("TT2_BIAS")) {   // the forward linears' epilogue (bias prefetched before the K loop)
+    float* bias = nullptr;
+    hipMalloc(&bias, (size_t)n * 4);
+    hipMemset(bias, 0, (size_t)n * 4);
+    g.bias = bias;
+  }
   for (int i = 0; i < 5; ++i)
     if (tt2_gemm(&g, 0) != TT2_OK) { fprintf(stderr, "gemm: %s\n", tt2_last_error()); return 1; }
   hipDeviceSynchronize();

@@ -20,13 +20,35 @@
 // Split-K (gridDim.z > 1) writes raw f32 partial slabs to the workspace and a
 // second kernel (gemm_splitk_reduce) sums them in a fixed order (bitwise
 // reproducible) and applies the epilogue.
+#include <hip/hip_ext.h>
+
 #include <algorithm>
+#include <vector>
 
 #include "tt2_common.h"
 #include "tt2_capi.h"
 #include "tt2_internal.h"
 
 namespace {
+
+// Launch probe (measurement): when armed, the next main GEMM kernel launched on this
+// thread records a start / stop event pair at its own dispatch and completion
+// (hipExtLaunchKernelGGL), i.e. the kernel's execution time as rocprofv3 reports it,
+// without the gaps an event recorded around the launch on the stream adds.
+struct ProbeSlot { hipEvent_t start, stop; bool used; };
+thread_local std::vector<ProbeSlot> g_probe;
+thread_local int g_probe_armed = -1;
+
+bool probe_take(hipEvent_t& e0, hipEvent_t& e1) {
+  if (g_probe_armed < 0) return false;
+  ProbeSlot& p = g_probe[g_probe_armed];
+  e0 = p.start;
+  e1 = p.stop;
+  p.used = true;
+  g_probe_armed = -1;
+  return true;
+}
+
 
 constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
 
@@ -835,7 +857,12 @@ hipError_t launch2(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   }
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
   dim3 grid(ntm * ntn, splits);
-  hipLaunchKernelGGL((gemm2_kernel<AK, BKC>), grid, dim3(NT), 0, s, A, B, E, M, N, K, k_split,
+  hipEvent_t e0, e1;
+  if (probe_take(e0, e1))
+    hipExtLaunchKernelGGL((gemm2_kernel<AK, BKC>), grid, dim3(NT), 0, s, e0, e1, 0, A, B, E, M, N, K, k_split,
+                     splits > 1 ? ws : nullptr, ntm, ntn);
+  else
+    hipLaunchKernelGGL((gemm2_kernel<AK, BKC>), grid, dim3(NT), 0, s, A, B, E, M, N, K, k_split,
                      splits > 1 ? ws : nullptr, ntm, ntn);
   if (splits > 1 && !E.main_only) {
     const int64_t total = (int64_t)M * N;
@@ -1474,7 +1501,11 @@ template <bool AK, bool BKC>
 hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
                    hipStream_t s) {
   const G7Prob P = g7_prob(A, B, E, M, N, K, splits, ws);
-  hipLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, P);
+  hipEvent_t e0, e1;
+  if (probe_take(e0, e1))
+    hipExtLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, e0, e1, 0, P);
+  else
+    hipLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, P);
   if (P.splits > 1 && !E.main_only) {
     const int64_t total = (int64_t)M * N;
     int64_t nb = (total + 255) / 256;
@@ -1704,11 +1735,46 @@ extern "C" int tt2_gemm_grouped(const tt2_gemm_args* probs, int n, hipStream_t s
     }
   }
   if (G.np == 0) return TT2_OK;
-  if (!ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<true, true>), dim3(G.items), dim3(G7_NT), 0, stream, G);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (probe_take(e0, e1)) {
+#define TT2_G7G(A_, B_) hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_>), dim3(G.items), dim3(G7_NT), 0, stream, e0, e1, 0, G)
+    if (!ta && !tb) TT2_G7G(true, true);
+    else if (!ta && tb) TT2_G7G(true, false);
+    else if (ta && !tb) TT2_G7G(false, true);
+    else TT2_G7G(false, false);
+#undef TT2_G7G
+  } else if (!ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<true, true>), dim3(G.items), dim3(G7_NT), 0, stream, G);
   else if (!ta && tb) hipLaunchKernelGGL((gemm7g_kernel<true, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
   else if (ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<false, true>), dim3(G.items), dim3(G7_NT), 0, stream, G);
   else hipLaunchKernelGGL((gemm7g_kernel<false, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
   if (reduce_blocks > 0 && !main_only)
     hipLaunchKernelGGL(gemm_splitk_reduce_g, dim3(reduce_blocks, G.np), dim3(256), 0, stream, G);
   return tt2_check_launch(hipGetLastError(), "tt2_gemm_grouped");
+}
+
+extern "C" int tt2_probe_arm(void) {
+  ProbeSlot p{nullptr, nullptr, false};
+  hipError_t e = hipEventCreate(&p.start);
+  if (e == hipSuccess) e = hipEventCreate(&p.stop);
+  if (e != hipSuccess) return tt2_check_launch(e, "tt2_probe_arm");
+  g_probe.push_back(p);
+  g_probe_armed = (int)g_probe.size() - 1;
+  return g_probe_armed;
+}
+
+extern "C" float tt2_probe_ms(int slot) {
+  if (slot < 0 || slot >= (int)g_probe.size() || !g_probe[slot].used) return -1.f;
+  float ms = -1.f;
+  if (hipEventSynchronize(g_probe[slot].stop) != hipSuccess) return -1.f;
+  if (hipEventElapsedTime(&ms, g_probe[slot].start, g_probe[slot].stop) != hipSuccess) return -1.f;
+  return ms;
+}
+
+extern "C" void tt2_probe_reset(void) {
+  for (ProbeSlot& p : g_probe) {
+    (void)hipEventDestroy(p.start);
+    (void)hipEventDestroy(p.stop);
+  }
+  g_probe.clear();
+  g_probe_armed = -1;
 }

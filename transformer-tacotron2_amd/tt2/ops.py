@@ -167,20 +167,22 @@ def gemm_grouped(problems, ws: Workspace | None = None):
 
 
 class LaunchProbe:
-    """Brackets each GEMM launch with HIP events on the launching (current)
-    stream; used by bench.py for the live per-kernel roofline figure."""
+    """Times each GEMM's main kernel inside the step with libtt2's launch probe
+    (tt2_probe_arm: the kernel records start / stop events at its own dispatch and
+    completion, as rocprofv3 measures it); used by bench.py for the live per-kernel
+    roofline figure."""
 
     def __init__(self):
         self.rec = []
         self._s = None
 
     def begin(self):
-        self._s = torch.cuda.Event(enable_timing=True)
-        self._s.record()
+        self._s = lib().tt2_probe_arm()
+        if self._s < 0:
+            check(self._s, "tt2_probe_arm")
 
     def end(self, key, flops, algo_bytes=0, args=None):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
+        e = None
         saved = None
         if args is not None:   # a copy of the launch's tt2_gemm_args (array for a grouped launch)
             saved = (GemmArgs * len(args))()
@@ -191,13 +193,20 @@ class LaunchProbe:
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for key, flops, s, e, ab, _ in self.rec:
+        L = lib()
+        for key, flops, slot, _, ab, _ in self.rec:
+            ms = L.tt2_probe_ms(slot)
+            if ms < 0:
+                raise _lib.TT2Error(f"launch probe {slot} ({key}) recorded no kernel")
             d = out.setdefault(key, [0, 0.0, 0.0, 0.0])
             d[0] += 1
             d[1] += flops
-            d[2] += s.elapsed_time(e) * 1e-3
+            d[2] += ms * 1e-3
             d[3] += ab
         return out
+
+    def close(self):
+        lib().tt2_probe_reset()
 
     def replay_time(self, key, reps: int = 10) -> float:
         """Total device time of this variant's recorded launches, each re-launched
