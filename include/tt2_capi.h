@@ -191,6 +191,13 @@ typedef struct tt2_attn_decode_args {
    * *step >= stop_len[b] (step defaults to t_ptr); its output row is 0 and no key is read */
   const int32_t* stop_len;
   const int32_t* step;
+  /* optional fused output projection (wo != NULL): the workgroup of (b, h) also writes
+   * slab[(h * batch + b) * heads * head_dim + n] = sum_j o[b, h, j] * wo[n * wo_ld + h * head_dim + j]
+   * (f32, n < heads * head_dim): one split-K slab per head for tt2_ln_combine (splits = heads),
+   * which adds the bias; out may then be NULL */
+  const void* wo;
+  int64_t wo_ld;
+  float* slab;
 } tt2_attn_decode_args;
 int tt2_attn_decode(const tt2_attn_decode_args* a, hipStream_t stream);
 /* cache[b*c_bstride + (*t_ptr)*c_ld + c] = src[b*src_ld + c], c < n */
@@ -237,7 +244,8 @@ typedef struct tt2_dec_layer {
 typedef struct tt2_decode_desc {
   int32_t batch, text_len, t_max, n_layers, d_model, n_heads, d_ffn, n_mels, prenet_dim;
   int32_t dtype;        /* step storage type: TT2_DT_BF16, TT2_DT_F16 (batch <= 64) or TT2_DT_F32 */
-  int32_t schedule;     /* 0 auto, 1 plain (one launch per op), 2 split-K (16-bit, batch <= 64) */
+  int32_t schedule;     /* 0 auto, 1 plain (one launch per op), 2 split-K (16-bit, batch <= 64; output
+                         * projections fused into the attention launches), 3 split-K without that fusion */
   float ln_eps;
   float prenet_dropout; /* 0 = off (Tacotron2 keeps it on at inference) */
   float stop_logit;     /* logit(stop_threshold); +inf never stops */

@@ -168,6 +168,33 @@ def test_attn_decode_cross_ragged():
     assert out[2].float().abs().sum().item() == 0   # no keys -> zeros, never NaN
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_attn_decode_fused_oproj(dtype):
+    """The output projection fused into the decode attention launch: one f32 slab per
+    head, slab[h, b] = o[b, h] W_o[:, h]^T; the sum over heads is o W_o^T (float64 ref).
+    A finished utterance (stop_len) writes zero slabs."""
+    g = torch.Generator().manual_seed(11)
+    B, H, d, Tm, t = 6, 8, 512, 300, 140
+    mk = (lambda sh: _bf(sh, g)) if dtype == torch.bfloat16 else (lambda sh: _h(sh, g))
+    qkv, cache = mk((B, 3 * d)), mk((B, Tm, 2 * d))
+    wo = (torch.randn(d, d, generator=g) / math.sqrt(d)).to(dtype).cuda()
+    tp = torch.tensor([t], dtype=torch.int32, device="cuda")
+    stop = torch.tensor([1000, 1000, 50, 1000, 141, 1000], dtype=torch.int32, device="cuda")
+    out = torch.empty(B, d, dtype=dtype, device="cuda")
+    slab = torch.full((H, B, d), float("nan"), device="cuda")
+    args = (qkv, cache, cache[:, :, d:], None, 3 * d, Tm * 2 * d, 2 * d, Tm * 2 * d, 2 * d, d, B, H, Tm)
+    ops.attn_decode(*args, t_ptr=tp, scale=0.125, stop_len=stop, wo=wo, wo_ld=d, slab=slab)
+    ref_o = _attn_ref(qkv[:, :d], cache[:, :, :d], cache[:, :, d:], [t + 1] * B, 0.125)
+    done = (stop.cpu() <= t)
+    ref_o[done] = 0.0
+    w = wo.double().cpu()
+    ref = torch.stack([ref_o[:, h * 64:(h + 1) * 64] @ w[:, h * 64:(h + 1) * 64].t() for h in range(H)])
+    assert torch.isfinite(slab).all()
+    assert rel(slab, ref) < 1e-2
+    assert slab[:, 2].abs().sum().item() == 0
+    assert rel(slab.sum(0), ref_o @ w.t()) < 1e-2
+
+
 def _h(shape, gen, scale=1.0):
     return (torch.randn(shape, generator=gen) * scale).half().cuda()
 

@@ -21,7 +21,7 @@ DB = int(os.environ.get("DEC_B", bench.DEC_B))        # DEC_B=64 DEC_DT=f16: the
 DDT = torch.float16 if os.environ.get("DEC_DT") == "f16" else None
 text = torch.randint(1, 80, (DB, bench.TX), generator=g).cuda()
 tl = torch.full((DB,), bench.TX, dtype=torch.int32, device="cuda")
-for sched in (SCHEDULE_SPLIT, SCHEDULE_PLAIN) * 2:
+for sched in ((SCHEDULE_SPLIT, 3) if DDT is not None else (SCHEDULE_SPLIT, 3, SCHEDULE_PLAIN)) * 2:
     dec = Decoder(model.engine, DB, bench.TX, bench.DEC_T, dtype=DDT, schedule=sched)
     dec.encode(text, tl)
     dec.capture(None)

@@ -38,7 +38,7 @@ int main(int argc, char** argv) {
   hipDeviceSynchronize();
   std::vector<unsigned long long> st(4096 * 64 * 4);
   hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_st), st.size() * 8);
-  const int bm = var >= 11 && var <= 13 ? 256 : 128, bn = var == 11 ? 256 : 128;  // v7 (13): 256 x 128
+  const int bm = var >= 11 && var <= 14 ? 256 : 128, bn = var == 11 ? 256 : 128;  // v7 (13/14): 256 x 128
   int k_split = k, splits = 1;
   if (sp > 1) { k_split = ((k + sp - 1) / sp + 63) / 64 * 64; splits = (k + k_split - 1) / k_split; }
   const int nwg = ((m + bm - 1) / bm) * ((n + bn - 1) / bn) * splits;
@@ -51,7 +51,7 @@ int main(int argc, char** argv) {
     for (int t = 0; t < steps; ++t) {
       const unsigned long long* r = s + t * 4;
       const unsigned long long next = s[(t + 1) * 4];
-      if (var == 13) {   // v7 MFMA wave 0: [0] step start, [1] after the step's MFMAs
+      if (var == 13 || var == 14) {   // v7 MFMA wave 0: [0] step start, [1] after the step's MFMAs
         c += (double)(r[1] - r[0]); w += (double)(next - r[1]);
       } else {
         w += (double)(r[1] - r[0]); is += (double)(r[2] - r[1]); c += (double)(next - r[2]);
@@ -62,6 +62,22 @@ int main(int argc, char** argv) {
     tot += (double)(s[steps * 4 + 3] - s[0]);
     t0min = std::min(t0min, s[0]); t0max = std::max(t0max, s[0]); tend = std::max(tend, s[steps * 4 + 3]);
   }
+  // chip-wide timeline (s_memrealtime, 100 MHz) and one launch's event time
+  unsigned long long rs = ~0ull, rs_max = 0, re_max = 0;
+  for (int b = 0; b < nwg && b < 4096; ++b) {
+    const unsigned long long* s = &st[(size_t)b * 64 * 4 + 63 * 4];
+    rs = std::min(rs, s[0]); rs_max = std::max(rs_max, s[0]); re_max = std::max(re_max, s[1]);
+  }
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  hipEventRecord(e0, 0);
+  for (int i = 0; i < 20; ++i) tt2_gemm(&g, 0);
+  hipEventRecord(e1, 0);
+  hipEventSynchronize(e1);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, e0, e1);
+  printf("  realtime: WG start spread %.2f us, first start -> last exit %.2f us; back-to-back launch %.2f us\n",
+         (rs_max - rs) / 100.0, (re_max - rs) / 100.0, ms * 1e3 / 20);
   printf("%dx%dx%d ta%d tb%d v%d sp%d: %d WGs x %d steps | per step: wait %.0f issue %.0f comp %.0f cyc | "
          "epilogue %.0f | WG total %.0f | start spread %llu | span %llu cyc\n",
          m, n, k, ta, tb, var, sp, nwg, nkt, w / cnt, is / cnt, c / cnt, epi / nwg, tot / nwg, t0max - t0min,

@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU-box pass (run via gpurun from the repo root): GPU tests, smoke, bench, rocprof
+# kernel-trace stats of the bench step.  Every GPU step has its own time limit; the
+# steps are chained so that the first failure ends the call.
+#   tools/gpu_round.sh <tag> [tests|bench|prof ...]   (default: all three)
+set -euo pipefail
+TAG=${1:-r02}
+shift || true
+STEPS=${*:-tests bench prof}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        > "$OUT/gpu_tests.log" 2>&1
+      timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+      ;;
+    bench)
+      timeout -k 10 420 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+      ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
+        python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-decode \
+        > "$OUT/bench_kt.json" 2> "$OUT/bench_kt.err"
+      ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+  echo "step $s ok"
+done

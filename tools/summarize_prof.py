@@ -34,6 +34,8 @@ def per_kernel_counter(path, counter):
 
 def main(tag: str):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    if not os.path.isdir(src):  # tools/gpu_round.sh layout
+        src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
     stats = os.path.join(src, "kt", "run_kernel_stats.csv")

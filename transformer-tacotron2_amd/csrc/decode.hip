@@ -48,20 +48,52 @@ struct DecArgs {
   const int32_t* t_ptr;     // self attention: keys = *t_ptr + 1
   const int32_t* stop_len;  // optional [B]: utterance b is finished once *step >= stop_len[b]
   const int32_t* step;
-  int tk, H;
+  int tk, H, B;
   float scale;
+  const void* wo; int64_t wo_ld; float* slab;   // fused output projection (wo != null)
 };
+
+// slab[(h*B + b)*H*64 + n] = sum_j o[j] * Wo[n][h*64 + j] for the H*64 output columns.
+// Eight lanes cover one 128-B row of Wo's head slice (lane & 7 = 16-B chunk), so a wave
+// instruction reads 8 whole rows; every lane issues its 8 row loads before the first FMA;
+// the 8 chunk partials of a row meet by xor shuffles and leave through LDS as one
+// coalesced row of the slab.  o: this lane's 8 elements of the head output (chunk lane & 7).
+template <typename T, int NW>
+TT2_DEV void oproj_slab(const DecArgs& a, int b, int h, const float (&o)[8], float* sres) {
+  const int N = a.H * D, lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 7, g = lane >> 3;
+  for (int r0 = w * 64; r0 < N; r0 += NW * 64) {
+    float wv[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      load8f(reinterpret_cast<const T*>(a.wo) + (int64_t)(r0 + 8 * i + g) * a.wo_ld + h * D + 8 * c, wv[i]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float p = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p += o[j] * wv[i][j];
+      p += __shfl_xor(p, 1, 64);
+      p += __shfl_xor(p, 2, 64);
+      p += __shfl_xor(p, 4, 64);
+      if (c == 0) sres[r0 + 8 * i + g] = p;
+    }
+  }
+  __syncthreads();
+  for (int n = threadIdx.x; n < N; n += NW * 64) a.slab[((int64_t)h * a.B + b) * N + n] = sres[n];
+}
 
 template <typename T, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
   constexpr int U = 4;   // 8-key groups per wave per iteration: 2*U 16-B loads in flight per lane
-  __shared__ float sm[NW], sl[NW], so[NW][D];
+  __shared__ float sm[NW], sl[NW], so[NW][D], sfin[D], sres[512];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
   const int dc = lane & 7, kg = lane >> 3;   // 8-dim chunk, key slot within an 8-key group
   if (a.stop_len && *a.step >= a.stop_len[b]) {
     // a finished utterance: its frames past the stop are discarded, so skip the key stream
-    if (threadIdx.x < D) reinterpret_cast<T*>(a.out)[(int64_t)b * a.o_ld + h * D + threadIdx.x] = from_f32<T>(0.f);
+    if (a.out && threadIdx.x < D)
+      reinterpret_cast<T*>(a.out)[(int64_t)b * a.o_ld + h * D + threadIdx.x] = from_f32<T>(0.f);
+    if (a.wo)
+      for (int n = threadIdx.x; n < a.H * D; n += NW * 64) a.slab[((int64_t)h * a.B + b) * a.H * D + n] = 0.f;
     return;
   }
   float qv[8];
@@ -140,7 +172,16 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
       L += sl[i] * f;
       O += so[i][d] * f;
     }
-    reinterpret_cast<T*>(a.out)[(int64_t)b * a.o_ld + h * D + d] = from_f32<T>(L > 0.f ? O / L : 0.f);
+    const float r = L > 0.f ? O / L : 0.f;
+    if (a.out) reinterpret_cast<T*>(a.out)[(int64_t)b * a.o_ld + h * D + d] = from_f32<T>(r);
+    sfin[d] = r;
+  }
+  if (a.wo) {
+    __syncthreads();
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = sfin[8 * (lane & 7) + j];
+    oproj_slab<T, NW>(a, b, h, o, sres);
   }
 }
 
@@ -198,6 +239,12 @@ extern "C" int tt2_attn_decode(const tt2_attn_decode_args* p, hipStream_t s) {
   a.o_ld = p->o_ld; a.key_len = p->key_len; a.t_ptr = p->t_ptr; a.tk = p->tk; a.H = p->heads; a.scale = p->scale;
   a.stop_len = p->stop_len;
   a.step = p->step ? p->step : p->t_ptr;
+  a.B = p->batch;
+  a.wo = p->wo; a.wo_ld = p->wo_ld; a.slab = p->slab;
+  if (a.wo && (!a.slab || (p->wo_ld * esz) % 16 || p->heads * D > 512))
+    return tt2_set_error(TT2_E_INVALID, "tt2_attn_decode: the fused projection needs slab, a 16-B wo_ld and "
+                                       "heads * head_dim <= 512");
+  if (!a.out && !a.wo) return tt2_set_error(TT2_E_INVALID, "tt2_attn_decode: null out");
   if (a.stop_len && !a.step) return tt2_set_error(TT2_E_INVALID, "tt2_attn_decode: stop_len needs step or t_ptr");
   dim3 g(p->batch * p->heads);
   // 8 waves per (batch, head): each wave takes 1/8 of the keys, 32 keys per iteration

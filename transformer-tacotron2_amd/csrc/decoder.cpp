@@ -72,7 +72,7 @@ Bufs carve(const tt2_decode_desc* d, char* base) {
 bool split_schedule(const tt2_decode_desc* d) {
   const bool half = d->dtype == TT2_DT_BF16 || d->dtype == TT2_DT_F16;
   if (d->schedule == 1) return false;
-  if (d->schedule == 2) return true;
+  if (d->schedule == 2 || d->schedule == 3) return true;
   return half && d->batch <= 64;
 }
 
@@ -127,6 +127,7 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
   const int dt = d->dtype;
   const size_t e = esz_of(dt);
   const bool split = split_schedule(d);
+  const bool fuse_o = split && d->schedule != 3;   // output projections inside the attention launches
   const float scale = 1.f / std::sqrt((float)(D / H));
   const int64_t kvld = (int64_t)d->n_layers * 2 * D;
 
@@ -160,7 +161,7 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
   }
 
   auto attn = [&](const void* q, int64_t q_ld, const void* k, const void* v, int64_t bstride, int64_t ld, int tk,
-                  const int32_t* key_len, const int32_t* t_ptr, void* out) {
+                  const int32_t* key_len, const int32_t* t_ptr, void* out, const void* wo) {
     tt2_attn_decode_args a;
     std::memset(&a, 0, sizeof(a));
     a.q = q; a.k = k; a.v = v; a.out = out;
@@ -168,6 +169,9 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
     a.key_len = key_len; a.t_ptr = t_ptr;
     a.batch = B; a.heads = H; a.head_dim = D / H; a.tk = tk; a.dtype = dt; a.scale = scale;
     a.stop_len = d->stop_len; a.step = d->step;
+    if (wo) {   // split schedule: the output projection rides in the attention launch (one slab per head)
+      a.out = nullptr; a.wo = wo; a.wo_ld = D; a.slab = b.slab;
+    }
     return tt2_attn_decode(&a, s);
   };
   // raw split-K partial slabs of x[B, k] W[n, k]^T (no epilogue; tt2_ln_combine folds them)
@@ -201,10 +205,12 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
       TT2_TRY(tt2_gemm(&g, s));
       if (!split) TT2_TRY(tt2_kv_append(b.qkv + D * e, 3 * D, cache, cb, 2 * D, 2 * D, B, d->step, dt, s));
     }
-    TT2_TRY(attn(b.qkv, 3 * D, cache, cache + D * e, cb, 2 * D, d->t_max, nullptr, d->step, b.att));
+    TT2_TRY(attn(b.qkv, 3 * D, cache, cache + D * e, cb, 2 * D, d->t_max, nullptr, d->step, b.att,
+                 fuse_o ? L.o_w : nullptr));
     if (split) {
-      TT2_TRY(slabs(b.att, L.o_w, D, D, SPLIT_O));
-      TT2_TRY(tt2_ln_combine(x, b.slab, SPLIT_O, L.o_b, L.ln1_g, L.ln1_b, b.h1, B, D, d->ln_eps, dt, s));
+      if (!fuse_o) TT2_TRY(slabs(b.att, L.o_w, D, D, SPLIT_O));
+      TT2_TRY(tt2_ln_combine(x, b.slab, fuse_o ? H : SPLIT_O, L.o_b, L.ln1_g, L.ln1_b, b.h1, B, D, d->ln_eps, dt,
+                             s));
     } else {
       tt2_gemm_args g = lin(b.att, L.o_w, b.o, B, D, D, L.o_b, dt, dt);
       TT2_TRY(tt2_gemm(&g, s));
@@ -217,10 +223,11 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
     }
     const char* mk = mkv + (size_t)2 * D * l * e;
     TT2_TRY(attn(b.cq, D, mk, mk + D * e, (int64_t)d->text_len * kvld, kvld, d->text_len, d->text_lens, nullptr,
-                 b.catt));
+                 b.catt, fuse_o ? L.co_w : nullptr));
     if (split) {
-      TT2_TRY(slabs(b.catt, L.co_w, D, D, SPLIT_O));
-      TT2_TRY(tt2_ln_combine(b.h1, b.slab, SPLIT_O, L.co_b, L.ln2_g, L.ln2_b, b.h2, B, D, d->ln_eps, dt, s));
+      if (!fuse_o) TT2_TRY(slabs(b.catt, L.co_w, D, D, SPLIT_O));
+      TT2_TRY(tt2_ln_combine(b.h1, b.slab, fuse_o ? H : SPLIT_O, L.co_b, L.ln2_g, L.ln2_b, b.h2, B, D, d->ln_eps,
+                             dt, s));
     } else {
       tt2_gemm_args g = lin(b.catt, L.co_w, b.co, B, D, D, L.co_b, dt, dt);
       TT2_TRY(tt2_gemm(&g, s));

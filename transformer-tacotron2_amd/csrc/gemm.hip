@@ -23,6 +23,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "tt2_common.h"
@@ -357,45 +358,53 @@ TT2_DEV void ld8_any(const void* p, int64_t off, int dt, float (&o)[8]) {
 // aligned chunks (E.vec) take 16-B loads/stores with every option tested once
 // per chunk; edge chunks fall back to the per-element path.
 // pre_b: alpha and bias were already applied to v (v7's prefetched bias; E.vec, full chunk)
+// Vectorised chunk epilogue without the store: o = epi(v) for a full, aligned chunk (E.vec).
+TT2_DEV void epi_calc8(const EpiParams& E, uint32_t seed, int m, int n0, const float (&v)[8], bool pre_b,
+                       float (&o)[8]) {
+  const int64_t off = (int64_t)m * E.ldc + n0;
+  float t[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = pre_b ? v[j] : v[j] * E.alpha;
+  if (E.bias && !pre_b) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(E.bias + n0), b = *reinterpret_cast<const f32x4*>(E.bias + n0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o[j] += a[j]; o[4 + j] += b[j]; }
+  }
+  if (E.res) {
+    ld8_any(E.res, (int64_t)m * E.ldr + n0, E.res_dt, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] += t[j];
+  }
+  if (E.act == ACT_RELU) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
+  } else if (E.act == ACT_TANH) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = tanhf(o[j]);
+  }
+  if (E.gate) {
+    ld8_any(E.gate, (int64_t)m * E.ldg + n0, E.gate_dt, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = t[j] != 0.f ? o[j] * E.gate_scale : 0.f;
+  }
+  if (E.drop.thr) {
+    const uint32_t base = (uint32_t)((int64_t)m * E.n_log + n0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = drop_apply(E.drop, seed, base + j, o[j]);
+  }
+  if (E.beta != 0.f) {
+    ld8_any(E.c, off, E.c_dt, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] += E.beta * t[j];
+  }
+}
+
 TT2_DEV void epi_store8(const EpiParams& E, uint32_t seed, int m, int n0, int N, const float (&v)[8],
                         bool pre_b = false) {
   const int64_t off = (int64_t)m * E.ldc + n0;
   if (E.vec && n0 + 8 <= N) {
-    float o[8], t[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = pre_b ? v[j] : v[j] * E.alpha;
-    if (E.bias && !pre_b) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(E.bias + n0), b = *reinterpret_cast<const f32x4*>(E.bias + n0 + 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { o[j] += a[j]; o[4 + j] += b[j]; }
-    }
-    if (E.res) {
-      ld8_any(E.res, (int64_t)m * E.ldr + n0, E.res_dt, t);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] += t[j];
-    }
-    if (E.act == ACT_RELU) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
-    } else if (E.act == ACT_TANH) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = tanhf(o[j]);
-    }
-    if (E.gate) {
-      ld8_any(E.gate, (int64_t)m * E.ldg + n0, E.gate_dt, t);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = t[j] != 0.f ? o[j] * E.gate_scale : 0.f;
-    }
-    if (E.drop.thr) {
-      const uint32_t base = (uint32_t)((int64_t)m * E.n_log + n0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = drop_apply(E.drop, seed, base + j, o[j]);
-    }
-    if (E.beta != 0.f) {
-      ld8_any(E.c, off, E.c_dt, t);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] += E.beta * t[j];
-    }
+    float o[8];
+    epi_calc8(E, seed, m, n0, v, pre_b, o);
     if (E.c_dt == TT2_BF16) {
       bf16x8 x;
 #pragma unroll
@@ -896,8 +905,12 @@ __device__ unsigned long long g_st[4096 * 64 * 4];
 #define G6_STAMP(t, slot)                                                                            \
   if (tid == 0 && (t) < 64)                                                                          \
     g_st[((size_t)(blockIdx.x + gridDim.x * blockIdx.y) * 64 + (t)) * 4 + (slot)] = __builtin_amdgcn_s_memtime();
+// workgroup entry / exit on the chip-wide 100 MHz clock (wave 0)
+#define G7_RT(slot)                                                                                  \
+  if (threadIdx.x == 0) g_st[(size_t)blockIdx.x * 64 * 4 + 63 * 4 + (slot)] = __builtin_amdgcn_s_memrealtime();
 #else
 #define G6_STAMP(t, slot)
+#define G7_RT(slot)
 #endif
 template <int BN_> struct G6 {
   static constexpr int WM = BN_ == 256 ? 2 : 4, WN = 8 / WM;
@@ -1290,12 +1303,24 @@ struct G7Prob {
   EpiParams E;
   int M, N, K, k_split, splits, ntn, items, item0;
   float* ws;   // split-K slabs [splits][M][N] (+ [splits][M] k-sums); used when splits > 1
+  int lds_epi; // C leaves through an LDS image in whole 256-B row segments (bf16 C, no split)
 };
 constexpr int G7_MAXP = 8;
 struct G7Group {
   G7Prob p[G7_MAXP];
   int np, items;
 };
+
+// whole-row store of the LDS C image (all 768 threads; 4 rows x 256 B per wave instruction)
+TT2_DEV void g7_store_c(const G7Prob& P, const char* smem, int m0, int n0) {
+  bf16* C = reinterpret_cast<bf16*>(P.E.c);
+  for (int id = threadIdx.x; id < 256 * 16; id += G7_NT) {
+    const int r = id >> 4, c = id & 15, m = m0 + r, n = n0 + 8 * c;
+    if (m < P.M && n < P.N)
+      *reinterpret_cast<bf16x8*>(C + (int64_t)m * P.E.ldc + n) =
+          *reinterpret_cast<const bf16x8*>(smem + r * 256 + ((c ^ (r & 15)) << 4));
+  }
+}
 
 template <bool AK, bool BKC>
 TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
@@ -1337,6 +1362,9 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
       }
       __builtin_amdgcn_s_barrier();
     }
+    if (!P.lds_epi) return;
+    __syncthreads();   // the MFMA waves' C image is in LDS
+    g7_store_c(P, smem, m0, n0);
     return;
   }
 
@@ -1412,6 +1440,46 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
   // column blocks (2p, 2p+1) between row pairs q, q^1 leaves 8 consecutive columns per lane
   const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
   const int q = ql;
+  if (P.lds_epi) {
+    // epilogue values -> bf16 C image [256 rows][16 chunks of 16 B] (chunk c of row r at
+    // c ^ (r & 15): the 16 rows of one store instruction hit 16 different bank groups),
+    // then all 12 waves store whole 256-B row segments
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wm * 64 + 16 * i + (lane & 15), m = m0 + r;
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        float v[8];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * pr][rr]),
+                                                           __float_as_uint(acc[i][2 * pr + 1][rr]), false, false);
+          v[rr] = __uint_as_float(sw[0]);
+          v[4 + rr] = __uint_as_float(sw[1]);
+        }
+        const int cl = wn * 64 + 16 * (2 * pr + (q & 1)) + 8 * (q >> 1), n = n0 + cl;
+        if (m >= M || n >= N) continue;
+        if (pre_b) {
+          const f32x4 b0 = pbias[pr][0], b1 = pbias[pr][1];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] = v[j] * E.alpha + b0[j];
+            v[4 + j] = v[4 + j] * E.alpha + b1[j];
+          }
+        }
+        float o[8];
+        epi_calc8(E, seed, m, n, v, pre_b, o);
+        bf16x8 x;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = (bf16)o[j];
+        *reinterpret_cast<bf16x8*>(smem + r * 256 + (((cl >> 3) ^ (r & 15)) << 4)) = x;
+      }
+    }
+    __syncthreads();
+    g7_store_c(P, smem, m0, n0);
+    G6_STAMP(nkt, 3)
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm * 64 + 16 * i + (lane & 15);
@@ -1461,8 +1529,10 @@ TT2_DEV int xcd_item(int bid, int n) {
 template <bool AK, bool BKC>
 __global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(G7Prob P) {
   __shared__ __attribute__((aligned(1024))) char smem[G7_STAGES * G7_STAGE];
+  G7_RT(0)
   const int u = xcd_item(blockIdx.x, P.items);
   g7_item<AK, BKC>(P, u % (P.items / P.splits), u / (P.items / P.splits), smem);
+  G7_RT(1)
 }
 
 // Grouped launch: up to G7_MAXP independent problems of one layout (e.g. all weight
@@ -1488,7 +1558,7 @@ __global__ void gemm_splitk_reduce_g(G7Group G) {
 
 G7Prob g7_prob(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits,
                             float* ws) {
-  G7Prob P{A, B, E, M, N, K, K, 1, (N + 127) / 128, 0, 0, ws};
+  G7Prob P{A, B, E, M, N, K, K, 1, (N + 127) / 128, 0, 0, ws, 0};
   if (splits > 1) {
     P.k_split = ((K + splits - 1) / splits + 63) / 64 * 64;
     P.splits = (K + P.k_split - 1) / P.k_split;
@@ -1499,8 +1569,9 @@ G7Prob g7_prob(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int 
 
 template <bool AK, bool BKC>
 hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
-                   hipStream_t s) {
-  const G7Prob P = g7_prob(A, B, E, M, N, K, splits, ws);
+                   hipStream_t s, bool lds_epi) {
+  G7Prob P = g7_prob(A, B, E, M, N, K, splits, ws);
+  P.lds_epi = lds_epi && P.splits == 1 && E.c_dt == TT2_BF16 && E.vec && (N % 8) == 0;
   hipEvent_t e0, e1;
   if (probe_take(e0, e1))
     hipExtLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, e0, e1, 0, P);
@@ -1520,6 +1591,18 @@ hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
 extern "C" size_t tt2_gemm_workspace_size(const tt2_gemm_args* a) {
   if (a->splits <= 1) return 0;
   return (size_t)a->splits * a->m * (a->n + (a->a_ksum ? 1 : 0)) * sizeof(float);
+}
+
+// v7 epilogue form: 14 = through the LDS C image, 13 = straight from registers; auto
+// follows TT2_G7_EPI (measurement switch, default 1)
+static bool g7_lds_epi(int variant) {
+  if (variant == 14) return true;
+  if (variant == 13) return false;
+  static const int env = [] {
+    const char* e = getenv("TT2_G7_EPI");
+    return e ? atoi(e) : 1;
+  }();
+  return env != 0;
 }
 
 // Kernel selection (also exported as tt2_gemm_plan): 1 v1 register-staged, 2 v2
@@ -1571,7 +1654,7 @@ static int gemm_plan(const tt2_gemm_args* a) {
   const bool v7ok = conv_ok(a->a_conv_t, a->a_conv_c) && conv_ok(a->b_conv_t, a->b_conv_c) &&
                     (int64_t)(a->trans_a ? a->k : a->m) * a->lda * 2 < (1LL << 31) &&
                     (int64_t)(a->trans_b ? a->k : a->n) * a->ldb * 2 < (1LL << 31);
-  if ((var == 13 || var == 0) && v7ok) return 13;
+  if ((var == 13 || var == 14 || var == 0) && v7ok) return 13;
   return 2;
 }
 
@@ -1673,10 +1756,11 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
     return tt2_check_launch(hipGetLastError(), "tt2_gemm(skinny)");
   }
   if (plan == 13) {
-    if (!a->trans_a && !a->trans_b) err = launch7<true, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
-    else if (!a->trans_a && a->trans_b) err = launch7<true, false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
-    else if (a->trans_a && !a->trans_b) err = launch7<false, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
-    else err = launch7<false, false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
+    const bool le = g7_lds_epi(a->kernel_variant);
+    if (!a->trans_a && !a->trans_b) err = launch7<true, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream, le);
+    else if (!a->trans_a && a->trans_b) err = launch7<true, false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream, le);
+    else if (a->trans_a && !a->trans_b) err = launch7<false, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream, le);
+    else err = launch7<false, false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream, le);
     return tt2_check_launch(err, "tt2_gemm(v7)");
   }
   if (plan == 11 || plan == 12) {

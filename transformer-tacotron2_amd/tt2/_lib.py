@@ -244,6 +244,7 @@ class AttnDecodeArgs(C.Structure):
         ("batch", i32), ("heads", i32), ("head_dim", i32), ("tk", i32), ("dtype", i32),
         ("scale", f32),
         ("stop_len", vp), ("step", vp),
+        ("wo", vp), ("wo_ld", i64), ("slab", vp),
     ]
 
 

@@ -466,11 +466,13 @@ def step_bump(step, seed=None):
 
 
 def attn_decode(q, k, v, out, q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld, batch, heads, tk, key_len=None,
-                t_ptr=None, scale=0.125, stop_len=None, step=None):
-    """One query row per batch element over a key cache (see tt2_attn_decode_args)."""
+                t_ptr=None, scale=0.125, stop_len=None, step=None, wo=None, wo_ld=0, slab=None):
+    """One query row per batch element over a key cache (see tt2_attn_decode_args).
+    wo / slab: the fused output projection, slab[h, b, :] = o[b, h] @ wo[:, h*64:(h+1)*64]^T (f32)."""
     a = _lib.AttnDecodeArgs()
     a.stop_len, a.step = ptr(stop_len), ptr(step)
-    a.q, a.k, a.v, a.out = q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr()
+    a.q, a.k, a.v, a.out = q.data_ptr(), k.data_ptr(), v.data_ptr(), ptr(out)
+    a.wo, a.wo_ld, a.slab = ptr(wo), wo_ld, ptr(slab)
     a.q_ld, a.k_bstride, a.k_ld, a.v_bstride, a.v_ld, a.o_ld = q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld
     a.key_len, a.t_ptr = ptr(key_len), ptr(t_ptr)
     a.batch, a.heads, a.head_dim, a.tk, a.dtype, a.scale = batch, heads, 64, tk, dt(q), scale
