@@ -434,6 +434,134 @@ int tt2_adam_step(const tt2_adam_args* a, hipStream_t stream);
 /* step += 1; seed += 1 (seed may be NULL) */
 int tt2_step_bump(int32_t* step, uint32_t* seed, hipStream_t stream);
 
+/* ---------------------------------------------------------- block-level entry points
+ * One call per block of the path: each is a fixed sequence of the kernels
+ * above on the caller's stream, with the block's shape and options in a tt2_desc.
+ * Layout: activations channels-last [rows = batch * tq (or tk), channels] of desc.dtype
+ * (TT2_DT_BF16 or TT2_DT_F32); weights of desc.dtype in nn.Linear layout [out][in]
+ * (conv: [c_out][kernel][c_in], see tt2_conv_weight_pack); biases, LayerNorm / BatchNorm
+ * parameters, statistics and every weight / bias gradient f32.  Weight and bias
+ * gradients are written (not accumulated).
+ *  - `saved`: activations a forward keeps for its backward, tt2_<block>_saved_size() bytes,
+ *    written by _fwd and read by _bwd (the caller keeps it between them);
+ *  - `workspace`: scratch of tt2_<block>_workspace_size() bytes (split-K slabs, partials),
+ *    free again when the call's work has finished on the stream.
+ * Dropout: p = desc.dropout at hash site desc.site (the FFN's second site is site + 1)
+ * with seed *desc.seed, applied when desc.training is set. */
+typedef struct tt2_desc {
+  int32_t batch;          /* B */
+  int32_t tq;             /* rows per utterance: query / sequence length */
+  int32_t tk;             /* attention keys per utterance (cross: memory length; self: = tq) */
+  int32_t d_model;        /* 512 (heads of width 64) */
+  int32_t n_heads;
+  int32_t d_ffn;
+  int32_t c_in, c_out;    /* linear / conv1d_bn_act / heads channels (heads: c_out = n_mels + 1) */
+  int32_t kernel;         /* conv taps (odd; "same" padding (kernel - 1) / 2) */
+  int32_t dtype;          /* TT2_DT_BF16 or TT2_DT_F32 */
+  int32_t causal;         /* attention: causal mask (self-attention) */
+  int32_t cross;          /* attention: 1 = Q from x, K / V from mem (in_proj rows 0:d / d:3d) */
+  int32_t act;            /* conv1d_bn_act: 0 none, 1 relu, 2 tanh */
+  int32_t training;       /* dropout on; BatchNorm batch statistics + running-stat update */
+  float eps;              /* LayerNorm / BatchNorm epsilon */
+  float momentum;         /* BatchNorm running-stat momentum */
+  float dropout;          /* p (0 = none) */
+  const uint32_t* seed;   /* device dropout seed */
+  uint32_t site;          /* dropout hash site */
+  const int32_t* k_len;   /* [batch] valid keys per utterance (key padding mask) or NULL */
+  const int32_t* mel_len; /* loss: [batch] valid frames */
+  int32_t n_mels;         /* loss / heads: mel channels (80) */
+  int32_t heads_ld;       /* heads / loss: row stride of the heads buffer (>= n_mels + 1) */
+  float pos_weight;       /* loss: BCE positive weight */
+  float grad_scale;       /* loss: multiplies every gradient (1 / world under data parallelism) */
+} tt2_desc;
+
+/* Attention sublayer (SURVEY 8(a) a3 / a6 / a7 + residual + post-LN):
+ *   y = LN(x + drop(out_proj(SDPA(q = x Wq^T + bq, k|v = src Wkv^T + bkv))) ; src = cross ? mem : x
+ * w_in [3d][d] (nn.MultiheadAttention in_proj), b_in [3d], w_out [d][d], b_out [d], ln_g / ln_b [d].
+ * bwd: dy -> dx (residual + query path; + key/value path when not cross), dmem (cross: the
+ * key/value path; NULL otherwise), and the parameter gradients. */
+size_t tt2_attn_block_saved_size(const tt2_desc* d);
+size_t tt2_attn_block_workspace_size(const tt2_desc* d);
+int tt2_attn_block_fwd(const tt2_desc* d, const void* x, const void* mem, const void* w_in, const float* b_in,
+                       const void* w_out, const float* b_out, const float* ln_g, const float* ln_b, void* y,
+                       void* saved, void* workspace, size_t ws_bytes, hipStream_t stream);
+int tt2_attn_block_bwd(const tt2_desc* d, const void* x, const void* mem, const void* w_in, const void* w_out,
+                       const float* ln_g, const float* ln_b, const void* saved, const void* dy, void* dx, void* dmem,
+                       float* dw_in, float* db_in, float* dw_out, float* db_out, float* dln_g, float* dln_b,
+                       void* workspace, size_t ws_bytes, hipStream_t stream);
+
+/* Position-wise FFN sublayer:
+ *   y = LN(x + drop_{site+1}(drop_{site}(relu(x W1^T + b1)) W2^T + b2)),  w1 [d_ffn][d], w2 [d][d_ffn]. */
+size_t tt2_ffn_saved_size(const tt2_desc* d);
+size_t tt2_ffn_workspace_size(const tt2_desc* d);
+int tt2_ffn_fwd(const tt2_desc* d, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                const float* ln_g, const float* ln_b, void* y, void* saved, void* workspace, size_t ws_bytes,
+                hipStream_t stream);
+int tt2_ffn_bwd(const tt2_desc* d, const void* x, const void* w1, const void* w2, const float* ln_g,
+                const float* ln_b, const void* saved, const void* dy, void* dx, float* dw1, float* db1, float* dw2,
+                float* db2, float* dln_g, float* dln_b, void* workspace, size_t ws_bytes, hipStream_t stream);
+
+/* Linear (pre-net / projections): y [rows][c_out] = x [rows][c_in] W^T + b (b may be NULL). */
+size_t tt2_linear_workspace_size(const tt2_desc* d);
+int tt2_linear_fwd(const tt2_desc* d, const void* x, const void* w, const float* b, void* y, void* workspace,
+                   size_t ws_bytes, hipStream_t stream);
+int tt2_linear_bwd(const tt2_desc* d, const void* x, const void* w, const void* dy, void* dx, float* dw, float* db,
+                   void* workspace, size_t ws_bytes, hipStream_t stream);
+
+/* Residual add + post-LayerNorm: y = LN(x + drop(branch)) over d_model channels; saved = mean / rstd.
+ * bwd: dx = dL/d(x + drop(branch)), dbranch = drop'(dx), dln_g / dln_b. */
+size_t tt2_add_ln_saved_size(const tt2_desc* d);
+size_t tt2_add_ln_workspace_size(const tt2_desc* d);
+int tt2_add_ln_fwd(const tt2_desc* d, const void* x, const void* branch, const float* ln_g, const float* ln_b,
+                   void* y, void* saved, hipStream_t stream);
+int tt2_add_ln_bwd(const tt2_desc* d, const void* x, const void* branch, const float* ln_g, const void* saved,
+                   const void* dy, void* dx, void* dbranch, float* dln_g, float* dln_b, void* workspace,
+                   size_t ws_bytes, hipStream_t stream);
+
+/* Conv1d + BatchNorm + activation + dropout (SURVEY 8(a) a1 encoder pre-net, a9 post-net):
+ *   out = drop(act(BN(conv(x) + b))) (+ res, [rows][c_out] of res_dtype, when res != NULL);
+ * w [c_out][kernel][c_in]; BN over all rows (training: batch statistics, run_mean / run_var
+ * updated; eval: the running statistics).  bwd: dout -> dx and dw / db / dbn_g / dbn_b. */
+size_t tt2_conv1d_bn_act_saved_size(const tt2_desc* d);
+size_t tt2_conv1d_bn_act_workspace_size(const tt2_desc* d);
+int tt2_conv1d_bn_act_fwd(const tt2_desc* d, const void* x, const void* w, const float* b, const float* bn_g,
+                          const float* bn_b, float* run_mean, float* run_var, const void* res, int32_t res_dtype,
+                          void* out, void* saved, void* workspace, size_t ws_bytes, hipStream_t stream);
+int tt2_conv1d_bn_act_bwd(const tt2_desc* d, const void* x, const void* w, const float* bn_g, const float* bn_b,
+                          const void* saved, const void* dout, void* dx, float* dw, float* db, float* dbn_g,
+                          float* dbn_b, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* nn.Conv1d weight [c_out][c_in][k] -> the blocks' tap-major [c_out][k][c_in] (same dtype) */
+int tt2_conv_weight_pack(const void* w, void* wp, int32_t cout, int32_t cin, int32_t k, int32_t dtype,
+                         hipStream_t stream);
+
+/* Mel + stop heads: heads [rows][heads_ld] f32, cols 0..n_mels-1 = mel_before,
+ * col n_mels = stop logit; w [n_mels + 1][d_model] (mel_linear rows, then stop_linear), b f32.
+ * bwd: g_heads (f32, same layout) -> dx, dw, db. */
+size_t tt2_heads_workspace_size(const tt2_desc* d);
+int tt2_heads_fwd(const tt2_desc* d, const void* x, const void* w, const float* b, float* heads, void* workspace,
+                  size_t ws_bytes, hipStream_t stream);
+int tt2_heads_bwd(const tt2_desc* d, const void* x, const void* w, const float* g_heads, void* dx, float* dw,
+                  float* db, void* workspace, size_t ws_bytes, hipStream_t stream);
+
+/* Loss over rows = batch * tq: loss_out[4] = (total, mse_before, mse_after, bce);
+ * bwd also writes g_heads (d/d mel_before in cols < n_mels, d/d stop logit in col n_mels) and
+ * g_after (d/d mel_after, desc.dtype). */
+size_t tt2_loss_block_workspace_size(const tt2_desc* d);
+int tt2_loss_fwd(const tt2_desc* d, const float* heads, const float* mel_after, const float* target,
+                 float* loss_out, void* workspace, size_t ws_bytes, hipStream_t stream);
+int tt2_loss_bwd(const tt2_desc* d, const float* heads, const float* mel_after, const float* target,
+                 float* loss_out, float* g_heads, void* g_after, void* workspace, size_t ws_bytes,
+                 hipStream_t stream);
+
+/* Data-parallel gradient bucket: in-place SUM all-reduce of n elements of
+ * dtype over an RCCL communicator (ncclComm_t) on the caller's stream.  librccl is bound at
+ * the first call (dlopen); the communicator helpers below wrap ncclGetUniqueId /
+ * ncclCommInitRank / ncclCommDestroy for hosts without torch.distributed. */
+int tt2_allreduce_bucket(void* buf, size_t n, int32_t dtype, void* comm, hipStream_t stream);
+int tt2_comm_unique_id(void* id_out /* 128 bytes */);
+int tt2_comm_init(void** comm_out, int32_t nranks, const void* id /* 128 bytes */, int32_t rank);
+int tt2_comm_destroy(void* comm);
+
 /* ------------------------------------------------------------ audio data path
  * Either side of the mel engine: log-mel extraction of the
  * training targets and Griffin-Lim inversion of synthesised mels.  The STFT, inverse DFT

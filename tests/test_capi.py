@@ -51,7 +51,8 @@ def test_struct_sizes_match_c_layout(lib):
     import tempfile
     structs = {"tt2_gemm_args": lib.GemmArgs, "tt2_attn_args": lib.AttnArgs, "tt2_ln_args": lib.LnArgs,
                "tt2_bn_args": lib.BnArgs, "tt2_pe_args": lib.PeArgs, "tt2_loss_args": lib.LossArgs,
-               "tt2_adam_args": lib.AdamArgs, "tt2_reduce_args": lib.ReduceArgs}
+               "tt2_adam_args": lib.AdamArgs, "tt2_reduce_args": lib.ReduceArgs,
+               "tt2_attn_decode_args": lib.AttnDecodeArgs, "tt2_decode_desc": lib.DecodeDesc, "tt2_desc": lib.Desc}
     prog = "#include <stdio.h>\n#include <stddef.h>\n#include \"tt2_capi.h\"\nint main(){\n"
     for name, cls in structs.items():
         last = cls._fields_[-1][0]
@@ -80,3 +81,29 @@ def test_no_cpu_fallback(lib):
         pytest.skip("GPU present")
     with pytest.raises(lib.TT2Error):
         lib.lib()
+
+
+def test_block_sizes_without_gpu(lib):
+    """The block-level size queries are host-only (the dry pass of each block, no device
+    call): positive, growing with the batch, 0 for an invalid descriptor."""
+    import ctypes as C
+    L = lib.load()
+
+    def desc(batch, **kw):
+        d = lib.Desc()
+        d.batch, d.tq, d.tk, d.d_model, d.n_heads, d.d_ffn = batch, 800, 128, 512, 8, 2048
+        d.c_in, d.c_out, d.kernel, d.dtype, d.n_mels, d.heads_ld = 512, 512, 5, lib.DT_BF16, 80, 96
+        for k, v in kw.items():
+            setattr(d, k, v)
+        return d
+
+    for fn in ("tt2_attn_block_saved_size", "tt2_attn_block_workspace_size", "tt2_ffn_saved_size",
+               "tt2_ffn_workspace_size", "tt2_linear_workspace_size", "tt2_add_ln_saved_size",
+               "tt2_add_ln_workspace_size", "tt2_conv1d_bn_act_saved_size", "tt2_conv1d_bn_act_workspace_size",
+               "tt2_heads_workspace_size", "tt2_loss_block_workspace_size"):
+        f = getattr(L, fn)
+        small, big = f(C.byref(desc(2))), f(C.byref(desc(16)))
+        assert 0 < small <= big, fn
+    assert L.tt2_attn_block_saved_size(C.byref(desc(2, cross=1))) > 0
+    assert L.tt2_attn_block_saved_size(C.byref(desc(2, d_model=384))) == 0
+    assert L.tt2_conv1d_bn_act_workspace_size(C.byref(desc(2, kernel=4))) == 0

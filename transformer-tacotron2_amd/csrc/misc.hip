@@ -6,6 +6,8 @@
 // except the embedding scatter).
 #include <math.h>
 
+#include <algorithm>
+
 #include "tt2_capi.h"
 #include "tt2_internal.h"
 #include "tt2_common.h"
@@ -335,6 +337,19 @@ __global__ __launch_bounds__(NT) void conv_wflip_kernel(const T* w, T* wd, int C
   }
 }
 
+// nn.Conv1d weight [Cout][Cin][K] -> tap-major [Cout][K][Cin]: per output channel a
+// [Cin x K] -> [K x Cin] transpose (weights are small; one thread per element, writes coalesced)
+template <typename T>
+__global__ __launch_bounds__(NT) void conv_wpack_kernel(const T* w, T* wp, int Cout, int Cin, int K) {
+  const int64_t total = (int64_t)Cout * Cin * K;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
+    const int ci = (int)(i % Cin);
+    const int64_t r = i / Cin;
+    const int tap = (int)(r % K), co = (int)(r / K);
+    wp[i] = w[((int64_t)co * Cin + ci) * K + tap];
+  }
+}
+
 // ------------------------------------------------------------------ Adam
 __global__ __launch_bounds__(NT) void sumsq_kernel(const float* g, int64_t n, float* part) {
   __shared__ float red[NT / 64];
@@ -567,6 +582,21 @@ extern "C" int tt2_conv_weight_flip(const void* w, void* wd, int cout, int cin, 
   else
     hipLaunchKernelGGL(conv_wflip_kernel<float>, g, dim3(NT), 0, s, (const float*)w, (float*)wd, cout, cin, k);
   return tt2_check_launch(hipGetLastError(), "tt2_conv_weight_flip");
+}
+
+extern "C" int tt2_conv_weight_pack(const void* w, void* wp, int32_t cout, int32_t cin, int32_t k, int32_t dtype,
+                                    hipStream_t s) {
+  if (cout <= 0 || cin <= 0 || k <= 0) return TT2_OK;
+  if (!w || !wp || w == wp) return tt2_set_error(TT2_E_INVALID, "tt2_conv_weight_pack: null or in-place");
+  const int64_t total = (int64_t)cout * cin * k;
+  const int g = (int)std::min<int64_t>((total + NT - 1) / NT, 4096);
+  if (dtype == TT2_DT_BF16)
+    hipLaunchKernelGGL(conv_wpack_kernel<bf16>, dim3(g), dim3(NT), 0, s, (const bf16*)w, (bf16*)wp, cout, cin, k);
+  else if (dtype == TT2_DT_F32)
+    hipLaunchKernelGGL(conv_wpack_kernel<float>, dim3(g), dim3(NT), 0, s, (const float*)w, (float*)wp, cout, cin, k);
+  else
+    return tt2_set_error(TT2_E_INVALID, "tt2_conv_weight_pack: dtype");
+  return tt2_check_launch(hipGetLastError(), "tt2_conv_weight_pack");
 }
 
 extern "C" size_t tt2_adam_workspace_size(void) { return (TT2_ADAM_NORM_BLOCKS + 16) * sizeof(float); }

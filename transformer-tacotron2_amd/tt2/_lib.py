@@ -283,3 +283,49 @@ SIGNATURES.update({
     "tt2_decode_graph_launch": ([vp, i32, vp], C.c_int),
     "tt2_decode_graph_destroy": ([vp], C.c_int),
 })
+
+
+class Desc(C.Structure):
+    """tt2_desc: shape and options of one block-level call (include/tt2_capi.h)."""
+    _fields_ = [
+        ("batch", i32), ("tq", i32), ("tk", i32), ("d_model", i32), ("n_heads", i32), ("d_ffn", i32),
+        ("c_in", i32), ("c_out", i32), ("kernel", i32), ("dtype", i32), ("causal", i32), ("cross", i32),
+        ("act", i32), ("training", i32), ("eps", f32), ("momentum", f32), ("dropout", f32),
+        ("seed", vp), ("site", u32), ("k_len", vp), ("mel_len", vp), ("n_mels", i32), ("heads_ld", i32),
+        ("pos_weight", f32), ("grad_scale", f32),
+    ]
+
+
+_PD = C.POINTER(Desc)
+SIGNATURES.update({
+    "tt2_attn_block_saved_size": ([_PD], sz),
+    "tt2_attn_block_workspace_size": ([_PD], sz),
+    "tt2_attn_block_fwd": ([_PD] + [vp] * 11 + [sz, vp], C.c_int),
+    "tt2_attn_block_bwd": ([_PD] + [vp] * 17 + [sz, vp], C.c_int),
+    "tt2_ffn_saved_size": ([_PD], sz),
+    "tt2_ffn_workspace_size": ([_PD], sz),
+    "tt2_ffn_fwd": ([_PD] + [vp] * 10 + [sz, vp], C.c_int),
+    "tt2_ffn_bwd": ([_PD] + [vp] * 15 + [sz, vp], C.c_int),
+    "tt2_linear_workspace_size": ([_PD], sz),
+    "tt2_linear_fwd": ([_PD] + [vp] * 5 + [sz, vp], C.c_int),
+    "tt2_linear_bwd": ([_PD] + [vp] * 7 + [sz, vp], C.c_int),
+    "tt2_add_ln_saved_size": ([_PD], sz),
+    "tt2_add_ln_workspace_size": ([_PD], sz),
+    "tt2_add_ln_fwd": ([_PD] + [vp] * 6 + [vp], C.c_int),
+    "tt2_add_ln_bwd": ([_PD] + [vp] * 10 + [sz, vp], C.c_int),
+    "tt2_conv1d_bn_act_saved_size": ([_PD], sz),
+    "tt2_conv1d_bn_act_workspace_size": ([_PD], sz),
+    "tt2_conv1d_bn_act_fwd": ([_PD] + [vp] * 8 + [i32, vp, vp, vp, sz, vp], C.c_int),
+    "tt2_conv1d_bn_act_bwd": ([_PD] + [vp] * 12 + [sz, vp], C.c_int),
+    "tt2_conv_weight_pack": ([vp, vp, i32, i32, i32, i32, vp], C.c_int),
+    "tt2_heads_workspace_size": ([_PD], sz),
+    "tt2_heads_fwd": ([_PD] + [vp] * 5 + [sz, vp], C.c_int),
+    "tt2_heads_bwd": ([_PD] + [vp] * 7 + [sz, vp], C.c_int),
+    "tt2_loss_block_workspace_size": ([_PD], sz),
+    "tt2_loss_fwd": ([_PD] + [vp] * 5 + [sz, vp], C.c_int),
+    "tt2_loss_bwd": ([_PD] + [vp] * 7 + [sz, vp], C.c_int),
+    "tt2_allreduce_bucket": ([vp, sz, i32, vp, vp], C.c_int),
+    "tt2_comm_unique_id": ([vp], C.c_int),
+    "tt2_comm_init": ([C.POINTER(vp), i32, vp, i32], C.c_int),
+    "tt2_comm_destroy": ([vp], C.c_int),
+})
