@@ -197,16 +197,12 @@ def gemm_kernel_name(plan: int, ta: int, tb: int) -> str:
     ak, bk = t(not ta), t(not tb)
     if plan == 2:
         return f"gemm2_kernel<{ak}, {bk}>"
-    if plan in (9, 10):
-        return f"gemm5_kernel<{ak}, {bk}, {3 if plan == 9 else 2}>"
-    if plan == 8:
-        return f"gemm4_kernel<{bk}>"
     if plan == 3:
         return "gemm_skinny_kernel"
     if plan == 13:
         return f"gemm7_kernel<{ak}, {bk}>"
-    if plan in (11, 12):
-        return f"gemm6_kernel<{ak}, {bk}, {256 if plan == 11 else 128}>"
+    if plan == 1:
+        return "gemm_kernel"
     return f"gemm plan {plan}"
 
 

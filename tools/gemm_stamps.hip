@@ -1,15 +1,22 @@
-// In-kernel timeline of the v6 GEMM (dev tool): builds gemm.hip with TT2_STAMPS, runs a
+// In-kernel timeline of the v7 GEMM (dev tool): builds gemm.hip with its stamp hooks defined, runs a
 // shape, and prints the average per-K-step split (s_memtime cycles, wave 0 of every
 // workgroup): wait = vmcnt + barrier, issue = LDS-DMA issue, comp = fragment reads +
 // MFMA issue, plus the epilogue and the spread of workgroup start times.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I transformer-tacotron2_amd/csrc \
-//     -DTT2_STAMPS tools/gemm_stamps.hip -o tools/bin/gemm_stamps
+//     tools/gemm_stamps.hip -o tools/bin/gemm_stamps
 //   tools/bin/gemm_stamps m n k ta tb variant splits
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
 
+// the stamp hooks gemm.hip leaves empty in the library build (wave 0 of every workgroup)
+__device__ unsigned long long g_st[4096 * 64 * 4];
+#define G7_STAMP(t, slot)                                                                            \
+  if (threadIdx.x == 0 && (t) < 64)                                                                  \
+    g_st[((size_t)(blockIdx.x + gridDim.x * blockIdx.y) * 64 + (t)) * 4 + (slot)] = __builtin_amdgcn_s_memtime();
+#define G7_RT(slot)                                                                                  \
+  if (threadIdx.x == 0) g_st[(size_t)blockIdx.x * 64 * 4 + 63 * 4 + (slot)] = __builtin_amdgcn_s_memrealtime();
 #include "../transformer-tacotron2_amd/csrc/gemm.hip"
 #include "../transformer-tacotron2_amd/csrc/runtime.cpp"
 

@@ -474,21 +474,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 TT2_DEV void mma32(const bf16x8& a, const bf16x8& b, f32x16& c) {
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
-#ifdef TT2_ABL_NOEXP   // timing-only ablation builds (tools/attn_ablate.sh)
-TT2_DEV float fast_exp2(float x) { return x; }
-#else
 TT2_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
-#endif
-#ifdef TT2_ABL_L2HOT
-#define ABL_ROW(x) 0
-#else
-#define ABL_ROW(x) (x)
-#endif
-#ifdef TT2_ABL_NOSYNC
-#define ABL_SYNC()
-#else
-#define ABL_SYNC() __syncthreads()
-#endif
 
 // 16-B chunk c of tile row r lives at slot c ^ swz(r), swz(r) = h((r >> 1) & 7) with
 // h(x) = ((x & 1) << 2) | (x >> 1).  Row reads (ds_read_b128: 16 distinct rows mod 16
@@ -631,8 +617,8 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
     const int k0 = 64 * t;
     const bool more = t + 1 < ntile;
     if (more) {
-      g2r3<NTH>(rk, K, ABL_ROW(k0 + 64), tid);
-      g2r3<NTH>(rv, V, ABL_ROW(k0 + 64), tid);
+      g2r3<NTH>(rk, K, k0 + 64, tid);
+      g2r3<NTH>(rv, V, k0 + 64, tid);
     }
     const bf16* cK = sK[BUF];
     const bf16* cV = sV[BUF];
@@ -689,7 +675,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
       r2s3<NTH>(rk, sK[BUF ^ 1], tid);
       r2s3<NTH>(rv, sV[BUF ^ 1], tid);
     }
-    ABL_SYNC();
+    __syncthreads();
   };
   for (int t = 0; t < ntile; t += 2) {
     tile(std::integral_constant<int, 0>{}, t);
@@ -760,8 +746,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
     const int k0 = 64 * t;
     const bool more = t + 1 < ntile;
     if (more) {
-      g2r3<NTH>(rk, K, ABL_ROW(k0 + 64), tid);
-      g2r3<NTH>(rv, V, ABL_ROW(k0 + 64), tid);
+      g2r3<NTH>(rk, K, k0 + 64, tid);
+      g2r3<NTH>(rv, V, k0 + 64, tid);
     }
     const bf16* cK = sK[BUF];
     const bf16* cV = sV[BUF];
@@ -797,7 +783,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
       r2s3<NTH>(rk, sK[BUF ^ 1], tid);
       r2s3<NTH>(rv, sV[BUF ^ 1], tid);
     }
-    ABL_SYNC();
+    __syncthreads();
   };
   for (int t = 0; t < ntile; t += 2) {
     tile(std::integral_constant<int, 0>{}, t);
@@ -862,8 +848,8 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
     const int q0 = qstart + 64 * t;
     const bool more = t + 1 < ntile;
     if (more) {
-      g2r3<NTH>(rq, Q, ABL_ROW(q0 + 64), tid);
-      g2r3<NTH>(rd, dO, ABL_ROW(q0 + 64), tid);
+      g2r3<NTH>(rq, Q, q0 + 64, tid);
+      g2r3<NTH>(rd, dO, q0 + 64, tid);
     }
     const bf16* cQ = sQ[BUF];
     const bf16* cD = sdO[BUF];
@@ -918,7 +904,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
       r2s3<NTH>(rd, sdO[BUF ^ 1], tid);
       stats(BUF ^ 1, q0 + 64);
     }
-    ABL_SYNC();
+    __syncthreads();
   };
   for (int t = 0; t < ntile; t += 2) {
     tile(std::integral_constant<int, 0>{}, t);

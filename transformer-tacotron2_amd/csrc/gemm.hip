@@ -520,13 +520,11 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
   for (int kt = 0; kt < nkt; ++kt) {
     const char* sa = smem + (kt & 1) * STAGE_BYTES;
     const char* sb = sa + TILE_BYTES;
-#ifndef TT2_ABL_NO_LOAD
     if (kt + 1 < nkt) {
       char* na = smem + ((kt + 1) & 1) * STAGE_BYTES;
       issue_tile<AK>(A, na, m0, kb + (kt + 1) * BK2, lane, wave);
       issue_tile<BKC>(B, na + TILE_BYTES, n0, kb + (kt + 1) * BK2, lane, wave);
     }
-#endif
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       Frag8<bf16> fa[4], fb[4];
@@ -534,21 +532,10 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
       for (int i = 0; i < 4; ++i) frag2<AK>(fa[i], sa, wm * 64 + 16 * i, kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) frag2<BKC>(fb[j], sb, wn * 64 + 16 * j, kk, lane);
-#ifdef TT2_ABL_NO_MFMA
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { asm volatile("" :: "v"(fa[i].v)); asm volatile("" :: "v"(fb[i].v)); }
-#else
-#ifdef TT2_G2_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) mma16(fa[i], fb[j], acc[i][j]);
-#ifdef TT2_G2_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
-#endif
     }
     if (!AK && do_ks) {
       // rows 4*(tid>>4) .. +3 of the [64 k][128 m] A image, m-chunk tid & 15
@@ -587,10 +574,6 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
     }
     __syncthreads();
   }
-#ifdef TT2_ABL_NO_EPI
-  if (acc[0][0][0] == 1234.5f && acc[3][3][3] == 1234.5f) reinterpret_cast<float*>(E.c)[tid] = acc[1][1][1];
-  return;
-#endif
 
   // stage C (f32) through LDS: row-major [128][EPI_LD]
   float* cs = reinterpret_cast<float*>(smem);
@@ -614,9 +597,6 @@ __global__ __launch_bounds__(NT, 2) void gemm2_kernel(OpDesc A, OpDesc B, EpiPar
     const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * EPI_LD + c8 + 4);
     v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
     v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-#ifdef TT2_ABL_NO_STORE
-    if (v[0] != 1234.5f) continue;
-#endif
     if (ws) {
       float* w = ws + ((int64_t)blockIdx.y * M + m) * N + n;
       if (n + 8 <= N && (N % 4) == 0) {
@@ -883,319 +863,23 @@ hipError_t launch2(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
 }
 
 
-// =====================================================================================
-// v6 (bf16, plain operands): 256-row tiles.  Every 128^2 kernel above streams operand
-// tiles at ~50 GB/s per CU, and making both operands L2-resident speeds the same launch
-// up by only ~5 %: the L2 -> LDS path, not HBM, bounds them, so FLOPs per staged byte
-// is the lever -- 256 x 256 (128 FLOP/B) or 256 x 128 (85 FLOP/B) against 64.
-// 512 threads = 8 waves.  BN = 256: 2 (M) x 4 (N) waves of 128 x 64, 2 LDS stages;
-// BN = 128: 4 x 2 waves of 64 x 64, 3 stages (counted vmcnt + raw s_barrier).  BK = 64.
-// Each lane's LDS-DMA source is a loop-invariant 32-bit byte offset from a wave-uniform
-// base that advances one K tile per step, so the loop spends no VALU on addresses.
-// Rows / columns past M or N are clamped to the last valid one (they only feed C rows /
-// columns that are never stored); the K tail (the last step when the K range is not a
-// multiple of 64) takes a masked copy that reads the zero page.
-// Images are v2's: K-contiguous [rows][8 chunks], chunk c of row r at c ^ (r & 7);
-// M/N-contiguous as 128-column sub-images [64 k][16 chunks], chunk c of row k at
-// c ^ mc_swz(k).
-// =====================================================================================
-constexpr int G6_NT = 512;
-#ifdef TT2_STAMPS   // dev timeline (tools/gemm_stamps.hip): per workgroup and K step, wave 0
-__device__ unsigned long long g_st[4096 * 64 * 4];
-#define G6_STAMP(t, slot)                                                                            \
-  if (tid == 0 && (t) < 64)                                                                          \
-    g_st[((size_t)(blockIdx.x + gridDim.x * blockIdx.y) * 64 + (t)) * 4 + (slot)] = __builtin_amdgcn_s_memtime();
-// workgroup entry / exit on the chip-wide 100 MHz clock (wave 0)
-#define G7_RT(slot)                                                                                  \
-  if (threadIdx.x == 0) g_st[(size_t)blockIdx.x * 64 * 4 + 63 * 4 + (slot)] = __builtin_amdgcn_s_memrealtime();
-#else
-#define G6_STAMP(t, slot)
-#define G7_RT(slot)
-#endif
-template <int BN_> struct G6 {
-  static constexpr int WM = BN_ == 256 ? 2 : 4, WN = 8 / WM;
-  static constexpr int TM = 256 / WM, TN = BN_ / WN;              // wave tile
-  static constexpr int MI = TM / 16, NJ = TN / 16;
-  static constexpr int A_BYTES = 256 * 128, B_BYTES = BN_ * 128;   // 64 k x 2 B per row
-  static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int A_INST = A_BYTES / 1024 / 8, B_INST = B_BYTES / 1024 / 8;   // per wave
-  static constexpr int INST = A_INST + B_INST;
-  static constexpr int STAGES = BN_ == 256 ? 2 : 3;
-  static constexpr int EPI_ROWS = BN_ == 256 ? 128 : 256;          // C rows staged per pass
-  static constexpr int EPI_LDW = BN_ + 4;
-  static constexpr int EPI = EPI_ROWS * EPI_LDW * 4;
-  static constexpr int SMEM = STAGES * STAGE > EPI ? STAGES * STAGE : EPI;
-};
-
-// loop-invariant byte offsets of this lane's NI copies of one operand tile
-template <bool KC, int NI>
-TT2_DEV void g6_offsets(uint32_t (&off)[NI], const OpDesc& d, int r0, int lane, int wave) {
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int inst = wave * NI + i;
-    if (KC) {
-      const int row = inst * 8 + (lane >> 3);
-      const int gc = (lane & 7) ^ (row & 7);
-      const int r = min(r0 + row, d.outer_max - 1);
-      off[i] = (uint32_t)(((int64_t)r * d.ld + gc * 8) * 2);
-    } else {
-      const int sub = inst >> 4, kr = (inst & 15) * 4 + (lane >> 4);
-      const int gc = (lane & 15) ^ mc_swz(kr);
-      int col = r0 + sub * 128 + gc * 8;
-      col = col < d.inner_max ? col : d.inner_max - 8;
-      off[i] = (uint32_t)(((int64_t)kr * d.ld + col) * 2);
-    }
-  }
-}
-
-template <bool KC, int NI>
-TT2_DEV void g6_issue(const OpDesc& d, const uint32_t (&off)[NI], char* lds, int k0, int wave) {
-  const char* base = reinterpret_cast<const char*>(d.p) + (KC ? (int64_t)k0 * 2 : (int64_t)k0 * d.ld * 2);
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-    __builtin_amdgcn_global_load_lds((gvoid_t*)(base + off[i]), (lvoid_t*)(lds + (wave * NI + i) * 1024), 16, 0, 0);
-}
-
-// the K-tail copy: chunks (KC) or k rows (M/N-contiguous) at k >= ke read the zero page
-template <bool KC, int NI>
-TT2_DEV void g6_issue_tail(const OpDesc& d, const uint32_t (&off)[NI], char* lds, int k0, int ke, int lane,
-                           int wave) {
-  const char* base = reinterpret_cast<const char*>(d.p) + (KC ? (int64_t)k0 * 2 : (int64_t)k0 * d.ld * 2);
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int inst = wave * NI + i;
-    int k;
-    if (KC) {
-      const int row = inst * 8 + (lane >> 3);
-      k = k0 + ((lane & 7) ^ (row & 7)) * 8;
-    } else {
-      k = k0 + (inst & 15) * 4 + (lane >> 4);
-    }
-    const void* src = k < ke ? (const void*)(base + off[i]) : (const void*)g_zero_page;
-    __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(lds + inst * 1024), 16, 0, 0);
-  }
-}
-
-// one LDS-DMA copy (instruction `inst` of the operand's tile); tl: the K-tail step
+// Fragment reads of the 256-row LDS images: K-contiguous [rows][8 chunks] with chunk c of
+// row r at c ^ (r & 7); M/N-contiguous as 128-column sub-images [64 k][16 chunks] with
+// chunk c of row k at c ^ mc_swz(k) (v2's images, stacked).
 template <bool KC>
-TT2_DEV void g6_issue_one(const OpDesc& d, uint32_t off, char* lds, int k0, int ke, int inst, int lane, bool tl) {
-  const char* base = reinterpret_cast<const char*>(d.p) + (KC ? (int64_t)k0 * 2 : (int64_t)k0 * d.ld * 2);
-  const void* src = base + off;
-  if (tl) {
-    int k;
-    if (KC) {
-      const int row = inst * 8 + (lane >> 3);
-      k = k0 + ((lane & 7) ^ (row & 7)) * 8;
-    } else {
-      k = k0 + (inst & 15) * 4 + (lane >> 4);
-    }
-    src = k < ke ? src : (const void*)g_zero_page;
-  }
-  __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(lds + inst * 1024), 16, 0, 0);
-}
-
-template <bool KC>
-TT2_DEV void g6_frag(Frag8<bf16>& f, const char* img, int r0, int kk, int lane) {
+TT2_DEV void g7_frag(Frag8<bf16>& f, const char* img, int r0, int kk, int lane) {
   if (KC) frag2<true>(f, img, r0, kk, lane);
   else frag2<false>(f, img + (r0 >> 7) * 16384, r0 & 127, kk, lane);
 }
 
-template <int N> TT2_DEV void g6_wait() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else static_assert(N == 0, "g6_wait: add the count");
-}
-
-template <bool AK, bool BKC, int BN_>
-__global__ __launch_bounds__(G6_NT, 1) void gemm6_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
-                                                         int k_split, float* ws, int ntm, int ntn) {
-  using G = G6<BN_>;
-  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / G::WN, wn = wave % G::WN;
-  const int nt = ntm * ntn, bid = blockIdx.x;
-  const int q8 = nt / 8, rr = nt % 8, x = bid % 8;
-  const int tile = (x < rr ? x * (q8 + 1) : rr * (q8 + 1) + (x - rr) * q8) + bid / 8;
-  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * BN_;
-  const int kb = blockIdx.y * k_split, ke = min(K, kb + k_split);
-  const int nkt = (ke - kb + 63) / 64;
-  const bool tail = ((ke - kb) & 63) != 0;
-  const bool do_ks = !AK && E.ksum && (tile % ntn) == 0;
-  float ks[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  uint32_t oa[G::A_INST], ob[G::B_INST];
-  g6_offsets<AK>(oa, A, m0, lane, wave);
-  g6_offsets<BKC>(ob, B, n0, lane, wave);
-
-  f32x4 acc[G::MI][G::NJ];
-#pragma unroll
-  for (int i = 0; i < G::MI; ++i)
-#pragma unroll
-    for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto issue = [&](int step, int stage) {
-    char* sa = smem + stage * G::STAGE;
-    const int k0 = kb + 64 * step;
-    if (tail && step == nkt - 1) {
-      g6_issue_tail<AK>(A, oa, sa, k0, ke, lane, wave);
-      g6_issue_tail<BKC>(B, ob, sa + G::A_BYTES, k0, ke, lane, wave);
-    } else {
-      g6_issue<AK>(A, oa, sa, k0, wave);
-      g6_issue<BKC>(B, ob, sa + G::A_BYTES, k0, wave);
-    }
-  };
-#pragma unroll
-  for (int s = 0; s < G::STAGES - 1; ++s)
-    if (s < nkt) issue(s, s);
-
-  int stage = 0;
-  for (int t = 0; t < nkt; ++t) {
-    G6_STAMP(t, 0)
-    if (G::STAGES == 3 && t + 1 < nkt) g6_wait<G::INST>();
-    else g6_wait<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // last step's reads retired (WAR)
-    __builtin_amdgcn_s_barrier();   // step t landed everywhere; step t-1's stage is free
-    G6_STAMP(t, 1)
-    const bool more = t + G::STAGES - 1 < nkt;
-    const int nstep = t + G::STAGES - 1, nstage = stage == 0 ? G::STAGES - 1 : stage - 1;
-#ifdef TT2_G6_NOIL
-    if (more) issue(nstep, nstage);
+// Measurement hook: tools/gemm_stamps.hip defines these (and the buffer they write)
+// before including this file; the library build compiles them away.
+#ifndef G7_STAMP
+#define G7_STAMP(t, slot)
 #endif
-    G6_STAMP(t, 2)
-    const char* sa = smem + stage * G::STAGE;
-    const char* sb = sa + G::A_BYTES;
-    char* na = smem + nstage * G::STAGE;
-    const int nk0 = kb + 64 * nstep;
-    const bool ntl = tail && nstep == nkt - 1;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      Frag8<bf16> fa[G::MI], fb[G::NJ];
-#pragma unroll
-      for (int i = 0; i < G::MI; ++i) g6_frag<AK>(fa[i], sa, wm * G::TM + 16 * i, kk, lane);
-#pragma unroll
-      for (int j = 0; j < G::NJ; ++j) g6_frag<BKC>(fb[j], sb, wn * G::TN + 16 * j, kk, lane);
-#pragma unroll
-      for (int i = 0; i < G::MI; ++i) {
-#pragma unroll
-        for (int j = 0; j < G::NJ; ++j) mma16(fa[i], fb[j], acc[i][j]);
-#ifndef TT2_G6_NOIL
-        // the next stage's copies ride between the MFMA rows (the TA is otherwise idle
-        // while the MFMAs run): copy q goes after MFMA row floor(q * 2 MI / INST)
-        const int slot = kk * G::MI + i;
-#pragma unroll
-        for (int q = 0; q < G::INST; ++q)
-          if (q * 2 * G::MI / G::INST == slot) {
-            if (more) {
-              if (q < G::A_INST) g6_issue_one<AK>(A, oa[q], na, nk0, ke, wave * G::A_INST + q, lane, ntl);
-              else g6_issue_one<BKC>(B, ob[q - G::A_INST], na + G::A_BYTES, nk0, ke,
-                                     wave * G::B_INST + q - G::A_INST, lane, ntl);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-          }
+#ifndef G7_RT
+#define G7_RT(slot)
 #endif
-      }
-    }
-    if (!AK && do_ks) {
-      // m-chunk tid & 31 (sub-image (tid >> 4) & 1), k rows 4 * (tid >> 5) .. +3
-      const int cc = tid & 31;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kr = 4 * (tid >> 5) + r;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(sa + (cc >> 4) * 16384 + kr * 256 +
-                                                          (((cc & 15) ^ mc_swz(kr)) << 4));
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ks[j] += (float)v[j];
-      }
-    }
-    stage = stage == G::STAGES - 1 ? 0 : stage + 1;
-  }
-  G6_STAMP(nkt, 0)
-  __syncthreads();   // every wave is done with the ring
-
-  if (!AK && do_ks) {
-    float* red = reinterpret_cast<float*>(smem);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ks[j] += __shfl_xor(ks[j], 32, 64);
-    if (lane < 32) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) red[(wave * 32 + lane) * 8 + j] = ks[j];
-    }
-    __syncthreads();
-    if (tid < 256) {
-      const int cc = tid >> 3, j = tid & 7, m = m0 + tid;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) v += red[(w * 32 + cc) * 8 + j];
-      if (m < M) {
-        if (ws) ws[(int64_t)gridDim.y * M * N + (int64_t)blockIdx.y * M + m] = v;
-        else E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + v : v;
-      }
-    }
-    __syncthreads();
-  }
-
-  float* cs = reinterpret_cast<float*>(smem);
-  const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
-  constexpr int CPR = BN_ / 8;   // 8-column chunks per C row
-#pragma unroll
-  for (int p = 0; p < 256 / G::EPI_ROWS; ++p) {
-    if ((wm * G::TM) / G::EPI_ROWS == p) {
-      const int rb = wm * G::TM - p * G::EPI_ROWS;
-#pragma unroll
-      for (int i = 0; i < G::MI; ++i)
-#pragma unroll
-        for (int j = 0; j < G::NJ; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            cs[(rb + 16 * i + 4 * (lane >> 4) + r) * G::EPI_LDW + wn * G::TN + 16 * j + (lane & 15)] = acc[i][j][r];
-    }
-    __syncthreads();
-#pragma unroll 2
-    for (int it = 0; it < G::EPI_ROWS * CPR / G6_NT; ++it) {
-      const int id = tid + G6_NT * it;
-      const int row = id / CPR, c8 = (id % CPR) * 8;
-      const int m = m0 + p * G::EPI_ROWS + row, n = n0 + c8;
-      if (m >= M || n >= N) continue;
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(cs + row * G::EPI_LDW + c8);
-      const f32x4 hi = *reinterpret_cast<const f32x4*>(cs + row * G::EPI_LDW + c8 + 4);
-      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      if (ws) {
-        float* w = ws + ((int64_t)blockIdx.y * M + m) * N + n;
-        if (n + 8 <= N && (N % 4) == 0) {
-          *reinterpret_cast<f32x4*>(w) = lo;
-          *reinterpret_cast<f32x4*>(w + 4) = hi;
-        } else {
-          for (int j = 0; j < 8; ++j)
-            if (n + j < N) w[j] = v[j];
-        }
-      } else {
-        epi_store8(E, seed, m, n, N, v);
-      }
-    }
-    __syncthreads();
-  }
-  G6_STAMP(nkt, 3)
-}
-
-template <bool AK, bool BKC, int BN_>
-hipError_t launch6(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
-                   hipStream_t s) {
-  int k_split = K;
-  if (splits > 1) {
-    k_split = ((K + splits - 1) / splits + 63) / 64 * 64;
-    splits = (K + k_split - 1) / k_split;
-  }
-  const int ntm = (M + 255) / 256, ntn = (N + BN_ - 1) / BN_;
-  hipLaunchKernelGGL((gemm6_kernel<AK, BKC, BN_>), dim3(ntm * ntn, splits), dim3(G6_NT), 0, s, A, B, E, M, N, K,
-                     k_split, splits > 1 ? ws : nullptr, ntm, ntn);
-  if (splits > 1 && !E.main_only) {
-    const int64_t total = (int64_t)M * N;
-    int64_t nb = (total + 255) / 256;
-    int blocks = (int)(nb < 4096 ? nb : 4096);
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, splits, E, M, N);
-  }
-  return hipGetLastError();
-}
 
 // =====================================================================================
 // v7 (bf16, plain operands): warp-specialised 256 x 128 tile.  In v6 every wave both
@@ -1395,16 +1079,16 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
   __builtin_amdgcn_s_barrier();
   int stage = 0;
   for (int t = 0; t < nkt; ++t) {
-    G6_STAMP(t, 0)
+    G7_STAMP(t, 0)
     const char* sa = smem + stage * G7_STAGE;
     const char* sb = sa + G7_A;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       Frag8<bf16> fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) g6_frag<AK>(fa[i], sa, wm * 64 + 16 * i, kk, lane);
+      for (int i = 0; i < 4; ++i) g7_frag<AK>(fa[i], sa, wm * 64 + 16 * i, kk, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) g6_frag<BKC>(fb[j], sb, wn * 64 + 16 * j, kk, lane);
+      for (int j = 0; j < 4; ++j) g7_frag<BKC>(fb[j], sb, wn * 64 + 16 * j, kk, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1417,11 +1101,11 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
       }
     }
     stage = stage == 2 ? 0 : stage + 1;
-    G6_STAMP(t, 1)
+    G7_STAMP(t, 1)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this stage's reads retired (WAR vs the next copy)
     __builtin_amdgcn_s_barrier();
   }
-  G6_STAMP(nkt, 0)
+  G7_STAMP(nkt, 0)
 
   if (!AK && do_ks) {
 #pragma unroll
@@ -1477,7 +1161,7 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
     }
     __syncthreads();
     g7_store_c(P, smem, m0, n0);
-    G6_STAMP(nkt, 3)
+    G7_STAMP(nkt, 3)
     return;
   }
 #pragma unroll
@@ -1517,7 +1201,7 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
       }
     }
   }
-  G6_STAMP(nkt, 3)
+  G7_STAMP(nkt, 3)
 }
 
 // flat block index -> XCD-contiguous work item (blocks b and b + 8 share an XCD)
@@ -1606,8 +1290,8 @@ static bool g7_lds_epi(int variant) {
 }
 
 // Kernel selection (also exported as tt2_gemm_plan): 1 v1 register-staged, 2 v2
-// LDS-DMA 128^2, 3 skinny (M <= 64), 11 / 12 v6 256x256 / 256x128, 13 v7 warp-
-// specialised 256x128 (auto).  Returns -1 (error set) for an unsupported fusion request.
+// LDS-DMA 128^2, 3 skinny (M <= 64), 13 v7 warp-specialised 256x128 (auto; variant 14
+// forces its LDS-image epilogue, 13 its register epilogue).  Returns -1 (error set) for an unsupported fusion request.
 static int gemm_plan(const tt2_gemm_args* a) {
   const int var = a->kernel_variant;
   const int64_t a_inner = a->trans_a ? a->m : a->k, b_inner = a->trans_b ? a->n : a->k;
@@ -1641,13 +1325,10 @@ static int gemm_plan(const tt2_gemm_args* a) {
   if (a->a_ksum && !(v2 && a->trans_a && a->a_conv_t == 0))
     return tt2_set_error(TT2_E_INVALID, "tt2_gemm: a_ksum needs bf16, trans_a, no conv A, the LDS-DMA kernel"), -1;
   if (!v2) return 1;
-  // 256-row-tile kernels (v6 / v7) need per-lane byte offsets that fit 32 bits; v6
-  // plain operands only.  Auto = v7, the warp-specialised 256 x 128 kernel (fastest on
-  // every GEMM of the training step: 1.2-1.6x v2).
-  const bool v6ok = a->a_conv_t == 0 && a->b_conv_t == 0 &&
-                    (int64_t)(a->trans_a ? a->k : a->m) * a->lda * 2 < (1LL << 31) &&
-                    (int64_t)(a->trans_b ? a->k : a->n) * a->ldb * 2 < (1LL << 31);
-  if ((var == 11 || var == 12) && v6ok) return var;
+  // The 256-row-tile kernel needs per-lane byte offsets that fit 32 bits.  Auto = v7, the
+  // warp-specialised 256 x 128 kernel (fastest on every GEMM of the training step:
+  // 1.2-1.6x v2; a 256 x 256 / 256 x 128 kernel whose 8 waves both load and multiply was
+  // measured slower on every step shape and removed).
   // v7 also takes implicit-im2col operands (its loaders track tap / time per copy)
   // when every conv has C >= 64 and T >= 64 (one wrap per 64-deep K step)
   auto conv_ok = [](int t, int c) { return t == 0 || (t >= 64 && c >= 64); };
@@ -1762,16 +1443,6 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
     else if (a->trans_a && !a->trans_b) err = launch7<false, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream, le);
     else err = launch7<false, false>(A, B, ep, a->m, a->n, a->k, sp, ws, stream, le);
     return tt2_check_launch(err, "tt2_gemm(v7)");
-  }
-  if (plan == 11 || plan == 12) {
-#define TT2_G6(BN_)                                                                                           \
-    if (!a->trans_a && !a->trans_b) err = launch6<true, true, BN_>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);   \
-    else if (!a->trans_a && a->trans_b) err = launch6<true, false, BN_>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
-    else if (a->trans_a && !a->trans_b) err = launch6<false, true, BN_>(A, B, ep, a->m, a->n, a->k, sp, ws, stream); \
-    else err = launch6<false, false, BN_>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
-    if (plan == 11) { TT2_G6(256) } else { TT2_G6(128) }
-#undef TT2_G6
-    return tt2_check_launch(err, "tt2_gemm(v6)");
   }
   if (plan == 2) {
     if (!a->trans_a && !a->trans_b) err = launch2<true, true>(A, B, ep, a->m, a->n, a->k, sp, ws, stream);
