@@ -2,7 +2,7 @@
 # One GPU-box pass (run via gpurun from the repo root): GPU tests, smoke, bench, rocprof
 # kernel-trace stats of the bench step.  Every GPU step has its own time limit; the
 # steps are chained so that the first failure ends the call.
-#   tools/gpu_round.sh <tag> [tests|bench|prof ...]   (default: all three)
+#   tools/gpu_round.sh <tag> [tests|bench|prof|pmc|dpmc ...]   (default: tests bench prof)
 set -euo pipefail
 TAG=${1:-r02}
 shift || true
@@ -24,6 +24,19 @@ for s in $STEPS; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
         python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-decode \
         > "$OUT/bench_kt.json" 2> "$OUT/bench_kt.err"
+      ;;
+    pmc)   # HBM bytes of the bench step's kernels (FETCH_SIZE and WRITE_SIZE cannot share a pass)
+      ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-decode"
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
+        python3 bench.py $ARGS > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.err"
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
+        python3 bench.py $ARGS > "$OUT/bench_write.json" 2> "$OUT/bench_write.err"
+      ;;
+    dpmc)  # the same for one cfg3 decode run
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/dtr/fetch" -o run --output-format csv -- \
+        python3 tools/decode_traffic.py > "$OUT/dtr_fetch.log" 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/dtr/write" -o run --output-format csv -- \
+        python3 tools/decode_traffic.py > "$OUT/dtr_write.log" 2>&1
       ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
