@@ -678,8 +678,7 @@ extern "C" int tt2_ln_combine(const void* x, const float* part, int32_t splits, 
 }
 
 static int ln_bwd_blocks(int m) {
-  static const int cap = getenv("TT2_LNB_CAP") ? atoi(getenv("TT2_LNB_CAP")) : 256;   // dev A/B knob
-  return min(cap, (m + 15) / 16);
+  return min(256, (m + 15) / 16);   // at most one workgroup per CU, 16+ rows each
 }
 
 static LnFin ln_fin_of(const tt2_ln_args* q) {
