@@ -1270,6 +1270,165 @@ hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   return hipGetLastError();
 }
 
+// =====================================================================================
+// v8 (bf16, A K-contiguous): 64 x 64 tiles for products whose 256 x 128 tiles cannot
+// fill the chip -- the encoder's 2048-row GEMMs give v7 32-96 tiles for 256 CUs, and a
+// lone v7 tile costs ~20k cycles however few CUs are busy.  512 threads: 4 MFMA waves,
+// each one 32 x 32 block on v_mfma_f32_32x32x16_bf16 (a single f32x16 accumulator), and
+// 4 loader waves that only issue LDS-DMA copies (as in v7: a wave that both copies into
+// LDS and reads it gets a compiler-inserted vmcnt(0) before its reads, which would drain
+// the pipeline every step).  Both operand tiles (64 rows x 64 k, 8 KB each) land in a
+// 4-stage ring three K steps ahead, one s_barrier per step; 64 KB of LDS per workgroup,
+// so two share a CU.  Images are 128-B rows with
+// chunk c of row r at slot c ^ g8_swz(r) (the attention tiles' swizzle): K-contiguous
+// operands are read as row fragments (two ds_read_b64), an N-contiguous B (dgrad) by
+// ds_read_b64_tr_b16; both deliver the same permuted k order, which the MFMA sums over.
+// Operands are swapped (D = B A^T) so each lane ends with one C row; a permlane32 swap
+// gives it 8 consecutive columns, the fused epilogue runs in registers, and the tile
+// leaves through LDS as whole 128-B rows.
+// =====================================================================================
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int G8_NT = 512, G8_STAGES = 4;   // 4 MFMA waves + 4 loader waves
+constexpr int G8_TILE = 64 * 128;          // bytes per operand tile: 64 rows x 64 bf16
+constexpr int G8_STAGE = 2 * G8_TILE;
+
+TT2_DEV int g8_swz(int r) {
+  const int x = (r >> 1) & 7;
+  return ((x & 1) << 2) | (x >> 1);
+}
+
+// this wave's 2 of the 8 LDS-DMA copies of one operand tile (8 rows x 128 B each);
+// KC: tile rows are m / n and chunks run along k; MC: tile rows are k, chunks along n
+template <bool KC>
+TT2_DEV void g8_issue(const OpDesc& d, char* img, int r0, int k0, int lane, int wave) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int inst = wave * 2 + i;
+    const int row = inst * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ g8_swz(row);
+    const void* src = KC ? chunk_src(d, r0 + row, k0 + c * 8) : chunk_src(d, k0 + row, r0 + c * 8);
+    __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(img + inst * 1024), 16, 0, 0);
+  }
+}
+
+// K-contiguous fragment of row `row`, k slice s (16 k): element j holds
+// k = 16 s + 8 (j >> 2) + 4 hi + (j & 3), the order the transposed read delivers
+TT2_DEV bf16x8 g8_frag_kc(const char* img, int row, int s, int hi) {
+  const char* r = img + row * 128 + 8 * hi;
+  const uint2 lo = *reinterpret_cast<const uint2*>(r + (((2 * s) ^ g8_swz(row)) << 4));
+  const uint2 up = *reinterpret_cast<const uint2*>(r + (((2 * s + 1) ^ g8_swz(row)) << 4));
+  union { uint4 u; bf16x8 v; } x;
+  x.u = make_uint4(lo.x, lo.y, up.x, up.y);
+  return x.v;
+}
+
+// N-contiguous fragment (image rows = k): column col0 + (lane & 31), same k order
+TT2_DEV bf16x8 g8_frag_mc(const char* img, int col0, int s, int lane) {
+  typedef __attribute__((address_space(3))) short4v lds_s4;
+  const int hi = lane >> 5, q = (lane >> 2) & 3, p = lane & 3, g = (lane >> 4) & 1;
+  const int col = col0 + 16 * g + 4 * p;
+  const int r0 = 16 * s + 4 * hi + q;
+  auto at = [&](int r) { return img + r * 128 + ((((col >> 3) ^ g8_swz(r))) << 4) + (col & 7) * 2; };
+  short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)at(r0));
+  short4v up = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)at(r0 + 8));
+  union { short4v s[2]; bf16x8 v; } u;
+  u.s[0] = lo;
+  u.s[1] = up;
+  return u.v;
+}
+
+template <bool BKC>
+__global__ __launch_bounds__(G8_NT, 2) void gemm8_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
+                                                         int ntn, int items) {
+  __shared__ __attribute__((aligned(1024))) char smem[G8_STAGES * G8_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5;
+  const int tile = xcd_item(blockIdx.x, items);
+  const int m0 = (tile / ntn) * 64, n0 = (tile % ntn) * 64;
+  const int nkt = (K + 63) / 64;
+  if (wave >= 4) {   // ---------------------------------------------- loader waves
+    const int lw = wave - 4;
+    auto issue = [&](int t) {
+      char* st = smem + (t & (G8_STAGES - 1)) * G8_STAGE;
+      g8_issue<true>(A, st, m0, 64 * t, lane, lw);
+      g8_issue<BKC>(B, st + G8_TILE, n0, 64 * t, lane, lw);
+    };
+    // three steps ahead; each step is 4 copies per loader wave
+    for (int t = 0; t < 3 && t < nkt; ++t) issue(t);
+    if (nkt >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (nkt == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int t = 0; t < nkt; ++t) {
+      if (t + 3 < nkt) issue(t + 3);   // into the stage step t-1 used: free since the last barrier
+      const int ahead = min(2, nkt - 2 - t);   // steps after t+1 that may stay in flight
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();    // step t+1 landed
+    }
+  } else {   // ------------------------------------------------------- MFMA waves
+    const int wm = wave >> 1, wn = wave & 1;
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    __builtin_amdgcn_s_barrier();
+    for (int t = 0; t < nkt; ++t) {
+      const char* sa = smem + (t & (G8_STAGES - 1)) * G8_STAGE;
+      const char* sb = sa + G8_TILE;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 fa = g8_frag_kc(sa, wm * 32 + (lane & 31), s, hi);
+        const bf16x8 fb = BKC ? g8_frag_kc(sb, wn * 32 + (lane & 31), s, hi) : g8_frag_mc(sb, wn * 32, s, lane);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb, fa, acc, 0, 0, 0);   // D[n][m]
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this stage's reads retired before it is re-filled
+      __builtin_amdgcn_s_barrier();
+    }
+    // lane holds C[m0 + 32 wm + (lane & 31)][n0 + 32 wn + (r & 3) + 8 (r >> 2) + 4 hi]; the
+    // permlane32 swap of register groups (0,1) and (2,3) leaves 8 consecutive columns per lane.
+    // The ring is free (every wave passed the last barrier): it takes the C image [64][128 B].
+    const int r = wm * 32 + (lane & 31), m = m0 + r;
+    const uint32_t seed = E.drop.thr ? *E.drop.seed : 0u;
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[8 * pr + i]),
+                                                         __float_as_uint(acc[8 * pr + 4 + i]), false, false);
+        v[i] = __uint_as_float(sw[0]);
+        v[4 + i] = __uint_as_float(sw[1]);
+      }
+      const int cl = wn * 32 + 16 * pr + 8 * hi, n = n0 + cl;
+      if (m >= M || n >= N) continue;
+      float o[8];
+      epi_calc8(E, seed, m, n, v, false, o);
+      bf16x8 x;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = (bf16)o[j];
+      *reinterpret_cast<bf16x8*>(smem + r * 128 + (((cl >> 3) ^ g8_swz(r)) << 4)) = x;
+    }
+  }
+  __syncthreads();   // the C image is complete: all 8 waves store whole 128-B rows
+  bf16* C = reinterpret_cast<bf16*>(E.c);
+  const int id = tid, rr = id >> 3, c = id & 7, mm = m0 + rr, nn = n0 + 8 * c;
+  if (mm < M && nn < N)
+    *reinterpret_cast<bf16x8*>(C + (int64_t)mm * E.ldc + nn) =
+        *reinterpret_cast<const bf16x8*>(smem + rr * 128 + ((c ^ g8_swz(rr)) << 4));
+}
+
+template <bool BKC>
+hipError_t launch8(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, hipStream_t s) {
+  const int ntn = (N + 63) / 64, items = ((M + 63) / 64) * ntn;
+  hipEvent_t e0, e1;
+  if (probe_take(e0, e1))
+    hipExtLaunchKernelGGL((gemm8_kernel<BKC>), dim3(items), dim3(G8_NT), 0, s, e0, e1, 0, A, B, E, M, N, K, ntn,
+                          items);
+  else
+    hipLaunchKernelGGL((gemm8_kernel<BKC>), dim3(items), dim3(G8_NT), 0, s, A, B, E, M, N, K, ntn, items);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" size_t tt2_gemm_workspace_size(const tt2_gemm_args* a) {
@@ -1335,6 +1494,14 @@ static int gemm_plan(const tt2_gemm_args* a) {
   const bool v7ok = conv_ok(a->a_conv_t, a->a_conv_c) && conv_ok(a->b_conv_t, a->b_conv_c) &&
                     (int64_t)(a->trans_a ? a->k : a->m) * a->lda * 2 < (1LL << 31) &&
                     (int64_t)(a->trans_b ? a->k : a->n) * a->ldb * 2 < (1LL << 31);
+  // v8 (64 x 64 tiles): K-contiguous A (conv allowed), no k-sums, bf16 C; forced by variant 15
+  const bool v8ok = !a->trans_a && !a->a_ksum && a->b_conv_t == 0 && a->dtype_out == TT2_BF16 && a->n % 8 == 0 &&
+                    (int64_t)a->m * a->lda * 2 < (1LL << 31) &&
+                    (int64_t)(a->trans_b ? a->k : a->n) * a->ldb * 2 < (1LL << 31);
+  // auto: v8 when v7 would run at most 64 tiles (the encoder's 2048-row products with N = 512,
+  // the post-net's 80-channel conv): 1.4-1.6x v7 there, slower once v7 has >= 96 tiles
+  const int64_t tiles7 = (int64_t)((a->m + 255) / 256) * ((a->n + 127) / 128);
+  if (v8ok && a->m >= 64 && (var == 15 || (var == 0 && tiles7 <= 64))) return 15;
   if ((var == 13 || var == 14 || var == 0) && v7ok) return 13;
   return 2;
 }
@@ -1399,8 +1566,13 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   const int sp = a->splits > 1 ? a->splits : 1;
 
   hipError_t err;
-  const int plan = gemm_plan(a);
+  int plan = gemm_plan(a);
   if (plan < 0) return TT2_E_INVALID;   // message already set
+  if (plan == 15 && !ep.vec) {          // v8 stores C in 16-B chunks: unaligned rows take v7 (or v2)
+    tt2_gemm_args b = *a;
+    b.kernel_variant = 13;
+    plan = gemm_plan(&b);
+  }
   if (plan == 3) {   // skinny-M weight-streaming path (decode step)
     SkinnyFuse F{reinterpret_cast<const bf16*>(a->a_ln_branch), a->a_ln_gamma, a->a_ln_beta,
                  reinterpret_cast<bf16*>(a->a_ln_out), a->a_ln_eps, a->kv_cache, a->kv_t,
@@ -1435,6 +1607,11 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
 #undef TT2_SK_M
 #undef TT2_SK
     return tt2_check_launch(hipGetLastError(), "tt2_gemm(skinny)");
+  }
+  if (plan == 15) {
+    if (!a->trans_b) err = launch8<true>(A, B, ep, a->m, a->n, a->k, stream);
+    else err = launch8<false>(A, B, ep, a->m, a->n, a->k, stream);
+    return tt2_check_launch(err, "tt2_gemm(v8)");
   }
   if (plan == 13) {
     const bool le = g7_lds_epi(a->kernel_variant);
