@@ -1685,9 +1685,11 @@ extern "C" int tt2_gemm_grouped(const tt2_gemm_args* probs, int n, hipStream_t s
 }
 
 extern "C" int tt2_probe_arm(void) {
+  // timing-only events: no system-scope fence (cache write-back) at the probed kernel's end,
+  // which would lengthen it beyond what it takes inside the step
   ProbeSlot p{nullptr, nullptr, false};
-  hipError_t e = hipEventCreate(&p.start);
-  if (e == hipSuccess) e = hipEventCreate(&p.stop);
+  hipError_t e = hipEventCreateWithFlags(&p.start, hipEventDisableSystemFence);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&p.stop, hipEventDisableSystemFence);
   if (e != hipSuccess) return tt2_check_launch(e, "tt2_probe_arm");
   g_probe.push_back(p);
   g_probe_armed = (int)g_probe.size() - 1;
