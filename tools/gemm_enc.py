@@ -34,7 +34,11 @@ SHAPES = [  # name, m, n, k, trans_b
     ("ffn2 fwd", 2048, 512, 2048, False), ("mkv fwd", 2048, 6144, 512, False),
     ("qkv dgrad", 2048, 512, 1536, True), ("o dgrad", 2048, 512, 512, True), ("ffn1 dgrad", 2048, 512, 2048, True),
     ("ffn2 dgrad", 2048, 2048, 512, True), ("dec o fwd", 12800, 512, 512, False),
+    ("pre fc1", 12800, 256, 80, False), ("pre fc2", 12800, 256, 256, False), ("pre proj", 12800, 512, 256, False),
+    ("fc2 dgrad", 12800, 256, 256, True), ("proj dgrad", 12800, 256, 512, True),
 ]
+if os.environ.get("ONLY_NEW"):
+    SHAPES = SHAPES[-5:]
 variants = [int(v) for v in sys.argv[1:]] or [2, 13]
 ws = ops.Workspace() if hasattr(ops, "Workspace") else None
 for name, m, n, k, tb in SHAPES:
