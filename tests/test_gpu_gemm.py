@@ -69,6 +69,35 @@ def test_gemm_epilogue(dtype, variant, n, splits):
     assert rel(out, ref) < tol
 
 
+@pytest.mark.parametrize("variant", [0, 13, 14])
+@pytest.mark.parametrize("k", [64, 128, 192, 520])
+@pytest.mark.parametrize("tile_op", ["res", "gate", "none"])
+def test_gemm_epilogue_staged(variant, k, tile_op):
+    """v7 with the loader waves hashing the dropout bits and staging the residual / gate
+    tile in LDS (K steps 1, 2, 3 and 9: every stage hand-off of the staged image), ragged
+    M and N edges."""
+    m, n = 520, 264
+    g = torch.Generator().manual_seed(k + len(tile_op))
+    A, B = _mk((m, k), torch.bfloat16, g), _mk((n, k), torch.bfloat16, g)
+    bias = torch.randn(n, generator=g).cuda()
+    X = _mk((m, n), torch.bfloat16, g)
+    seed = torch.tensor([99], dtype=torch.int32).cuda()
+    out = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+    kw = dict(res=X, ldr=n) if tile_op == "res" else (dict(gate=X.relu(), ldg=n, gate_scale=1.3)
+                                                     if tile_op == "gate" else {})
+    ops.gemm(A, B, out, m, n, k, k, k, n, bias=bias, act=ops._lib.ACT_RELU, drop=ops.Drop(seed, 5, 0.25),
+             variant=variant, **kw)
+    ref = A.double() @ B.double().t() + bias.double()
+    if tile_op == "res":
+        ref = ref + X.double()
+    ref = ref.relu()
+    if tile_op == "gate":
+        ref = ref * (X.double().relu() != 0) * 1.3
+    keep = torch.from_numpy(dropout_keep(99, 5, m * n, 0.25)).view(m, n).cuda()
+    ref = ref * keep / 0.75
+    assert rel(out, ref) < 8e-3
+
+
 @pytest.mark.parametrize("dtype,variant", VARIANTS)
 def test_gemm_splitk_tanh_beta(dtype, variant):
     m, n, k = 160, 96, 1000

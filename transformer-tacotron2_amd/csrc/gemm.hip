@@ -359,8 +359,15 @@ TT2_DEV void ld8_any(const void* p, int64_t off, int dt, float (&o)[8]) {
 // per chunk; edge chunks fall back to the per-element path.
 // pre_b: alpha and bias were already applied to v (v7's prefetched bias; E.vec, full chunk)
 // Vectorised chunk epilogue without the store: o = epi(v) for a full, aligned chunk (E.vec).
+// res_l / gate_l: the chunk of a bf16 residual / gate already staged in LDS by v7's loader
+// waves.
+TT2_DEV void unpack_lds8(const void* p, float (&t)[8]) {
+  const bf16x8 x = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t[j] = (float)x[j];
+}
 TT2_DEV void epi_calc8(const EpiParams& E, uint32_t seed, int m, int n0, const float (&v)[8], bool pre_b,
-                       float (&o)[8]) {
+                       float (&o)[8], const void* res_l = nullptr, const void* gate_l = nullptr) {
   const int64_t off = (int64_t)m * E.ldc + n0;
   float t[8];
 #pragma unroll
@@ -371,7 +378,8 @@ TT2_DEV void epi_calc8(const EpiParams& E, uint32_t seed, int m, int n0, const f
     for (int j = 0; j < 4; ++j) { o[j] += a[j]; o[4 + j] += b[j]; }
   }
   if (E.res) {
-    ld8_any(E.res, (int64_t)m * E.ldr + n0, E.res_dt, t);
+    if (res_l) unpack_lds8(res_l, t);
+    else ld8_any(E.res, (int64_t)m * E.ldr + n0, E.res_dt, t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] += t[j];
   }
@@ -383,7 +391,8 @@ TT2_DEV void epi_calc8(const EpiParams& E, uint32_t seed, int m, int n0, const f
     for (int j = 0; j < 8; ++j) o[j] = tanhf(o[j]);
   }
   if (E.gate) {
-    ld8_any(E.gate, (int64_t)m * E.ldg + n0, E.gate_dt, t);
+    if (gate_l) unpack_lds8(gate_l, t);
+    else ld8_any(E.gate, (int64_t)m * E.ldg + n0, E.gate_dt, t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = t[j] != 0.f ? o[j] * E.gate_scale : 0.f;
   }
@@ -899,6 +908,7 @@ constexpr int G7_A = 256 * 128, G7_B = 128 * 128;   // bytes per stage: 64 k x 2
 constexpr int G7_STAGE = G7_A + G7_B;               // 48 KB
 constexpr int G7_STAGES = 3;
 constexpr int G7_AI = G7_A / 1024 / 4, G7_BI = G7_B / 1024 / 4;   // copies per loader wave: 8 + 4
+constexpr int G7_SMEM = G7_STAGES * G7_STAGE;
 
 // Loader-lane state of one operand (NI copies per step).  Plain operands: a loop-
 // invariant byte offset from a wave-uniform base.  Conv operands (implicit im2col,
@@ -988,6 +998,7 @@ struct G7Prob {
   int M, N, K, k_split, splits, ntn, items, item0;
   float* ws;   // split-K slabs [splits][M][N] (+ [splits][M] k-sums); used when splits > 1
   int lds_epi; // C leaves through an LDS image in whole 256-B row segments (bf16 C, no split)
+  int pre_x;     // the loader waves stage the bf16 residual (1) or gate (2) tile in LDS (lds_epi only)
 };
 constexpr int G7_MAXP = 8;
 struct G7Group {
@@ -995,14 +1006,35 @@ struct G7Group {
   int np, items;
 };
 
+// The epilogue's 256-row image (C, and before it the staged residual / gate in place):
+// rows 0..191 fill the ring stage of K step nkt - 3 (the first stage that no later step
+// reuses), rows 192..255 the stage of step nkt - 2, so the staged tile can land while the
+// last K steps still read the third stage.  Chunk c of row r sits at slot c ^ (r & 15).
+TT2_DEV int g7_img_row(int nkt, int r) {
+  return r < 192 ? (nkt % 3) * G7_STAGE + r * 256 : ((nkt + 1) % 3) * G7_STAGE + (r - 192) * 256;
+}
+
 // whole-row store of the LDS C image (all 768 threads; 4 rows x 256 B per wave instruction)
-TT2_DEV void g7_store_c(const G7Prob& P, const char* smem, int m0, int n0) {
+TT2_DEV void g7_store_c(const G7Prob& P, const char* smem, int m0, int n0, int nkt) {
   bf16* C = reinterpret_cast<bf16*>(P.E.c);
   for (int id = threadIdx.x; id < 256 * 16; id += G7_NT) {
     const int r = id >> 4, c = id & 15, m = m0 + r, n = n0 + 8 * c;
     if (m < P.M && n < P.N)
       *reinterpret_cast<bf16x8*>(C + (int64_t)m * P.E.ldc + n) =
-          *reinterpret_cast<const bf16x8*>(smem + r * 256 + ((c ^ (r & 15)) << 4));
+          *reinterpret_cast<const bf16x8*>(smem + g7_img_row(nkt, r) + ((c ^ (r & 15)) << 4));
+  }
+}
+
+// Loader waves: stage rows [r0, r0 + 4 * ni * 4) of the residual / gate tile (bf16, 16-B
+// aligned rows) into the image, ni copies per wave (rows past M repeat row M - 1).
+TT2_DEV void g7_issue_x(const G7Prob& P, const void* x, int64_t ldx, char* smem, int nkt, int m0, int n0, int r0,
+                        int ni, int lane, int lw) {
+  const char* base = reinterpret_cast<const char*>(x);
+  for (int i = 0; i < ni; ++i) {
+    const int inst = lw * ni + i, r = r0 + inst * 4 + (lane >> 4);
+    const int m = min(m0 + r, P.M - 1), c = (lane & 15) ^ (r & 15);
+    __builtin_amdgcn_global_load_lds((gvoid_t*)(base + ((int64_t)m * ldx + n0 + 8 * c) * 2),
+                                     (lvoid_t*)(smem + g7_img_row(nkt, r0 + inst * 4)), 16, 0, 0);
   }
 }
 
@@ -1031,6 +1063,10 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
       g7_issue<AK>(A, la, sa, k0, ke, lane, lw, tl);
       g7_issue<BKC>(B, lb, sa + G7_A, k0, ke, lane, lw, tl);
     };
+    // staged epilogue operand (whole tiles only)
+    const bool px = P.pre_x && n0 + 128 <= N;
+    const void* xs = P.pre_x == 1 ? E.res : E.gate;
+    const int64_t ldx = P.pre_x == 1 ? E.ldr : E.ldg;
     issue(0, 0);
     if (nkt > 1) { issue(1, 1); asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); }
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1040,15 +1076,24 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
       if (t + 2 < nkt) {
         issue(t + 2, st);
         st = st == 2 ? 0 : st + 1;
-        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // step t+1 landed, t+2 in flight
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (px) {
+        // rows 0..191 once the stage of step nkt - 3 is free, rows 192..255 a step later
+        if (t == nkt - 2 || nkt == 1) g7_issue_x(P, xs, ldx, smem, nkt, m0, n0, 0, 12, lane, lw);
+        if (t == nkt - 1) g7_issue_x(P, xs, ldx, smem, nkt, m0, n0, 192, 4, lane, lw);
       }
+      if (t + 2 < nkt || (px && t == nkt - 2))
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // step t+1 landed; t+2 (or the staged rows) in flight
+      else if (!px)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    if (px) {   // the staged tile has landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
     if (!P.lds_epi) return;
     __syncthreads();   // the MFMA waves' C image is in LDS
-    g7_store_c(P, smem, m0, n0);
+    g7_store_c(P, smem, m0, n0, nkt);
     return;
   }
 
@@ -1124,6 +1169,8 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
   // column blocks (2p, 2p+1) between row pairs q, q^1 leaves 8 consecutive columns per lane
   const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
   const int q = ql;
+  const bool px = P.pre_x && n0 + 128 <= N;
+  if (px) __builtin_amdgcn_s_barrier();   // the loaders' staged residual / gate tile has landed
   if (P.lds_epi) {
     // epilogue values -> bf16 C image [256 rows][16 chunks of 16 B] (chunk c of row r at
     // c ^ (r & 15): the 16 rows of one store instruction hit 16 different bank groups),
@@ -1152,15 +1199,16 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
           }
         }
         float o[8];
-        epi_calc8(E, seed, m, n, v, pre_b, o);
+        char* cp = smem + g7_img_row(nkt, r) + (((cl >> 3) ^ (r & 15)) << 4);   // C overwrites the staged chunk
+        epi_calc8(E, seed, m, n, v, pre_b, o, px && P.pre_x == 1 ? cp : nullptr, px && P.pre_x == 2 ? cp : nullptr);
         bf16x8 x;
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = (bf16)o[j];
-        *reinterpret_cast<bf16x8*>(smem + r * 256 + (((cl >> 3) ^ (r & 15)) << 4)) = x;
+        *reinterpret_cast<bf16x8*>(cp) = x;
       }
     }
     __syncthreads();
-    g7_store_c(P, smem, m0, n0);
+    g7_store_c(P, smem, m0, n0, nkt);
     G7_STAMP(nkt, 3)
     return;
   }
@@ -1212,7 +1260,7 @@ TT2_DEV int xcd_item(int bid, int n) {
 
 template <bool AK, bool BKC>
 __global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(G7Prob P) {
-  __shared__ __attribute__((aligned(1024))) char smem[G7_STAGES * G7_STAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[G7_SMEM];
   G7_RT(0)
   const int u = xcd_item(blockIdx.x, P.items);
   g7_item<AK, BKC>(P, u % (P.items / P.splits), u / (P.items / P.splits), smem);
@@ -1223,7 +1271,7 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(G7Prob P) {
 // gradients of a layer, which share K = tokens), one workgroup per work item.
 template <bool AK, bool BKC>
 __global__ __launch_bounds__(G7_NT, 1) void gemm7g_kernel(G7Group G) {
-  __shared__ __attribute__((aligned(1024))) char smem[G7_STAGES * G7_STAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[G7_SMEM];
   const int u = xcd_item(blockIdx.x, G.items);
   int p = 0;
 #pragma unroll
@@ -1242,7 +1290,7 @@ __global__ void gemm_splitk_reduce_g(G7Group G) {
 
 G7Prob g7_prob(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits,
                             float* ws) {
-  G7Prob P{A, B, E, M, N, K, K, 1, (N + 127) / 128, 0, 0, ws, 0};
+  G7Prob P{A, B, E, M, N, K, K, 1, (N + 127) / 128, 0, 0, ws, 0, 0};
   if (splits > 1) {
     P.k_split = ((K + splits - 1) / splits + 63) / 64 * 64;
     P.splits = (K + P.k_split - 1) / P.k_split;
@@ -1251,11 +1299,22 @@ G7Prob g7_prob(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int 
   return P;
 }
 
+// loader-wave residual / gate staging (TT2_G7_PRE=0: the epilogue loads them itself; a
+// measurement switch, default on)
+bool g7_pre_on() {
+  static const bool on = [] {
+    const char* e = getenv("TT2_G7_PRE");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
 template <bool AK, bool BKC>
 hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
                    hipStream_t s, bool lds_epi) {
   G7Prob P = g7_prob(A, B, E, M, N, K, splits, ws);
   P.lds_epi = lds_epi && P.splits == 1 && E.c_dt == TT2_BF16 && E.vec && (N % 8) == 0;
+  P.pre_x = !P.lds_epi || !g7_pre_on() ? 0 : (E.res && E.res_dt == TT2_BF16) ? 1 : (E.gate && E.gate_dt == TT2_BF16) ? 2 : 0;
   hipEvent_t e0, e1;
   if (probe_take(e0, e1))
     hipExtLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, e0, e1, 0, P);
