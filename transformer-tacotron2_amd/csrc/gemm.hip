@@ -1115,7 +1115,14 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
       pbias[pr][1] = *reinterpret_cast<const f32x4*>(E.bias + n + 4);
     }
   }
-  float ks[4] = {0.f, 0.f, 0.f, 0.f};
+  // k-sums on the matrix core: an all-ones B fragment makes D[n][m] = sum_k A[m][k] (one
+  // extra MFMA per A fragment; summing the fragments on the VALU stalled the K loop)
+  f32x4 ksa[4];
+  Frag8<bf16> fones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) fones.v[e] = (bf16)1.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ksa[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -1140,9 +1147,7 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
         for (int j = 0; j < 4; ++j) mma16(fb[j], fa[i], acc[i][j]);   // D[n][m]
       if (!AK && do_ks) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) ks[i] += (float)fa[i].v[e];
+        for (int i = 0; i < 4; ++i) mma16(fones, fa[i], ksa[i]);
       }
     }
     stage = stage == 2 ? 0 : stage + 1;
@@ -1155,12 +1160,11 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
   if (!AK && do_ks) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      ks[i] += __shfl_xor(ks[i], 16, 64);
-      ks[i] += __shfl_xor(ks[i], 32, 64);
+      const float ks = ksa[i][0];   // every lane of the row's column (lane & 15) holds it
       const int m = m0 + wm * 64 + 16 * i + lane;
       if (lane < 16 && m < M) {
-        if (ws) ws[(int64_t)P.splits * M * N + (int64_t)split * M + m] = ks[i];
-        else E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + ks[i] : ks[i];
+        if (ws) ws[(int64_t)P.splits * M * N + (int64_t)split * M + m] = ks;
+        else E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + ks : ks;
       }
     }
   }
