@@ -1014,14 +1014,18 @@ TT2_DEV int g7_img_row(int nkt, int r) {
   return r < 192 ? (nkt % 3) * G7_STAGE + r * 256 : ((nkt + 1) % 3) * G7_STAGE + (r - 192) * 256;
 }
 
-// whole-row store of the LDS C image (all 768 threads; 4 rows x 256 B per wave instruction)
+// whole-row store of the LDS C image (all 768 threads; 4 rows x 256 B per wave instruction).
+// Nontemporal: C streams out during the epilogue instead of sitting dirty in L2 until the
+// end-of-kernel write-back (the consumer kernel reads it from the Infinity Cache either way).
 TT2_DEV void g7_store_c(const G7Prob& P, const char* smem, int m0, int n0, int nkt) {
   bf16* C = reinterpret_cast<bf16*>(P.E.c);
   for (int id = threadIdx.x; id < 256 * 16; id += G7_NT) {
     const int r = id >> 4, c = id & 15, m = m0 + r, n = n0 + 8 * c;
-    if (m < P.M && n < P.N)
-      *reinterpret_cast<bf16x8*>(C + (int64_t)m * P.E.ldc + n) =
-          *reinterpret_cast<const bf16x8*>(smem + g7_img_row(nkt, r) + ((c ^ (r & 15)) << 4));
+    if (m < P.M && n < P.N) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(smem + g7_img_row(nkt, r) + ((c ^ (r & 15)) << 4));
+      u32x4* dst = reinterpret_cast<u32x4*>(C + (int64_t)m * P.E.ldc + n);
+      __builtin_nontemporal_store(v, dst);
+    }
   }
 }
 
@@ -1475,9 +1479,9 @@ __global__ __launch_bounds__(G8_NT, 2) void gemm8_kernel(OpDesc A, OpDesc B, Epi
   __syncthreads();   // the C image is complete: all 8 waves store whole 128-B rows
   bf16* C = reinterpret_cast<bf16*>(E.c);
   const int id = tid, rr = id >> 3, c = id & 7, mm = m0 + rr, nn = n0 + 8 * c;
-  if (mm < M && nn < N)
-    *reinterpret_cast<bf16x8*>(C + (int64_t)mm * E.ldc + nn) =
-        *reinterpret_cast<const bf16x8*>(smem + rr * 128 + ((c ^ g8_swz(rr)) << 4));
+  if (mm < M && nn < N)   // nontemporal, as v7's C (g7_store_c)
+    __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(smem + rr * 128 + ((c ^ g8_swz(rr)) << 4)),
+                                reinterpret_cast<u32x4*>(C + (int64_t)mm * E.ldc + nn));
 }
 
 template <bool BKC>

@@ -57,6 +57,19 @@ template <> TT2_DEV void st8(float* p, const float (&v)[8]) {
   *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
   *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
 }
+// Nontemporal form for the training kernels' full-tensor outputs: the rows stream out as
+// they are produced instead of sitting dirty in L2 until the end-of-kernel write-back.
+template <typename T> TT2_DEV void st8nt(T* p, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 4) {
+    __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f32x4*>(p));
+    __builtin_nontemporal_store(f32x4{v[4], v[5], v[6], v[7]}, reinterpret_cast<f32x4*>(p) + 1);
+  } else {
+    T x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = (T)v[j];
+    __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(x), reinterpret_cast<u32x4*>(p));
+  }
+}
 
 // --------------------------------------------------------------- LayerNorm
 // A deferred LayerNorm-backward finalize: column sums of part[nb][3][C] into (dg, db, dd).
@@ -133,7 +146,7 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(LnArgs a) {
     y[j] = (s[j] - mean) * rstd * g0[j] + b0[j];
     y[4 + j] = (s[4 + j] - mean) * rstd * g1[j] + b1[j];
   }
-  st8(reinterpret_cast<T*>(a.y) + off, y);
+  st8nt(reinterpret_cast<T*>(a.y) + off, y);
   if (lane == 0 && a.mean) { a.mean[row] = mean; a.rstd[row] = rstd; }
 }
 
@@ -283,8 +296,8 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
       db[j] = ds[j] * keep[j];
       pd[j] += db[j];
     }
-    st8(reinterpret_cast<T*>(a.dx) + off, ds);
-    if (a.dbranch) st8(reinterpret_cast<T*>(a.dbranch) + off, db);
+    st8nt(reinterpret_cast<T*>(a.dx) + off, ds);
+    if (a.dbranch) st8nt(reinterpret_cast<T*>(a.dbranch) + off, db);
     cur = nxt;
   }
   // 8 waves -> 4 rows of LDS partials -> 1
@@ -517,8 +530,8 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) z[j] += r[j];
     }
-    if (a.out_dt == TT2_BF16) st8(reinterpret_cast<bf16*>(a.out) + i0, z);
-    else st8(reinterpret_cast<float*>(a.out) + i0, z);
+    if (a.out_dt == TT2_BF16) st8nt(reinterpret_cast<bf16*>(a.out) + i0, z);
+    else st8nt(reinterpret_cast<float*>(a.out) + i0, z);
   }
 }
 
@@ -625,7 +638,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
       const float dp = bn_dpre(a, seed, (uint32_t)(i0 + j), xh, g[j], b[j], d[j]);
       o[j] = a.training ? g[j] * rs[j] * (dp - db[j] * invM - xh * dg[j] * invM) : g[j] * rs[j] * dp;
     }
-    st8(reinterpret_cast<T*>(a.dy) + i0, o);
+    st8nt(reinterpret_cast<T*>(a.dy) + i0, o);
   }
 }
 

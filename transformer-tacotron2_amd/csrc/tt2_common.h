@@ -15,6 +15,7 @@ typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16;   // the fp16 decode path
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
