@@ -422,15 +422,18 @@ __global__ __launch_bounds__(NT) void adam_kernel(AdamArgs a) {
       vo[j] = a.beta2 * v[j] + (1.f - a.beta2) * gj * gj;
       po[j] = pj - step_size * mo[j] / (sqrtf(vo[j]) / bc2_sqrt + a.eps);
     }
-    reinterpret_cast<f32x4*>(a.p)[i] = po;
-    reinterpret_cast<f32x4*>(a.m)[i] = mo;
-    reinterpret_cast<f32x4*>(a.v)[i] = vo;
+    // nontemporal: every lane's 16 B (8 B for the shadow) continue its neighbours' into
+    // whole lines, which stream to memory instead of being written back at the kernel's end
+    __builtin_nontemporal_store(po, reinterpret_cast<f32x4*>(a.p) + i);
+    __builtin_nontemporal_store(mo, reinterpret_cast<f32x4*>(a.m) + i);
+    __builtin_nontemporal_store(vo, reinterpret_cast<f32x4*>(a.v) + i);
     if (a.shadow) {
       typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
       bf16x4 sh;
 #pragma unroll
       for (int j = 0; j < 4; ++j) sh[j] = (bf16)po[j];
-      reinterpret_cast<bf16x4*>(a.shadow)[i] = sh;
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x2*>(&sh), reinterpret_cast<u32x2*>(a.shadow) + i);
     }
   }
   for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)NT + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * NT)
