@@ -920,7 +920,13 @@ constexpr int G7_SMEM = G7_STAGES * G7_STAGE;
 template <int NI> struct G7Lane {
   uint32_t off[NI];
   int t[NI], tap[NI], ci[NI];
+  uint32_t vm[NI];   // K-contiguous conv operand with C % 64 == 0: bit tap = row t + tap - pad is inside [0, T)
 };
+
+// A K-contiguous conv operand whose channel count is a multiple of 64 keeps every 64-deep K
+// step inside one tap, so a copy's validity is one bit of a per-row tap mask (no per-step
+// coordinate tracking on the loader waves, whose VALU work slows the MFMA waves' K loop).
+TT2_DEV bool g7_conv_fast(const OpDesc& d) { return d.conv_t > 0 && (d.conv_c & 63) == 0; }
 
 template <bool KC, int NI>
 TT2_DEV void g7_lane_init(G7Lane<NI>& L, const OpDesc& d, int r0, int kb, int lane, int lw) {
@@ -937,6 +943,8 @@ TT2_DEV void g7_lane_init(G7Lane<NI>& L, const OpDesc& d, int r0, int kb, int la
         L.t[i] = r % d.conv_t;
         L.tap[i] = k / d.conv_c;
         L.ci[i] = k - L.tap[i] * d.conv_c;
+        const int lo = max(0, d.conv_pad - L.t[i]), hi = min(31, d.conv_t - 1 - L.t[i] + d.conv_pad);
+        L.vm[i] = hi >= lo ? (0xFFFFFFFFu >> (31 - hi)) & (0xFFFFFFFFu << lo) : 0u;   // taps lo..hi
       }
     } else {
       const int sub = inst >> 4, kr = (inst & 15) * 4 + (lane >> 4);
@@ -954,7 +962,8 @@ TT2_DEV void g7_lane_init(G7Lane<NI>& L, const OpDesc& d, int r0, int kb, int la
 }
 
 template <bool KC, int NI>
-TT2_DEV void g7_issue(const OpDesc& d, G7Lane<NI>& L, char* lds, int k0, int ke, int lane, int lw, bool tl) {
+TT2_DEV void g7_issue(const OpDesc& d, G7Lane<NI>& L, char* lds, int k0, int ke, int lane, int lw, bool tl,
+                      bool cfast) {
   const bool conv = d.conv_t > 0;
   const int64_t shift = conv ? (int64_t)d.conv_pad * d.conv_c : 0;
   const char* base = reinterpret_cast<const char*>(d.p) + ((KC ? (int64_t)k0 : (int64_t)k0 * d.ld) - shift) * 2;
@@ -963,6 +972,15 @@ TT2_DEV void g7_issue(const OpDesc& d, G7Lane<NI>& L, char* lds, int k0, int ke,
     for (int i = 0; i < NI; ++i)
       __builtin_amdgcn_global_load_lds((gvoid_t*)(base + L.off[i]), (lvoid_t*)(lds + (lw * NI + i) * 1024), 16, 0,
                                        0);
+    return;
+  }
+  if (KC && cfast) {   // the whole step reads tap k0 / C
+    const int tap = k0 / d.conv_c;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const void* src = (L.vm[i] >> tap) & 1u ? (const void*)(base + L.off[i]) : (const void*)g_zero_page;
+      __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(lds + (lw * NI + i) * 1024), 16, 0, 0);
+    }
     return;
   }
 #pragma unroll
@@ -1058,14 +1076,15 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
     const int lw = wave - 8;
     G7Lane<G7_AI> la;
     G7Lane<G7_BI> lb;
+    const bool cfast_a = g7_conv_fast(A) && !tail, cfast_b = g7_conv_fast(B) && !tail;
     g7_lane_init<AK>(la, A, m0, kb, lane, lw);
     g7_lane_init<BKC>(lb, B, n0, kb, lane, lw);
     auto issue = [&](int step, int stage) {   // steps are issued in order 0, 1, 2, ...
       char* sa = smem + stage * G7_STAGE;
       const int k0 = kb + 64 * step;
       const bool tl = tail && step == nkt - 1;
-      g7_issue<AK>(A, la, sa, k0, ke, lane, lw, tl);
-      g7_issue<BKC>(B, lb, sa + G7_A, k0, ke, lane, lw, tl);
+      g7_issue<AK>(A, la, sa, k0, ke, lane, lw, tl, cfast_a);
+      g7_issue<BKC>(B, lb, sa + G7_A, k0, ke, lane, lw, tl, cfast_b);
     };
     // staged epilogue operand (whole tiles only)
     const bool px = P.pre_x && n0 + 128 <= N;
@@ -1378,6 +1397,29 @@ TT2_DEV void g8_issue(const OpDesc& d, char* img, int r0, int k0, int lane, int 
   }
 }
 
+// K-contiguous conv operand with C % 64 == 0 and K % 64 == 0 (as g7_conv_fast): each copy's
+// row offset and valid-tap mask are set once per tile; a step reads tap k0 / C.
+struct G8Conv { int64_t off[2]; uint32_t vm[2]; };
+TT2_DEV void g8_conv_init(const OpDesc& d, G8Conv& c, int r0, int lane, int wave) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + (lane >> 3), outer = r0 + row;
+    const int t = outer % d.conv_t;
+    const int lo = max(0, d.conv_pad - t), hi = min(31, d.conv_t - 1 - t + d.conv_pad);
+    c.off[i] = (int64_t)outer * d.ld + ((lane & 7) ^ g8_swz(row)) * 8 - (int64_t)d.conv_pad * d.conv_c;
+    c.vm[i] = outer < d.outer_max && hi >= lo ? (0xFFFFFFFFu >> (31 - hi)) & (0xFFFFFFFFu << lo) : 0u;
+  }
+}
+TT2_DEV void g8_issue_conv(const OpDesc& d, const G8Conv& c, char* img, int k0, int wave) {
+  const int tap = k0 / d.conv_c;
+  const bf16* p = reinterpret_cast<const bf16*>(d.p) + k0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const void* src = (c.vm[i] >> tap) & 1u ? (const void*)(p + c.off[i]) : (const void*)g_zero_page;
+    __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(img + (wave * 2 + i) * 1024), 16, 0, 0);
+  }
+}
+
 // K-contiguous fragment of row `row`, k slice s (16 k): element j holds
 // k = 16 s + 8 (j >> 2) + 4 hi + (j & 3), the order the transposed read delivers
 TT2_DEV bf16x8 g8_frag_kc(const char* img, int row, int s, int hi) {
@@ -1414,9 +1456,13 @@ __global__ __launch_bounds__(G8_NT, 2) void gemm8_kernel(OpDesc A, OpDesc B, Epi
   const int nkt = (K + 63) / 64;
   if (wave >= 4) {   // ---------------------------------------------- loader waves
     const int lw = wave - 4;
+    const bool afast = A.conv_t > 0 && (A.conv_c & 63) == 0 && (K & 63) == 0;
+    G8Conv ca;
+    if (afast) g8_conv_init(A, ca, m0, lane, lw);
     auto issue = [&](int t) {
       char* st = smem + (t & (G8_STAGES - 1)) * G8_STAGE;
-      g8_issue<true>(A, st, m0, 64 * t, lane, lw);
+      if (afast) g8_issue_conv(A, ca, st, 64 * t, lw);
+      else g8_issue<true>(A, st, m0, 64 * t, lane, lw);
       g8_issue<BKC>(B, st + G8_TILE, n0, 64 * t, lane, lw);
     };
     // three steps ahead; each step is 4 copies per loader wave
