@@ -103,19 +103,22 @@ def drop_threshold(p: float) -> int:
 def dropout_keep(seed: int, site: int, n: int, p: float, offset: int = 0) -> np.ndarray:
     """Keep-mask (bool[n]) for flat indices offset..offset+n-1.
 
-    uint32 hash: x = idx*0x9E3779B1 + seed*0x85EBCA77 + site*0xC2B2AE3D, then the
-    murmur3-style finaliser; keep iff x >= floor(p * 2^32).
+    uint32 hash of the element pair j = idx >> 1: x = j*0x9E3779B1 + seed*0x85EBCA77 +
+    site*0xC2B2AE3D, then the murmur3-style finaliser; element idx takes the low 16 bits
+    (even idx) or the high 16 bits (odd idx) and is kept iff they are >= floor(p * 2^16)
+    (= floor(p * 2^32) >> 16).  Restates csrc/tt2_common.h drop_keep / drop_bits8.
     """
     with np.errstate(over="ignore"):
         idx = np.arange(offset, offset + n, dtype=np.uint64)
-        x = (idx * np.uint64(0x9E3779B1) + np.uint64((seed * 0x85EBCA77) & 0xFFFFFFFF)
+        x = ((idx >> np.uint64(1)) * np.uint64(0x9E3779B1) + np.uint64((seed * 0x85EBCA77) & 0xFFFFFFFF)
              + np.uint64((site * 0xC2B2AE3D) & 0xFFFFFFFF)) & _M32
         x ^= x >> np.uint64(16)
         x = (x * np.uint64(0x7FEB352D)) & _M32
         x ^= x >> np.uint64(15)
         x = (x * np.uint64(0x846CA68B)) & _M32
         x ^= x >> np.uint64(16)
-    return x >= np.uint64(drop_threshold(p))
+        half = np.where((idx & np.uint64(1)) == 1, x >> np.uint64(16), x & np.uint64(0xFFFF))
+    return half >= np.uint64(drop_threshold(p) >> 16)
 
 
 class HashDropout(nn.Module):
@@ -187,7 +190,7 @@ class MHA(nn.Module):
         v = v.view(B, Tk, h, dh).transpose(1, 2)
         # scores and softmax in f32 (a no-op for the f32 oracle; under torch.autocast it mirrors
         # AMP's f32 softmax, so the autocast oracle is a standard bf16 mixed-precision reference)
-        s = (q @ k.transpose(-1, -2)).float() / math.sqrt(dh)
+        s = (q @ k.transpose(-1, -2)).to(torch.promote_types(q.dtype, torch.float32)) / math.sqrt(dh)
         allowed = torch.ones(B, 1, Tq, Tk, dtype=torch.bool)
         if key_len is not None:
             allowed = allowed & (torch.arange(Tk)[None, None, None, :] < key_len.view(B, 1, 1, 1))

@@ -16,7 +16,8 @@ OUTPUT, so tests/test_oracle.py can re-run the oracle block on the same data
 without transformers.  A final fixture stores end-to-end oracle outputs for
 seeded weights (init_deterministic) as a drift guard.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py            (all fixtures)
+    python tests/golden/make_golden.py --drift    (only the oracle-only fixtures 6 and 7)
 """
 from __future__ import annotations
 
@@ -119,6 +120,12 @@ def main():
         save("mha", q=q, kv=kv, key_len=kl, in_w=mha.in_proj_weight, in_b=mha.in_proj_bias,
              out_w=mha.out_proj.weight, out_b=mha.out_proj.bias, out=out)
 
+    drift_fixtures()
+
+
+def drift_fixtures():
+    """Fixtures of the oracle alone (no third-party code): regenerate with --drift after a
+    deliberate change of the oracle's dropout hash or initialisation."""
     # 6. dropout hash known answers
     save("dropout_hash", keep_a=dropout_keep(1234, 77, 4096, 0.3), keep_b=dropout_keep(0xFFFFFFFF, 129, 4096, 0.5,
                                                                                       offset=1 << 20))
@@ -143,4 +150,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    drift_fixtures() if "--drift" in sys.argv[1:] else main()

@@ -397,9 +397,7 @@ TT2_DEV void epi_calc8(const EpiParams& E, uint32_t seed, int m, int n0, const f
     for (int j = 0; j < 8; ++j) o[j] = t[j] != 0.f ? o[j] * E.gate_scale : 0.f;
   }
   if (E.drop.thr) {
-    const uint32_t base = (uint32_t)((int64_t)m * E.n_log + n0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = drop_apply(E.drop, seed, base + j, o[j]);
+    drop_apply8(E.drop, seed, (uint32_t)((int64_t)m * E.n_log + n0), o);
   }
   if (E.beta != 0.f) {
     ld8_any(E.c, off, E.c_dt, t);

@@ -179,10 +179,7 @@ __global__ __launch_bounds__(NT) void pe_bwd_kernel(const T* dout, const float* 
 #pragma unroll
       for (int j = 0; j < 4; ++j) { g[j] = lo[j]; g[4 + j] = hi[j]; }
     }
-    if (drop.thr) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = drop_apply(drop, seed, (uint32_t)(i0 + j), g[j]);
-    }
+    if (drop.thr) drop_apply8(drop, seed, (uint32_t)i0, g);
     const f32x4 p0 = *reinterpret_cast<const f32x4*>(pe + (int64_t)t * C + c0);
     const f32x4 p1 = *reinterpret_cast<const f32x4*>(pe + (int64_t)t * C + c0 + 4);
 #pragma unroll

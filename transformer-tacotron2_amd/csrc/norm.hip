@@ -129,8 +129,9 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(LnArgs a) {
   unpack8<T>(xr, s);
   if (has_br) {
     unpack8<T>(brr, br);
+    if (a.drop.thr) drop_apply8(a.drop, seed, (uint32_t)off, br);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] += a.drop.thr ? drop_apply(a.drop, seed, (uint32_t)(off + j), br[j]) : br[j];
+    for (int j = 0; j < 8; ++j) s[j] += br[j];
   }
   float sum = 0.f;
 #pragma unroll
@@ -267,10 +268,12 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
     float s[8], dy[8], keep[8];
     unpack8<T>(cur.x, s);
     unpack8<T>(cur.dy, dy);
+    {
+      const uint32_t kb = a.drop.thr ? drop_bits8(seed, a.drop.site, (uint32_t)off, a.drop.thr) : 0xFFu;
+      const float sc = a.drop.thr ? a.drop.scale : 1.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      keep[j] = a.drop.thr ? (drop_hash(seed, a.drop.site, (uint32_t)(off + j)) >= a.drop.thr ? a.drop.scale : 0.f)
-                           : 1.f;
+      for (int j = 0; j < 8; ++j) keep[j] = (kb >> j) & 1u ? sc : 0.f;
+    }
     if (a.branch) {
       float br[8];
       unpack8<T>(cur.br, br);
@@ -520,10 +523,8 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
     col8(a.mean, c0, mu); col8(a.rstd, c0, rs); col8(a.gamma, c0, g); col8(a.beta, c0, b);
     float z[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      z[j] = act_f(a.act, (v[j] - mu[j]) * rs[j] * g[j] + b[j]);
-      if (a.drop.thr) z[j] = drop_apply(a.drop, seed, (uint32_t)(i0 + j), z[j]);
-    }
+    for (int j = 0; j < 8; ++j) z[j] = act_f(a.act, (v[j] - mu[j]) * rs[j] * g[j] + b[j]);
+    if (a.drop.thr) drop_apply8(a.drop, seed, (uint32_t)i0, z);
     if (a.res) {
       float r[8];
       ld8v(a.res, (int64_t)m * a.res_ld + c0, a.res_dt, r);

@@ -96,7 +96,7 @@ template <typename T> TT2_DEV ChunkV<T> zero_chunk() {
 }
 
 // ---------------------------------------------------------------- dropout hash
-// Bit-identical to oracle/tt2_oracle.py::dropout_keep.
+// Bit-identical to oracle/tt2_oracle.py::dropout_keep (with drop_keep below).
 TT2_DEV uint32_t drop_hash(uint32_t seed, uint32_t site, uint32_t idx) {
   uint32_t x = idx * 0x9E3779B1u + seed * 0x85EBCA77u + site * 0xC2B2AE3Du;
   x ^= x >> 16;
@@ -113,8 +113,34 @@ struct DropDesc {
   uint32_t thr;          // floor(p * 2^32)
   float scale;           // 1 / (1 - p)
 };
+// Keep test of flat element idx: 16 bits per element, two elements per hash (the pair
+// idx >> 1; the even element takes the low half) against thr >> 16 = floor(p * 2^16).
+TT2_DEV bool drop_keep(uint32_t seed, uint32_t site, uint32_t idx, uint32_t thr) {
+  const uint32_t h = drop_hash(seed, site, idx >> 1);
+  return ((idx & 1u) ? (h >> 16) : (h & 0xFFFFu)) >= (thr >> 16);
+}
 TT2_DEV float drop_apply(const DropDesc& d, uint32_t seed, uint32_t idx, float v) {
-  return drop_hash(seed, d.site, idx) >= d.thr ? v * d.scale : 0.f;
+  return drop_keep(seed, d.site, idx, d.thr) ? v * d.scale : 0.f;
+}
+// Keep bits of elements base .. base + 7 (bit j: element base + j) from 4 hashes (5 for an
+// odd base): the same decisions as drop_keep.
+TT2_DEV uint32_t drop_bits8(uint32_t seed, uint32_t site, uint32_t base, uint32_t thr) {
+  const uint32_t t16 = thr >> 16, odd = base & 1u, p0 = base >> 1;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    if (q == 4 && !odd) break;
+    const uint32_t h = drop_hash(seed, site, p0 + q);
+    const int jl = 2 * q - (int)odd;   // element of the low half; jl + 1 takes the high half
+    if (jl >= 0) bits |= (uint32_t)((h & 0xFFFFu) >= t16) << jl;
+    if (jl + 1 < 8) bits |= (uint32_t)((h >> 16) >= t16) << (jl + 1);
+  }
+  return bits;
+}
+TT2_DEV void drop_apply8(const DropDesc& d, uint32_t seed, uint32_t base, float (&v)[8]) {
+  const uint32_t b = drop_bits8(seed, d.site, base, d.thr);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (b >> j) & 1u ? v[j] * d.scale : 0.f;
 }
 
 // ---------------------------------------------------------------- reductions
