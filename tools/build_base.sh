@@ -13,6 +13,8 @@ for o in "$PKG"/build/*.o; do
   f=$(basename "$o" .o)
   if [[ " $FILES " == *" $f "* ]]; then
     git -C "$ROOT" show "$REV:transformer-tacotron2_amd/csrc/$f" > "$TMP/$f"
+    [[ -n "${SED:-}" ]] && sed -i "$SED" "$TMP/$f"   # optional ablation edit, e.g. SED='s/st8nt(/st8(/g'
+    true
     extra=()
     [[ $f == attention.hip ]] && extra=(-mllvm -amdgpu-mfma-vgpr-form=1)
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -I"$PKG/csrc" \

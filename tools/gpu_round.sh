@@ -2,7 +2,7 @@
 # One GPU-box pass (run via gpurun from the repo root): GPU tests, smoke, bench, rocprof
 # kernel-trace stats of the bench step.  Every GPU step has its own time limit; the
 # steps are chained so that the first failure ends the call.
-#   tools/gpu_round.sh <tag> [tests|bench|prof|pmc|dpmc ...]   (default: tests bench prof)
+#   tools/gpu_round.sh <tag> [tests|bench|prof|pmc|mfma|dpmc ...]   (default: tests bench prof)
 set -euo pipefail
 TAG=${1:-r02}
 shift || true
@@ -31,6 +31,11 @@ for s in $STEPS; do
         python3 bench.py $ARGS > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.err"
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
         python3 bench.py $ARGS > "$OUT/bench_write.json" 2> "$OUT/bench_write.err"
+      ;;
+    mfma)  # matrix-pipe busy cycles per kernel (tools/summarize_mfma.py)
+      timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/mfma" -o run \
+        --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-decode --no-cpu-baseline --no-ragged \
+        > "$OUT/bench_mfma.json" 2> "$OUT/bench_mfma.err"
       ;;
     dpmc)  # the same for one cfg3 decode run
       timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/dtr/fetch" -o run --output-format csv -- \
