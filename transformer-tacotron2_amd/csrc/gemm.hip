@@ -899,7 +899,8 @@ TT2_DEV void g7_frag(Frag8<bf16>& f, const char* img, int r0, int kk, int lane) 
 // The MFMA operands are swapped (D = B A^T: each lane holds 4 consecutive C columns of
 // one row) and v_permlane16_swap pairs adjacent column blocks, so every lane stores 8
 // consecutive columns of a row straight from registers -- no LDS round trip for C.
-// ksum (row sums of an M-contiguous A) comes from the A fragments of the wn == 0 waves.
+// ksum (row sums of an M-contiguous A): the wn == 0 waves multiply their A fragments by an
+// all-ones fragment (one extra MFMA each).
 // =====================================================================================
 constexpr int G7_NT = 768;                          // 8 MFMA waves + 4 loader waves
 constexpr int G7_A = 256 * 128, G7_B = 128 * 128;   // bytes per stage: 64 k x 2 B per row

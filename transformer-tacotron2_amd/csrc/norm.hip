@@ -371,8 +371,14 @@ struct BnArgs {
   DropDesc drop;
 };
 
+// tanh through one v_exp_f32 and one v_rcp_f32 (ocml's tanhf is a long branchy sequence and
+// the BatchNorm passes evaluate it per element, twice in the backward): |error| < 1e-6
+TT2_DEV float fast_tanh(float x) {
+  const float t = 1.f - __fdividef(2.f, __expf(2.f * fabsf(x)) + 1.f);
+  return copysignf(t, x);
+}
 TT2_DEV float act_f(int act, float v) {
-  return act == ACT_RELU ? fmaxf(v, 0.f) : (act == ACT_TANH ? tanhf(v) : v);
+  return act == ACT_RELU ? fmaxf(v, 0.f) : (act == ACT_TANH ? fast_tanh(v) : v);
 }
 TT2_DEV float act_grad_from_out(int act, float z) {
   return act == ACT_RELU ? (z > 0.f ? 1.f : 0.f) : (act == ACT_TANH ? 1.f - z * z : 1.f);
@@ -537,10 +543,17 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(BnArgs a) {
 }
 
 // dpre = d(pre-activation BN output): recompute z from y.
-TT2_DEV float bn_dpre(const BnArgs& a, uint32_t seed, uint32_t i, float xh, float g, float b, float doutv) {
+// keep: the element's dropout factor (0 or 1 / (1 - p); 1 without dropout)
+TT2_DEV float bn_dpre(const BnArgs& a, float keep, float xh, float g, float b, float doutv) {
   const float z = act_f(a.act, xh * g + b);
-  const float d = a.drop.thr ? drop_apply(a.drop, seed, i, doutv) : doutv;
-  return d * act_grad_from_out(a.act, z);
+  return doutv * keep * act_grad_from_out(a.act, z);
+}
+// the dropout factors of elements i0 .. i0 + 7 (drop_bits8: 4-5 hashes for 8 elements)
+TT2_DEV void bn_keep8(const BnArgs& a, uint32_t seed, int64_t i0, float (&k)[8]) {
+  const uint32_t bits = a.drop.thr ? drop_bits8(seed, a.drop.site, (uint32_t)i0, a.drop.thr) : 0xFFu;
+  const float sc = a.drop.thr ? a.drop.scale : 1.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) k[j] = (bits >> j) & 1u ? sc : 0.f;
 }
 
 template <typename T, typename TD>
@@ -560,13 +573,14 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
   if (rl < nrl) {
     for (int r = r0 + rl; r < r1; r += nrl) {
       const int64_t i0 = (int64_t)r * a.C + c0;
-      float v[8], d[8];
+      float v[8], d[8], kp[8];
       ld8(y + i0, v);
       ld8(dout + i0, d);
+      bn_keep8(a, seed, i0, kp);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xh = (v[j] - mu[j]) * rs[j];
-        const float dp = bn_dpre(a, seed, (uint32_t)(i0 + j), xh, g[j], b[j], d[j]);
+        const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[j]);
         s1[j] += dp;
         s2[j] += dp * xh;
       }
@@ -633,10 +647,12 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
     ld8(dout + i0, d);
     col8(a.mean, c0, mu); col8(a.rstd, c0, rs); col8(a.gamma, c0, g); col8(a.beta, c0, b);
     if (a.training) { col8(a.dbeta, c0, db); col8(a.dgamma, c0, dg); }
+    float kp[8];
+    bn_keep8(a, seed, i0, kp);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float xh = (v[j] - mu[j]) * rs[j];
-      const float dp = bn_dpre(a, seed, (uint32_t)(i0 + j), xh, g[j], b[j], d[j]);
+      const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[j]);
       o[j] = a.training ? g[j] * rs[j] * (dp - db[j] * invM - xh * dg[j] * invM) : g[j] * rs[j] * dp;
     }
     st8nt(reinterpret_cast<T*>(a.dy) + i0, o);
