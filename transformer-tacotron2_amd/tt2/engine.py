@@ -21,6 +21,7 @@ import torch
 
 from . import ops
 from ._lib import ACT_NONE, ACT_RELU, ACT_TANH
+from .trace import ranged
 from .config import (SITE_DEC_FC1, SITE_DEC_FC2, SITE_DEC_LAYER, SITE_DEC_PE, SITE_ENC_CONV, SITE_ENC_LAYER,
                      SITE_ENC_PE, SITE_POSTNET, TTSConfig)
 from .ops import NO_DROP, Drop
@@ -350,6 +351,7 @@ class TTSEngine:
             for k in self.nbt:
                 self.nbt[k] += 1
 
+    @ranged("tt2.encoder")
     def forward_encoder(self, A: Arena):
         """Encoder pre-net + layers, then the K/V projection of the memory for
         all decoder layers (A["mkv"])."""
@@ -396,6 +398,7 @@ class TTSEngine:
         # one GEMM projects the memory to K/V for all decoder layers
         self._lin(mem, self.W("dec.kv.w"), A["mkv"], Me, c.n_dec * 2 * d, d, bias=self.P("dec.kv.b"))
 
+    @ranged("tt2.decoder")
     def forward_decoder(self, A: Arena):
         c = self.cfg
         B, Tx, Ty, Md = A.B, A.Tx, A.Ty, A.Md
@@ -446,6 +449,7 @@ class TTSEngine:
         ops.cast2d(A["heads"], A.heads_ld, A["pin"], c.n_mels, Md, c.n_mels)
         self._postnet_fwd(A, A["pin"], A["heads"], A.heads_ld, Md, Ty, tr)
 
+    @ranged("tt2.postnet")
     def _postnet_fwd(self, A, x_in, res, res_ld, Md, Ty, tr):
         c = self.cfg
         chans = postnet_channels(c)
@@ -469,6 +473,7 @@ class TTSEngine:
             x = out
 
     # ------------------------------------------------------------ loss
+    @ranged("tt2.loss")
     def loss(self, A: Arena):
         c = self.cfg
         ops.tts_loss(A["heads"], A.heads_ld, A["mel_after"], A["mel"], A["mel_len"], A["loss"], A["g_heads"],
@@ -479,6 +484,7 @@ class TTSEngine:
         if self.grad_ready_hook is not None:
             self.grad_ready_hook(self.lay.offset(name))
 
+    @ranged("tt2.backward")
     def backward(self, A: Arena):
         c, cd = self.cfg, self.cd
         B, Tx, Ty, Me, Md = A.B, A.Tx, A.Ty, A.Me, A.Md
@@ -675,6 +681,7 @@ class TTSEngine:
             self.exp_avg = torch.zeros_like(self.params)
             self.exp_avg_sq = torch.zeros_like(self.params)
 
+    @ranged("tt2.optimizer")
     def optimizer_step(self):
         o = self.opt
         ops.adam_step(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.shadow, self.step_t,

@@ -24,6 +24,7 @@ import math
 
 import torch
 
+from .trace import ranged
 from . import _lib, ops
 from ._lib import check, dt, lib, stream_ptr
 from .engine import TTSEngine
@@ -147,6 +148,7 @@ class Decoder:
         check(lib().tt2_decode_reset(C.byref(self.desc(math.inf)), self.seed0 & 0xFFFFFFFF, stream_ptr()),
               "tt2_decode_reset")
 
+    @ranged("tt2.decode.encode")
     def encode(self, text, text_len):
         e, A = self.e, self.A
         was = e.training
@@ -181,6 +183,7 @@ class Decoder:
         except Exception:   # interpreter shutdown: the library may be gone
             pass
 
+    @ranged("tt2.decode.loop")
     def decode_loop(self, n_steps: int, use_graph: bool = True, stop_threshold: float | None = None,
                     check_every: int = 32, limits: torch.Tensor | None = None) -> int:
         """Run up to n_steps frames; with stop_threshold, an utterance finishes at its first
@@ -219,6 +222,7 @@ class Decoder:
             out_len = torch.minimum(out_len, limits.to(out_len.device, torch.long))
         return out_len
 
+    @ranged("tt2.decode.postnet")
     def postnet(self, n_frames: int, stop_threshold: float | None, limits: torch.Tensor | None = None):
         e, c, A = self.e, self.e.cfg, self.A
         B, T = self.B, n_frames
