@@ -1,13 +1,15 @@
 #!/bin/bash
-# A/B two environment settings of the decode legs (cfg3, cfg5) of bench.py on one box:
-#   tools/ab_decode.sh "TT2_CAPTURE_MODE=global" "TT2_CAPTURE_MODE=thread_local" [rounds]
+# Interleaved decode A/B (dev tool, GPU): tools/decode_ab.py under two environments.
+#   tools/ab_decode.sh <tag> "<env A>" "<env B>" [rounds]   -> gpurun_out/<tag>/dab.txt
 set -euo pipefail
-A=$1; B=$2; R=${3:-2}
-ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-ragged"
-for i in $(seq "$R"); do
-  for v in A B; do
-    if [ $v = A ]; then E=$A; else E=$B; fi
-    r=$(env $E timeout -k 10 300 python3 bench.py $ARGS 2>/dev/null | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["decode"]["ms_per_frame_step"], d["decode_longform"]["ms_per_frame_step"])')
-    echo "$v ($E) train/decode/longform ms: $r"
+TAG=$1; A=$2; B=$3; R=${4:-2}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+: > "$OUT/dab.txt"
+for i in $(seq 1 "$R"); do
+  for e in "$A" "$B"; do
+    echo "== $e" >> "$OUT/dab.txt"
+    env $e timeout -k 10 300 python -u tools/decode_ab.py >> "$OUT/dab.txt" 2>&1
   done
 done
+cat "$OUT/dab.txt"
