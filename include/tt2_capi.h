@@ -415,6 +415,14 @@ int tt2_tts_loss(const tt2_loss_args* a, hipStream_t stream);
 
 /* conv dgrad weight: wd[ci][tap][co] = w[co][k-1-tap][ci] */
 int tt2_conv_weight_flip(const void* w, void* wd, int cout, int cin, int k, int dtype, hipStream_t stream);
+/* The same flip for up to TT2_WFLIP_MAX conv layers in one launch (the backward flips every
+ * encoder / post-net conv weight once per step). */
+#define TT2_WFLIP_MAX 16
+typedef struct tt2_wflip_job {
+  const void* w; void* wd;
+  int32_t cout, cin, k, pad_;
+} tt2_wflip_job;
+int tt2_conv_weight_flip_batch(const tt2_wflip_job* jobs, int32_t n, int32_t dtype, hipStream_t stream);
 
 /* -------------------------------------------------------------- optimizer
  * Fused Adam(W) over the flat f32 parameter buffer with optional global-norm

@@ -163,3 +163,18 @@ def test_conv_weight_flip(dtype, cout, cin):
     ops.conv_weight_flip(w, wd, cout, cin, K)
     ref = w.flip(1).permute(2, 1, 0).reshape(cin, K * cout)
     assert torch.equal(wd, ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_weight_flip_batch(dtype):
+    """All conv layers' flips in one launch == the per-layer flip (ragged channel counts and
+    kernel widths, so jobs span different work-item ranges)."""
+    from tt2 import ops
+    shapes = [(512, 512, 5), (80, 512, 5), (512, 80, 5), (100, 70, 3), (64, 64, 1)]
+    jobs = []
+    for cout, cin, K in shapes:
+        w = torch.randn(cout, K, cin, device="cuda").to(dtype)
+        jobs.append((w, torch.empty(cin, K * cout, device="cuda", dtype=dtype), cout, cin, K))
+    ops.conv_weight_flip_batch(jobs)
+    for w, wd, cout, cin, K in jobs:
+        assert torch.equal(wd, w.flip(1).permute(2, 1, 0).reshape(cin, K * cout))

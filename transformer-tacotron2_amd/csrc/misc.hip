@@ -316,9 +316,9 @@ __global__ void loss_finalize_kernel(const float* part, int nblocks, const int32
 // conv dgrad weight: wd[ci][tap'][co] = w[co][K-1-tap'][ci] -- per tap a [Cout x Cin] ->
 // [Cin x Cout] transpose through a 64 x 64 LDS tile: reads coalesced along ci, writes along co.
 template <typename T>
-__global__ __launch_bounds__(NT) void conv_wflip_kernel(const T* w, T* wd, int Cout, int Cin, int K) {
+TT2_DEV void conv_wflip_tile(const T* w, T* wd, int Cout, int Cin, int K, int bx, int by, int tap) {
   __shared__ T tile[64][65];
-  const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64, tap = blockIdx.z;
+  const int ci0 = bx * 64, co0 = by * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
 #pragma unroll 4
   for (int r = ty; r < 64; r += NT / 64) {
@@ -332,6 +332,28 @@ __global__ __launch_bounds__(NT) void conv_wflip_kernel(const T* w, T* wd, int C
     const int ci = ci0 + r, co = co0 + tx;
     if (co < Cout && ci < Cin) wd[((int64_t)ci * K + tp) * Cout + co] = tile[tx][r];
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void conv_wflip_kernel(const T* w, T* wd, int Cout, int Cin, int K) {
+  conv_wflip_tile<T>(w, wd, Cout, Cin, K, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// every conv layer's flip in one launch: workgroup b belongs to the job whose item range
+// [first[j], first[j + 1]) holds it; items are (tap, co block, ci block) in that order
+struct WflipBatch {
+  tt2_wflip_job job[TT2_WFLIP_MAX];
+  int first[TT2_WFLIP_MAX + 1];
+  int n;
+};
+template <typename T>
+__global__ __launch_bounds__(NT) void conv_wflip_batch_kernel(WflipBatch B) {
+  int j = 0;
+  while (j + 1 < B.n && (int)blockIdx.x >= B.first[j + 1]) ++j;
+  const tt2_wflip_job& J = B.job[j];
+  const int it = blockIdx.x - B.first[j], nbx = (J.cin + 63) / 64, nby = (J.cout + 63) / 64;
+  conv_wflip_tile<T>(reinterpret_cast<const T*>(J.w), reinterpret_cast<T*>(J.wd), J.cout, J.cin, J.k, it % nbx,
+                     (it / nbx) % nby, it / (nbx * nby));
 }
 
 // nn.Conv1d weight [Cout][Cin][K] -> tap-major [Cout][K][Cin]: per output channel a
@@ -582,6 +604,25 @@ extern "C" int tt2_conv_weight_flip(const void* w, void* wd, int cout, int cin, 
   else
     hipLaunchKernelGGL(conv_wflip_kernel<float>, g, dim3(NT), 0, s, (const float*)w, (float*)wd, cout, cin, k);
   return tt2_check_launch(hipGetLastError(), "tt2_conv_weight_flip");
+}
+
+extern "C" int tt2_conv_weight_flip_batch(const tt2_wflip_job* jobs, int32_t n, int32_t dtype, hipStream_t s) {
+  if (n <= 0) return TT2_OK;
+  if (n > TT2_WFLIP_MAX || !jobs) return tt2_set_error(TT2_E_INVALID, "tt2_conv_weight_flip_batch: 1..16 jobs");
+  WflipBatch B{};
+  B.n = n;
+  for (int j = 0; j < n; ++j) {
+    const tt2_wflip_job& J = jobs[j];
+    if (J.cout <= 0 || J.cin <= 0 || J.k <= 0 || !J.w || !J.wd || J.w == J.wd)
+      return tt2_set_error(TT2_E_INVALID, "tt2_conv_weight_flip_batch: bad job");
+    B.job[j] = J;
+    B.first[j + 1] = B.first[j] + ((J.cin + 63) / 64) * ((J.cout + 63) / 64) * J.k;
+  }
+  if (dtype == TT2_DT_BF16)
+    hipLaunchKernelGGL(conv_wflip_batch_kernel<bf16>, dim3(B.first[n]), dim3(NT), 0, s, B);
+  else
+    hipLaunchKernelGGL(conv_wflip_batch_kernel<float>, dim3(B.first[n]), dim3(NT), 0, s, B);
+  return tt2_check_launch(hipGetLastError(), "tt2_conv_weight_flip_batch");
 }
 
 extern "C" int tt2_conv_weight_pack(const void* w, void* wp, int32_t cout, int32_t cin, int32_t k, int32_t dtype,

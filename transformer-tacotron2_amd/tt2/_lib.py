@@ -51,6 +51,11 @@ class GemmArgs(C.Structure):
 
 
 # (name, argtypes) for every exported entry point; tests check these exist.
+class WflipJob(C.Structure):
+    """tt2_wflip_job: one conv weight of a batched dgrad-weight flip (include/tt2_capi.h)."""
+    _fields_ = [("w", vp), ("wd", vp), ("cout", i32), ("cin", i32), ("k", i32), ("pad_", i32)]
+
+
 SIGNATURES: dict[str, tuple[list, object]] = {
     "tt2_last_error": ([], C.c_char_p),
     "tt2_version": ([], C.c_int),
@@ -230,6 +235,7 @@ SIGNATURES.update({
     "tt2_loss_workspace_size": ([], sz),
     "tt2_tts_loss": ([P_(LossArgs), vp], C.c_int),
     "tt2_conv_weight_flip": ([vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp], C.c_int),
+    "tt2_conv_weight_flip_batch": ([C.POINTER(WflipJob), i32, i32, vp], C.c_int),
     "tt2_adam_workspace_size": ([], sz),
     "tt2_adam_step": ([P_(AdamArgs), vp], C.c_int),
     "tt2_step_bump": ([vp, vp, vp], C.c_int),

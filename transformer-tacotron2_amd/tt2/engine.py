@@ -200,6 +200,7 @@ class TTSEngine:
         self.ln_chain = os.environ.get("TT2_LN_CHAIN", "1") != "0"
         self._ln_parts = None
         self._wq = None   # weight-gradient requests queued for one grouped launch (see _defer_wgrads)
+        self.wflip_batch = os.environ.get("TT2_WFLIP_BATCH", "1") != "0"
         self.cd = dtype
         self.dev = torch.device(device)
         self.lay = Layout(build_slots(c))
@@ -492,6 +493,7 @@ class TTSEngine:
         pad = (K - 1) // 2
         scale = 1.0 / math.sqrt(c.head_dim)
         gs = lambda p: 1.0 / (1.0 - p) if (self.training and self.dropout_enabled and p > 0) else 1.0  # noqa: E731
+        self._flip_conv_weights()
         # ---------------- post-net
         chans = postnet_channels(c)
         nl = c.postnet_layers
@@ -665,13 +667,30 @@ class TTSEngine:
         ops.embedding_bwd(A["text"], gc, self.G("enc.embed"), Me, c.vocab, pad_idx=0)
         self._ready("enc.embed")
 
-    def _wflip(self, name, cout, cin, K):
+    def _wflip_buf(self, name, cout, cin, K):
         key = ("wflip", name)
         buf = self.__dict__.setdefault("_wflip_bufs", {}).get(key)
         if buf is None:
             buf = torch.empty(cin, K * cout, dtype=self.cd, device=self.dev)
             self._wflip_bufs[key] = buf
-        ops.conv_weight_flip(self.W(name), buf, cout, cin, K)
+        return buf
+
+    def _flip_conv_weights(self):
+        """Every conv layer's dgrad weight (tap-flipped, transposed) in one launch at the start
+        of the backward; _wflip then hands out the flipped copies (TT2_WFLIP_BATCH=0: one
+        launch per layer where it is used, the measurement baseline)."""
+        if not self.wflip_batch:
+            return
+        c = self.cfg
+        chans = postnet_channels(c)
+        convs = [(f"post.conv{i}.w", chans[i + 1], chans[i], c.postnet_kernel) for i in range(c.postnet_layers)]
+        convs += [(f"enc.conv{i}.w", c.d_model, c.d_model, c.enc_conv_kernel) for i in range(c.enc_conv_layers)]
+        ops.conv_weight_flip_batch([(self.W(n), self._wflip_buf(n, co, ci, k), co, ci, k) for n, co, ci, k in convs])
+
+    def _wflip(self, name, cout, cin, K):
+        buf = self._wflip_buf(name, cout, cin, K)
+        if not self.wflip_batch:
+            ops.conv_weight_flip(self.W(name), buf, cout, cin, K)
         return buf
 
     # ------------------------------------------------------------ optimizer

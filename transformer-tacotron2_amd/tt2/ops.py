@@ -443,6 +443,17 @@ def tts_loss(heads, heads_ld, mel_after, target, mel_len, loss_out, g_heads, g_a
     check(L.tt2_tts_loss(C.byref(a), stream_ptr()), "tt2_tts_loss")
 
 
+def conv_weight_flip_batch(jobs):
+    """One launch flipping every (w, wd, cout, cin, k) of `jobs` (<= 16; same dtype)."""
+    if not jobs:
+        return
+    arr = (_lib.WflipJob * len(jobs))()
+    for a, (w, wd, cout, cin, k) in zip(arr, jobs):
+        a.w, a.wd, a.cout, a.cin, a.k = w.data_ptr(), wd.data_ptr(), cout, cin, k
+    check(lib().tt2_conv_weight_flip_batch(arr, len(jobs), dt(jobs[0][0]), stream_ptr()),
+          "tt2_conv_weight_flip_batch")
+
+
 def conv_weight_flip(w, wd, cout, cin, k):
     check(lib().tt2_conv_weight_flip(w.data_ptr(), wd.data_ptr(), cout, cin, k, dt(w), stream_ptr()),
           "tt2_conv_weight_flip")
