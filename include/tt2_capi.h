@@ -327,6 +327,10 @@ typedef struct tt2_ln_args {
 } tt2_ln_args;
 int tt2_layernorm_fwd(const tt2_ln_args* a, hipStream_t stream);
 size_t tt2_layernorm_bwd_workspace_size(const tt2_ln_args* a);
+/* tt2_gemm_grouped that also completes `fin`, a deferred LayerNorm backward (defer_finalize
+ * = 1, partials still in its workspace), inside the group's split-K reduce launch: a layer's
+ * last LayerNorm gradients need no launch of their own.  fin may be NULL; n may be 0. */
+int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int32_t n, const tt2_ln_args* fin, hipStream_t stream);
 int tt2_layernorm_bwd(const tt2_ln_args* a, hipStream_t stream);
 /* Completes a deferred tt2_layernorm_bwd (defer_finalize = 1): dgamma/dbeta/dbias from the
  * partials it left in a->workspace.  Same fixed summation order as a chained finalize. */

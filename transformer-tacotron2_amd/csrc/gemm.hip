@@ -1018,10 +1018,21 @@ struct G7Prob {
   int pre_x;     // the loader waves stage the bf16 residual (1) or gate (2) tile in LDS (lds_epi only)
 };
 constexpr int G7_MAXP = 8;
+// A deferred LayerNorm backward's column-sum finalize (tt2_ln_args with defer_finalize) that
+// rides in the group's split-K reduce launch: part[nb][3][C] -> dg / db / dd (each
+// = gb * old + sum when gb != 0), one wave per output column, fixed order.
+struct G7Fin {
+  const float* part;
+  float* dst[3];
+  float gb;
+  int nb, C;
+};
 struct G7Group {
   G7Prob p[G7_MAXP];
   int np, items;
+  G7Fin fin;   // nb == 0: none
 };
+constexpr int G7_FIN_WAVES = 4;   // columns per 256-thread reduce block
 
 // The epilogue's 256-row image (C, and before it the staged residual / gate in place):
 // rows 0..191 fill the ring stage of K step nkt - 3 (the first stage that no later step
@@ -1308,8 +1319,29 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7g_kernel(G7Group G) {
   g7_item<AK, BKC>(P, local % nt, local / nt, smem);
 }
 
-// split-K reduce of every split problem of a group (blockIdx.y = problem)
+// split-K reduce of every split problem of a group (blockIdx.y = problem); plane y = np, when
+// present, finalizes the deferred LayerNorm column sums (4 loads in flight per lane)
 __global__ void gemm_splitk_reduce_g(G7Group G) {
+  if ((int)blockIdx.y == G.np) {
+    const G7Fin& f = G.fin;
+    const int o = blockIdx.x * G7_FIN_WAVES + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (o >= 3 * f.C) return;
+    const int which = o / f.C, c = o - which * f.C;
+    float* dst = f.dst[which];
+    if (!dst) return;
+    const float* src = f.part + (int64_t)which * f.C + c;
+    const int64_t rs = 3 * (int64_t)f.C;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int r = lane;
+    for (; r + 192 < f.nb; r += 256) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += src[(r + 64 * u) * rs];
+    }
+    for (; r < f.nb; r += 64) acc[0] += src[r * rs];
+    const float v = wave_sum((acc[0] + acc[1]) + (acc[2] + acc[3]));
+    if (lane == 0) dst[c] = f.gb != 0.f ? f.gb * dst[c] + v : v;
+    return;
+  }
   const G7Prob& P = G.p[blockIdx.y];
   if (P.splits > 1) splitk_reduce_body(P.ws, P.splits, P.E, P.M, P.N, blockIdx.x, gridDim.x);
 }
@@ -1750,10 +1782,20 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   return tt2_check_launch(err, "tt2_gemm");
 }
 
-extern "C" int tt2_gemm_grouped(const tt2_gemm_args* probs, int n, hipStream_t stream) {
-  if (n <= 0) return TT2_OK;
-  if (!probs || n > G7_MAXP) return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: 1..8 problems");
+extern "C" int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int n, const tt2_ln_args* fin,
+                                    hipStream_t stream) {
+  if (n <= 0 && !fin) return TT2_OK;
+  if ((n > 0 && !probs) || n > G7_MAXP) return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: 1..8 problems");
   G7Group G{};
+  if (fin && fin->m > 0) {
+    if (!fin->defer_finalize || !fin->workspace || fin->c <= 0)
+      return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped_fin: fin must be a deferred LayerNorm backward");
+    G.fin.part = reinterpret_cast<const float*>(fin->workspace);
+    G.fin.dst[0] = fin->dgamma; G.fin.dst[1] = fin->dbeta; G.fin.dst[2] = fin->dbias;
+    G.fin.gb = fin->grad_beta;
+    G.fin.C = fin->c;
+    G.fin.nb = (int)(tt2_layernorm_bwd_workspace_size(fin) / (3 * sizeof(float) * fin->c));
+  }
   int reduce_blocks = 0, ta = -1, tb = -1, main_only = 1;
   for (int i = 0; i < n; ++i) {
     const tt2_gemm_args* a = probs + i;
@@ -1778,7 +1820,11 @@ extern "C" int tt2_gemm_grouped(const tt2_gemm_args* probs, int n, hipStream_t s
       reduce_blocks = (int)std::max<int64_t>(reduce_blocks, nb < 4096 ? nb : 4096);
     }
   }
-  if (G.np == 0) return TT2_OK;
+  const int fin_blocks = G.fin.nb ? (3 * G.fin.C + G7_FIN_WAVES - 1) / G7_FIN_WAVES : 0;
+  if (G.np == 0) {
+    if (fin_blocks) hipLaunchKernelGGL(gemm_splitk_reduce_g, dim3(fin_blocks, 1), dim3(256), 0, stream, G);
+    return tt2_check_launch(hipGetLastError(), "tt2_gemm_grouped");
+  }
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (probe_take(e0, e1)) {
 #define TT2_G7G(A_, B_) hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_>), dim3(G.items), dim3(G7_NT), 0, stream, e0, e1, 0, G)
@@ -1791,9 +1837,15 @@ extern "C" int tt2_gemm_grouped(const tt2_gemm_args* probs, int n, hipStream_t s
   else if (!ta && tb) hipLaunchKernelGGL((gemm7g_kernel<true, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
   else if (ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<false, true>), dim3(G.items), dim3(G7_NT), 0, stream, G);
   else hipLaunchKernelGGL((gemm7g_kernel<false, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
-  if (reduce_blocks > 0 && !main_only)
-    hipLaunchKernelGGL(gemm_splitk_reduce_g, dim3(reduce_blocks, G.np), dim3(256), 0, stream, G);
+  if (main_only) reduce_blocks = 0;
+  if (reduce_blocks > 0 || fin_blocks > 0)
+    hipLaunchKernelGGL(gemm_splitk_reduce_g, dim3(std::max(reduce_blocks, fin_blocks), G.np + (fin_blocks ? 1 : 0)),
+                       dim3(256), 0, stream, G);
   return tt2_check_launch(hipGetLastError(), "tt2_gemm_grouped");
+}
+
+extern "C" int tt2_gemm_grouped(const tt2_gemm_args* probs, int n, hipStream_t stream) {
+  return tt2_gemm_grouped_fin(probs, n, nullptr, stream);
 }
 
 extern "C" int tt2_probe_arm(void) {

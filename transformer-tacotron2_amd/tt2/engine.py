@@ -199,6 +199,8 @@ class TTSEngine:
         # (two dedicated partials buffers alternate; see _ln_defer)
         self.ln_chain = os.environ.get("TT2_LN_CHAIN", "1") != "0"
         self._ln_parts = None
+        # ... and each layer's last one in the layer's grouped weight-gradient reduce launch
+        self.ln_fin_in_reduce = os.environ.get("TT2_LN_FIN_REDUCE", "1") != "0"
         self._wq = None   # weight-gradient requests queued for one grouped launch (see _defer_wgrads)
         self.wflip_batch = os.environ.get("TT2_WFLIP_BATCH", "1") != "0"
         self.cd = dtype
@@ -320,19 +322,32 @@ class TTSEngine:
             self._ln_parts = [torch.empty(nbytes, dtype=torch.uint8, device=self.dev) for _ in range(2)]
         return {"part": self._ln_parts[slot], "defer": True, "prev": prev}
 
+    def _ln_last(self, *args, prev=None, slot=0, **kw):
+        """A layer's last LayerNorm backward: with the chain on, deferred into partials slot
+        `slot` (free: its previous user was completed by `prev`'s launch) and returned for
+        _flush_wgrads to finalize inside the layer's grouped weight-gradient launch, which
+        precedes the layer's DP bucket (_ready) and the next use of the slot."""
+        extra = self._ln_defer(slot, 0, prev) if self.ln_chain and self.ln_fin_in_reduce else {"prev": prev}
+        a = ops.layernorm_bwd(*args, ws=self.ws, **kw, **extra)
+        return a if extra.get("defer") else None
+
     def _defer_wgrads(self):
         self._wq = []
 
-    def _flush_wgrads(self):
+    def _flush_wgrads(self, fin=None):
         """Launch the queued weight gradients as grouped v7 GEMMs (<= 8 per launch), one
-        split-K factor per group: about 256 work items, >= 512 tokens per split."""
+        split-K factor per group: about 256 work items, >= 512 tokens per split.  fin: the
+        layer's last (deferred) LayerNorm backward, finalized in the first group's reduce
+        launch instead of a launch of its own."""
         q, self._wq = self._wq, None
+        if not q and fin is not None:
+            ops.layernorm_bwd_finalize(fin)
         for i in range(0, len(q), 8):
             grp = q[i:i + 8]
             tiles = sum(((p["m"] + 255) // 256) * ((p["n"] + 127) // 128) for p in grp)
             kmin = min(p["k"] for p in grp)
             sp = max(1, min(16, 256 // tiles, kmin // 512))
-            ops.gemm_grouped([dict(p, splits=sp) for p in grp], ws=self.ws)
+            ops.gemm_grouped([dict(p, splits=sp) for p in grp], ws=self.ws, fin=fin if i == 0 else None)
 
     def _bias(self, dy, ld, m, n, gb):
         ops.colsum(dy, ld, m, n, gb, ws=self.ws)
@@ -579,9 +594,9 @@ class TTSEngine:
             self._dgrad(g_cq, self.W(p + "cq.w"), gx2, Md, d, d, res=A["g_res"])
             gx, gx2 = gx2, gx
             # LN1 + self attention
-            ops.layernorm_bwd(gx, x_in, A[f"do{l}"], self.P(p + "ln1.g"), A[f"dln1m{l}"], A[f"dln1r{l}"],
-                              A["g_res"], A["g_br"], self.G(p + "ln1.g"), self.G(p + "ln1.b"), Md,
-                              drop=self.drop(base, c.dropout), ws=self.ws, dbias=self.G(p + "o.b"), prev=ln2)
+            ln1 = self._ln_last(gx, x_in, A[f"do{l}"], self.P(p + "ln1.g"), A[f"dln1m{l}"], A[f"dln1r{l}"],
+                                A["g_res"], A["g_br"], self.G(p + "ln1.g"), self.G(p + "ln1.b"), Md,
+                                drop=self.drop(base, c.dropout), dbias=self.G(p + "o.b"), prev=ln2, slot=0)
             self._wgrad(A["g_br"], A[f"datt{l}"], self.G(p + "o.w"), d, d, Md)
             self._dgrad(A["g_br"], self.W(p + "o.w"), A["g_att"], Md, d, d)
             qkv, gq = A[f"dqkv{l}"], A["g_qkv"]
@@ -591,7 +606,7 @@ class TTSEngine:
             self._wgrad(gq, x_in, self.G(p + "qkv.w"), 3 * d, d, Md, gb=self.G(p + "qkv.b"))
             self._dgrad(gq, self.W(p + "qkv.w"), gx2, Md, d, 3 * d, res=A["g_res"])
             gx, gx2 = gx2, gx
-            self._flush_wgrads()
+            self._flush_wgrads(fin=ln1)
             self._ready(p + "qkv.w")
         # ---------------- decoder pre-net
         g_proj = A["g_br"]
@@ -633,9 +648,9 @@ class TTSEngine:
             self._wgrad(gf1, h1, self.G(p + "ffn1.w"), F, d, Me, gb=self.G(p + "ffn1.b"))
             self._dgrad(gf1, self.W(p + "ffn1.w"), gxe2, Me, d, F, res=gres)
             gxe, gxe2 = gxe2, gxe
-            ops.layernorm_bwd(gxe, x_in, A[f"eo{l}"], self.P(p + "ln1.g"), A[f"eln1m{l}"], A[f"eln1r{l}"], gres, gbr,
-                              self.G(p + "ln1.g"), self.G(p + "ln1.b"), Me, drop=self.drop(base, c.dropout),
-                              ws=self.ws, dbias=self.G(p + "o.b"), prev=ln2)
+            ln1 = self._ln_last(gxe, x_in, A[f"eo{l}"], self.P(p + "ln1.g"), A[f"eln1m{l}"], A[f"eln1r{l}"], gres,
+                                gbr, self.G(p + "ln1.g"), self.G(p + "ln1.b"), Me, drop=self.drop(base, c.dropout),
+                                dbias=self.G(p + "o.b"), prev=ln2, slot=1)
             self._wgrad(gbr, A[f"eatt{l}"], self.G(p + "o.w"), d, d, Me)
             self._dgrad(gbr, self.W(p + "o.w"), gatt, Me, d, d)
             qkv = A[f"eqkv{l}"]
@@ -645,7 +660,7 @@ class TTSEngine:
             self._wgrad(gq, x_in, self.G(p + "qkv.w"), 3 * d, d, Me, gb=self.G(p + "qkv.b"))
             self._dgrad(gq, self.W(p + "qkv.w"), gxe2, Me, d, 3 * d, res=gres)
             gxe, gxe2 = gxe2, gxe
-            self._flush_wgrads()
+            self._flush_wgrads(fin=ln1)
             self._ready(p + "qkv.w")
         # ---------------- encoder pre-net
         ops.posenc_bwd(gxe, self.pe, gbr, self.G("enc.alpha"), Me, Tx, drop=self.drop(SITE_ENC_PE, c.dropout),
