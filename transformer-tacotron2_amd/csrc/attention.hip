@@ -691,14 +691,16 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
 // dQ: wave = 32 queries (query on the lane), workgroup walks 64-key tiles in two
 // 32-key halves.
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
+// dQ body (also the fused dQ + dK/dV launch): workgroup (bx, by) of a (B*H, ny) grid; smem
+// holds sK[2][64 D] and sV[2][64 D]; publish: store delta = rowsum(dO * O) for a later dK/dV
+TT2_DEV void attn_bwd_dq3_body(const AttnArgs& a, int bx, int by, int ny, char* smem, bool publish) {
   constexpr int NTH = NW * 64, PER = Stage3<NTH>::PER, QB = 32 * NW;
-  __shared__ __attribute__((aligned(16))) bf16 sK[2][64 * D];
-  __shared__ __attribute__((aligned(16))) bf16 sV[2][64 * D];
+  bf16 (*sK)[64 * D] = reinterpret_cast<bf16 (*)[64 * D]>(smem);
+  bf16 (*sV)[64 * D] = reinterpret_cast<bf16 (*)[64 * D]>(smem + 2 * 64 * D * sizeof(bf16));
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ql = lane & 31, hi = lane >> 5;
-  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;   // x = (batch, head): block index on y
-  const int qblk = a.causal ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;
+  const int bh = bx, b = bh / a.H, h = bh % a.H;   // x = (batch, head): block index on y
+  const int qblk = a.causal ? ny - 1 - by : by;
   const int q0 = qblk * QB, qw = q0 + 32 * w, qv = qw + ql;
   const RowBuf Q = row_buf(reinterpret_cast<const bf16*>(a.q) + (int64_t)b * a.Tq * a.q_ld + h * D, a.q_ld, a.Tq);
   const RowBuf dO =
@@ -723,7 +725,7 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
     for (int j = 0; j < 8; ++j) dsum += (float)fdo[st][j] * (float)fo[st][j];
   dsum += __shfl_xor(dsum, 32, 64);
   const float dl = qok ? dsum : 0.f;
-  if (qok && hi == 0) a.delta[(int64_t)bh * a.Tq + qv] = dsum;
+  if (publish && qok && hi == 0) a.delta[(int64_t)bh * a.Tq + qv] = dsum;
   const float c = a.scale * LOG2E;
   f32x16 dq[2];
   zero16(dq[0]);
@@ -795,15 +797,18 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
 // dK, dV: wave = 32 keys (key on the lane), workgroup walks 64-query tiles in two
 // 32-query halves.
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
+// dK / dV body: workgroup (bx, by) of a (B*H, key blocks) grid; smem holds sQ[2][64 D],
+// sdO[2][64 D], sL[2][64], sDl[2][64]; reads delta (published by the dQ pass or attn_bwd_prep)
+TT2_DEV void attn_bwd_dkdv3_body(const AttnArgs& a, int bx, int by, char* smem) {
   constexpr int NTH = NW * 64, PER = Stage3<NTH>::PER, KB = 32 * NW;
-  __shared__ __attribute__((aligned(16))) bf16 sQ[2][64 * D];
-  __shared__ __attribute__((aligned(16))) bf16 sdO[2][64 * D];
-  __shared__ __attribute__((aligned(16))) float sL[2][64], sDl[2][64];
+  bf16 (*sQ)[64 * D] = reinterpret_cast<bf16 (*)[64 * D]>(smem);
+  bf16 (*sdO)[64 * D] = reinterpret_cast<bf16 (*)[64 * D]>(smem + 2 * 64 * D * sizeof(bf16));
+  float (*sL)[64] = reinterpret_cast<float (*)[64]>(smem + 4 * 64 * D * sizeof(bf16));
+  float (*sDl)[64] = reinterpret_cast<float (*)[64]>(smem + 4 * 64 * D * sizeof(bf16) + 2 * 64 * sizeof(float));
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int kl = lane & 31, hi = lane >> 5;
-  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;   // x = (batch, head): block index on y
-  const int k0 = blockIdx.y * KB, kw = k0 + 32 * w, kv = kw + kl;   // causal: low blocks (heaviest) first
+  const int bh = bx, b = bh / a.H, h = bh % a.H;   // x = (batch, head): block index on y
+  const int k0 = by * KB, kw = k0 + 32 * w, kv = kw + kl;   // causal: low blocks (heaviest) first
   const RowBuf Q = row_buf(reinterpret_cast<const bf16*>(a.q) + (int64_t)b * a.Tq * a.q_ld + h * D, a.q_ld, a.Tq);
   const RowBuf dO =
       row_buf(reinterpret_cast<const bf16*>(a.dout) + (int64_t)b * a.Tq * a.do_ld + h * D, a.do_ld, a.Tq);
@@ -916,6 +921,30 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
   }
 }
 
+constexpr int ATTN_BWD3_SMEM = 4 * 64 * D * sizeof(bf16) + 4 * 64 * sizeof(float);   // the larger (dK / dV) body
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 64 * D * sizeof(bf16)];
+  attn_bwd_dq3_body<NW>(a, blockIdx.x, blockIdx.y, gridDim.y, smem, true);
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[ATTN_BWD3_SMEM];
+  attn_bwd_dkdv3_body<NW>(a, blockIdx.x, blockIdx.y, smem);
+}
+
+// dQ and dK / dV in one launch (delta from attn_bwd_prep_kernel beforehand): y < nkb are the
+// key blocks, the rest the query blocks, so the (few, long) dK / dV workgroups of a short key
+// range run beside the dQ workgroups instead of after them on a mostly idle chip
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_fused3_kernel(AttnArgs a, int nkb) {
+  __shared__ __attribute__((aligned(16))) char smem[ATTN_BWD3_SMEM];
+  if ((int)blockIdx.y < nkb) attn_bwd_dkdv3_body<NW>(a, blockIdx.x, blockIdx.y, smem);
+  else attn_bwd_dq3_body<NW>(a, blockIdx.x, (int)blockIdx.y - nkb, (int)gridDim.y - nkb, smem, false);
+}
+
 AttnArgs to_args(const tt2_attn_args* p) {
   AttnArgs a;
   a.q = p->q; a.k = p->k; a.v = p->v; a.o = p->o; a.dout = p->dout;
@@ -1024,6 +1053,16 @@ extern "C" int tt2_attn_bwd(const tt2_attn_args* p, hipStream_t s) {
   if (p->dtype == TT2_DT_BF16) {
     const int nq = v3_waves(p, p->tq, false), nk = v3_waves(p, p->tk, false);
     // the v3 dQ kernel computes delta = rowsum(dO * O) itself (and stores it for dK / dV)
+    static const int fused_mode = [] {   // TT2_ATTN_FUSED: 0 off, 1 non-causal (default), 2 all
+      const char* e = getenv("TT2_ATTN_FUSED");
+      return e ? atoi(e) : 1;
+    }();
+    if (nq == 4 && nk == 4 && (fused_mode == 2 || (fused_mode == 1 && !p->causal))) {
+      const int nkb = (p->tk + 127) / 128, nqb = (p->tq + 127) / 128;
+      hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16>, gprep, dim3(NT), 0, s, a);
+      hipLaunchKernelGGL(attn_bwd_fused3_kernel<4>, dim3(BH, nkb + nqb), dim3(256), 0, s, a, nkb);
+      return tt2_check_launch(hipGetLastError(), "tt2_attn_bwd");
+    }
     if (nq == 0) hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16>, gprep, dim3(NT), 0, s, a);
     if (nq == 4) hipLaunchKernelGGL(attn_bwd_dq3_kernel<4>, dim3(BH, (p->tq + 127) / 128), dim3(256), 0, s, a);
     else if (nq == 2) hipLaunchKernelGGL(attn_bwd_dq3_kernel<2>, dim3(BH, (p->tq + 63) / 64), dim3(128), 0, s, a);
