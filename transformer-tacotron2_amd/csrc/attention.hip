@@ -799,7 +799,9 @@ TT2_DEV void attn_bwd_dq3_body(const AttnArgs& a, int bx, int by, int ny, char* 
 template <int NW>
 // dK / dV body: workgroup (bx, by) of a (B*H, key blocks) grid; smem holds sQ[2][64 D],
 // sdO[2][64 D], sL[2][64], sDl[2][64]; reads delta (published by the dQ pass or attn_bwd_prep)
-TT2_DEV void attn_bwd_dkdv3_body(const AttnArgs& a, int bx, int by, char* smem) {
+// self_delta: compute delta = rowsum(dO * O) of each staged query tile here (from the dO
+// chunks already in registers and the matching O chunks) instead of reading a.delta
+TT2_DEV void attn_bwd_dkdv3_body(const AttnArgs& a, int bx, int by, char* smem, bool self_delta) {
   constexpr int NTH = NW * 64, PER = Stage3<NTH>::PER, KB = 32 * NW;
   bf16 (*sQ)[64 * D] = reinterpret_cast<bf16 (*)[64 * D]>(smem);
   bf16 (*sdO)[64 * D] = reinterpret_cast<bf16 (*)[64 * D]>(smem + 2 * 64 * D * sizeof(bf16));
@@ -818,6 +820,7 @@ TT2_DEV void attn_bwd_dkdv3_body(const AttnArgs& a, int bx, int by, char* smem) 
   bf16* dV = reinterpret_cast<bf16*>(a.dv) + (int64_t)b * a.Tk * a.dv_ld + h * D;
   const float* LSE = a.lse + (int64_t)bh * a.Tq;
   const float* DL = a.delta + (int64_t)bh * a.Tq;
+  const RowBuf Ob = row_buf(reinterpret_cast<const bf16*>(a.o) + (int64_t)b * a.Tq * a.o_ld + h * D, a.o_ld, a.Tq);
 
   bf16x8 fk[4], fv[4];
   own_frags(fk, K, kv, hi);
@@ -832,17 +835,33 @@ TT2_DEV void attn_bwd_dkdv3_body(const AttnArgs& a, int bx, int by, char* smem) 
   const int klim = key_limit(a, b);
   const int qstart = a.causal ? (k0 / 64) * 64 : 0;
   const int ntile = k0 < klim && a.Tq > qstart ? (a.Tq - qstart + 63) / 64 : 0;
+  uint4 rq[PER], rd[PER], ro[PER];
   auto stats = [&](int buf, int qb) {
     if (tid < 64) {
       const int q = qb + tid;
       sL[buf][tid] = q < a.Tq ? LSE[q] : INFINITY;
-      sDl[buf][tid] = q < a.Tq ? DL[q] : 0.f;
+      if (!self_delta) sDl[buf][tid] = q < a.Tq ? DL[q] : 0.f;
+    }
+    if (self_delta) {   // chunk c = tid + NTH i is row c >> 3, 8 columns; the row's 8 chunks sit in 8 lanes
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        union { uint4 u; bf16x8 v; } x, y;
+        x.u = rd[i];
+        y.u = ro[i];
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += (float)x.v[j] * (float)y.v[j];
+        d += __shfl_xor(d, 1, 64);
+        d += __shfl_xor(d, 2, 64);
+        d += __shfl_xor(d, 4, 64);
+        if ((tid & 7) == 0) sDl[buf][(tid + NTH * i) >> 3] = d;
+      }
     }
   };
-  uint4 rq[PER], rd[PER];
   if (ntile > 0) {
     g2r3<NTH>(rq, Q, qstart, tid);
     g2r3<NTH>(rd, dO, qstart, tid);
+    if (self_delta) g2r3<NTH>(ro, Ob, qstart, tid);
     r2s3<NTH>(rq, sQ[0], tid);
     r2s3<NTH>(rd, sdO[0], tid);
     stats(0, qstart);
@@ -855,6 +874,7 @@ TT2_DEV void attn_bwd_dkdv3_body(const AttnArgs& a, int bx, int by, char* smem) 
     if (more) {
       g2r3<NTH>(rq, Q, q0 + 64, tid);
       g2r3<NTH>(rd, dO, q0 + 64, tid);
+      if (self_delta) g2r3<NTH>(ro, Ob, q0 + 64, tid);
     }
     const bf16* cQ = sQ[BUF];
     const bf16* cD = sdO[BUF];
@@ -932,16 +952,16 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dq3_kernel(AttnArgs a) {
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv3_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[ATTN_BWD3_SMEM];
-  attn_bwd_dkdv3_body<NW>(a, blockIdx.x, blockIdx.y, smem);
+  attn_bwd_dkdv3_body<NW>(a, blockIdx.x, blockIdx.y, smem, false);
 }
 
-// dQ and dK / dV in one launch (delta from attn_bwd_prep_kernel beforehand): y < nkb are the
-// key blocks, the rest the query blocks, so the (few, long) dK / dV workgroups of a short key
-// range run beside the dQ workgroups instead of after them on a mostly idle chip
+// dQ and dK / dV in one launch (each computes delta itself): y < nkb are the key blocks, the
+// rest the query blocks, so the (few, long) dK / dV workgroups of a short key range run
+// beside the dQ workgroups instead of after them on a mostly idle chip
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void attn_bwd_fused3_kernel(AttnArgs a, int nkb) {
   __shared__ __attribute__((aligned(16))) char smem[ATTN_BWD3_SMEM];
-  if ((int)blockIdx.y < nkb) attn_bwd_dkdv3_body<NW>(a, blockIdx.x, blockIdx.y, smem);
+  if ((int)blockIdx.y < nkb) attn_bwd_dkdv3_body<NW>(a, blockIdx.x, blockIdx.y, smem, true);
   else attn_bwd_dq3_body<NW>(a, blockIdx.x, (int)blockIdx.y - nkb, (int)gridDim.y - nkb, smem, false);
 }
 
@@ -1059,7 +1079,6 @@ extern "C" int tt2_attn_bwd(const tt2_attn_args* p, hipStream_t s) {
     }();
     if (nq == 4 && nk == 4 && (fused_mode == 2 || (fused_mode == 1 && !p->causal))) {
       const int nkb = (p->tk + 127) / 128, nqb = (p->tq + 127) / 128;
-      hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16>, gprep, dim3(NT), 0, s, a);
       hipLaunchKernelGGL(attn_bwd_fused3_kernel<4>, dim3(BH, nkb + nqb), dim3(256), 0, s, a, nkb);
       return tt2_check_launch(hipGetLastError(), "tt2_attn_bwd");
     }
