@@ -178,3 +178,23 @@ def test_conv_weight_flip_batch(dtype):
     ops.conv_weight_flip_batch(jobs)
     for w, wd, cout, cin, K in jobs:
         assert torch.equal(wd, w.flip(1).permute(2, 1, 0).reshape(cin, K * cout))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("c,t_offset", [(512, 0), (512, 3), (36, 0)])
+def test_posenc_fwd(dtype, c, t_offset):
+    """out = drop(x + alpha * pe[t % T + t_offset]) (8-wide path for C % 8 == 0, scalar else)."""
+    from tt2 import ops
+    B, T = 3, 37
+    m = B * T
+    x = torch.randn(m, c, device="cuda").to(dtype)
+    pe = torch.randn(T + 8, c, device="cuda")
+    alpha = torch.tensor([1.7], device="cuda")
+    out = torch.empty_like(x)
+    seed = torch.tensor([5], dtype=torch.int32, device="cuda")
+    ops.posenc_fwd(x, alpha, pe, out, m, T, drop=ops.Drop(seed, 9, 0.2), t_offset=t_offset)
+    rows = torch.arange(m, device="cuda") % T + t_offset
+    ref = x.double() + 1.7 * pe.double()[rows]
+    keep = torch.from_numpy(dropout_keep(5, 9, m * c, 0.2)).view(m, c).cuda()
+    ref = ref * keep / 0.8
+    assert rel(out, ref) < (1e-6 if dtype == torch.float32 else 8e-3)

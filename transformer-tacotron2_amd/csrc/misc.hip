@@ -155,6 +155,45 @@ __global__ void pe_fwd_kernel(const T* x, const float* alpha, const float* pe, T
     out[i] = from_f32<T>(v);
   }
 }
+// 8 elements per thread (C % 8 == 0, bf16 / f32): 16-B loads, 32-bit chunk indexing, the
+// dropout bits of the chunk from drop_bits8, nontemporal stores
+template <typename T>
+__global__ __launch_bounds__(NT) void pe_fwd8_kernel(const T* x, const float* alpha, const float* pe, T* out, int M,
+                                                     int C, int Tlen, int t_off, const int32_t* t_ptr, DropDesc drop) {
+  const int cpr = C >> 3, nchunk = M * cpr;
+  const float al = *alpha;
+  if (t_ptr) t_off += *t_ptr;
+  const uint32_t seed = drop.thr ? *drop.seed : 0u;
+  for (int q = blockIdx.x * NT + threadIdx.x; q < nchunk; q += gridDim.x * NT) {
+    const int m = q / cpr, c0 = (q - m * cpr) * 8, t = m % Tlen + t_off;
+    const uint32_t i0 = (uint32_t)m * C + c0;
+    float v[8];
+    if constexpr (sizeof(T) == 2) {
+      const bf16x8 xv = *reinterpret_cast<const bf16x8*>(x + i0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (float)xv[j];
+    } else {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(x + i0), b = *reinterpret_cast<const f32x4*>(x + i0 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+    }
+    const f32x4 p0 = *reinterpret_cast<const f32x4*>(pe + (int64_t)t * C + c0);
+    const f32x4 p1 = *reinterpret_cast<const f32x4*>(pe + (int64_t)t * C + c0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] += al * p0[j]; v[4 + j] += al * p1[j]; }
+    if (drop.thr) drop_apply8(drop, seed, i0, v);
+    if constexpr (sizeof(T) == 2) {
+      bf16 o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(o), reinterpret_cast<u32x4*>(out + i0));
+    } else {
+      __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f32x4*>(out + i0));
+      __builtin_nontemporal_store(f32x4{v[4], v[5], v[6], v[7]}, reinterpret_cast<f32x4*>(out + i0) + 1);
+    }
+  }
+}
+
 // dx = drop'(dout); part[block] = sum dx * pe
 // dx = drop(dout) and a per-block partial of dalpha = sum(dx * pe[t]).  8-element
 // chunks (C % 8 == 0): 16-B loads, 32-bit chunk indexing.
@@ -529,6 +568,18 @@ extern "C" int tt2_embedding_bwd(const int64_t* ids, const void* dout, float* dt
 
 extern "C" int tt2_posenc_fwd(const tt2_pe_args* p, hipStream_t s) {
   DropDesc d{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
+  const bool v8 = p->c % 8 == 0 && (int64_t)p->m * p->c < (1ll << 31) &&
+                  reinterpret_cast<uintptr_t>(p->x) % 16 == 0 && reinterpret_cast<uintptr_t>(p->out) % 16 == 0;
+  if (v8) {
+    const int g8 = grid_for((int64_t)p->m * p->c / 8);
+    if (p->dtype == TT2_DT_BF16)
+      hipLaunchKernelGGL(pe_fwd8_kernel<bf16>, dim3(g8), dim3(NT), 0, s, (const bf16*)p->x, p->alpha, p->pe,
+                         (bf16*)p->out, p->m, p->c, p->t, p->t_offset, p->t_ptr, d);
+    else
+      hipLaunchKernelGGL(pe_fwd8_kernel<float>, dim3(g8), dim3(NT), 0, s, (const float*)p->x, p->alpha, p->pe,
+                         (float*)p->out, p->m, p->c, p->t, p->t_offset, p->t_ptr, d);
+    return tt2_check_launch(hipGetLastError(), "tt2_posenc_fwd");
+  }
   const int g = grid_for((int64_t)p->m * p->c);
   if (p->dtype == TT2_DT_BF16)
     hipLaunchKernelGGL(pe_fwd_kernel<bf16>, dim3(g), dim3(NT), 0, s, (const bf16*)p->x, p->alpha, p->pe,
