@@ -92,20 +92,22 @@ def test_layernorm_bwd_chained_finalize(m1, m2):
                                   prev=prev if mode == "chain" else None, **kw)
             if mode == "standalone" and i == 0:
                 ops.layernorm_bwd_finalize(a)
+            if mode == "grouped" and i == 0:   # completed in a (here empty) grouped GEMM's reduce launch
+                ops.gemm_grouped([], fin=a)
             prev = a
             outs.append((dx, dbr, dg, db, dbias))
         torch.cuda.synchronize()
         return outs
 
-    ref, chain, alone = run("plain"), run("chain"), run("standalone")
-    for got in (chain, alone):
+    ref, chain, alone, grouped = run("plain"), run("chain"), run("standalone"), run("grouped")
+    for got in (chain, alone, grouped):
         for (rx, rb, rg, rbe, rbi), (gx, gb, gg, gbe, gbi) in zip(ref, got):
             assert torch.equal(rx, gx) and torch.equal(rb, gb)
             for r, v in ((rg, gg), (rbe, gbe), (rbi, gbi)):
                 assert rel(v, r) < 1e-5
     # chained and standalone completions share one summation order: bitwise equal
-    for a_, b_ in zip(chain[0][2:], alone[0][2:]):
-        assert torch.equal(a_, b_)
+    for a_, b_, c_ in zip(chain[0][2:], alone[0][2:], grouped[0][2:]):
+        assert torch.equal(a_, b_) and torch.equal(a_, c_)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
