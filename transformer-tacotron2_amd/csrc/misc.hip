@@ -272,15 +272,56 @@ template <typename T>
 __global__ __launch_bounds__(NT) void loss_kernel(const float* heads, int64_t hld, const float* after,
                                                   const float* target, const int32_t* mel_len, int B, int Tlen,
                                                   int NM, float pos_weight, float gscale, float* g_heads, T* g_after, float* part,
-                                                  int separate) {
+                                                  int separate, int vec4) {
   __shared__ float red[3][NT / 64];
   int nvalid = 0;
   for (int b = 0; b < B; ++b) nvalid += min(max(mel_len[b], 0), Tlen);
   const float inv_n = nvalid > 0 ? gscale / nvalid : 0.f;
   const float inv_nm = inv_n / NM;
   const int M = B * Tlen;
-  const int64_t total = (int64_t)M * hld;
+  const int64_t total = vec4 ? 0 : (int64_t)M * hld;
   float sb = 0.f, sa = 0.f, ss = 0.f;
+  if (vec4) {   // 4 columns per thread (hld, NM % 4 == 0, 16-B aligned rows): 32-bit indexing, vector loads
+    const int cpr = (int)(hld >> 2), nchunk = M * cpr;
+    for (int q = blockIdx.x * NT + threadIdx.x; q < nchunk; q += gridDim.x * NT) {
+      const int m = q / cpr, c0 = (q - m * cpr) * 4;
+      const int b = m / Tlen, t = m - b * Tlen;
+      const int len = mel_len[b];
+      const bool valid = t < len;
+      const f32x4 hv = *reinterpret_cast<const f32x4*>(heads + (int64_t)m * hld + c0);
+      f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (c0 + 4 <= NM) {
+        const int64_t j = (int64_t)m * NM + c0;
+        const f32x4 tg = *reinterpret_cast<const f32x4*>(target + j), af = *reinterpret_cast<const f32x4*>(after + j);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float db = hv[k] - tg[k], da = af[k] - tg[k];
+          float ga = 0.f;
+          if (valid) {
+            sb += db * db;
+            sa += da * da;
+            g[k] = 2.f * db * inv_nm;
+            ga = 2.f * da * inv_nm;
+          }
+          g_after[j + k] = from_f32<T>(ga);
+          if (!separate) g[k] += ga;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (c0 + k != NM || !valid) continue;
+          const float x = hv[k];
+          const float y = (t == len - 1) ? 1.f : 0.f;
+          const float lsp = fminf(x, 0.f) - log1pf(expf(-fabsf(x)));
+          const float lsn = fminf(-x, 0.f) - log1pf(expf(-fabsf(x)));
+          ss += -(pos_weight * y * lsp + (1.f - y) * lsn);
+          const float sg = 1.f / (1.f + expf(-x));
+          g[k] = (pos_weight * y * (sg - 1.f) + (1.f - y) * sg) * inv_n;
+        }
+      }
+      *reinterpret_cast<f32x4*>(g_heads + (int64_t)m * hld + c0) = g;
+    }
+  }
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
     const int m = (int)(i / hld), c = (int)(i % hld);
     const int b = m / Tlen, t = m % Tlen;
@@ -634,14 +675,17 @@ extern "C" int tt2_tts_loss(const tt2_loss_args* p, hipStream_t s) {
   if (!p->workspace || p->ws_bytes < tt2_loss_workspace_size())
     return tt2_set_error(TT2_E_INVALID, "tt2_tts_loss: workspace");
   float* part = reinterpret_cast<float*>(p->workspace);
+  auto al16 = [](const void* q) { return reinterpret_cast<uintptr_t>(q) % 16 == 0; };
+  const int vec4 = p->heads_ld % 4 == 0 && p->n_mels % 4 == 0 && al16(p->heads) && al16(p->g_heads) &&
+                   al16(p->mel_after) && al16(p->target);
   if (p->grad_dtype == TT2_DT_BF16)
     hipLaunchKernelGGL(loss_kernel<bf16>, dim3(TT2_LOSS_BLOCKS), dim3(NT), 0, s, p->heads, p->heads_ld,
                        p->mel_after, p->target, p->mel_len, p->batch, p->t, p->n_mels, p->pos_weight, p->grad_scale, p->g_heads,
-                       (bf16*)p->g_after, part, p->separate_grads);
+                       (bf16*)p->g_after, part, p->separate_grads, vec4);
   else
     hipLaunchKernelGGL(loss_kernel<float>, dim3(TT2_LOSS_BLOCKS), dim3(NT), 0, s, p->heads, p->heads_ld,
                        p->mel_after, p->target, p->mel_len, p->batch, p->t, p->n_mels, p->pos_weight, p->grad_scale, p->g_heads,
-                       (float*)p->g_after, part, p->separate_grads);
+                       (float*)p->g_after, part, p->separate_grads, vec4);
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(64), 0, s, part, TT2_LOSS_BLOCKS, p->mel_len, p->batch,
                      p->t, p->n_mels, p->loss_out);
   return tt2_check_launch(hipGetLastError(), "tt2_tts_loss");
