@@ -452,7 +452,15 @@ TT2_DEV void splitk_reduce_body(const float* ws, int splits, const EpiParams& E,
         hi += wz[1];
       }
       const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const int m = (int)(8 * i / N), n = (int)(8 * i % N);
+      int m, n;
+      if (total < (1ll << 31)) {   // 32-bit division (the usual case) instead of a 64-bit one per chunk
+        const uint32_t e = 8u * (uint32_t)i;
+        m = (int)(e / (uint32_t)N);
+        n = (int)(e - (uint32_t)m * (uint32_t)N);
+      } else {
+        m = (int)(8 * i / N);
+        n = (int)(8 * i % N);
+      }
       epi_store8(E, seed, m, n, N, v);
     }
     return;
