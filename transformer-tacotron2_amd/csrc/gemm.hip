@@ -1039,6 +1039,7 @@ struct G7Group {
   G7Prob p[G7_MAXP];
   int np, items;
   G7Fin fin;   // nb == 0: none
+  int fin_only;   // the reduce launch holds only the finalize plane (no split problem to reduce)
 };
 constexpr int G7_FIN_WAVES = 4;   // columns per 256-thread reduce block
 
@@ -1330,7 +1331,7 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7g_kernel(G7Group G) {
 // split-K reduce of every split problem of a group (blockIdx.y = problem); plane y = np, when
 // present, finalizes the deferred LayerNorm column sums (4 loads in flight per lane)
 __global__ void gemm_splitk_reduce_g(G7Group G) {
-  if ((int)blockIdx.y == G.np) {
+  if (G.fin_only || (int)blockIdx.y == G.np) {
     const G7Fin& f = G.fin;
     const int o = blockIdx.x * G7_FIN_WAVES + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (o >= 3 * f.C) return;
@@ -1830,6 +1831,7 @@ extern "C" int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int n, const tt2
   }
   const int fin_blocks = G.fin.nb ? (3 * G.fin.C + G7_FIN_WAVES - 1) / G7_FIN_WAVES : 0;
   if (G.np == 0) {
+    G.fin_only = 1;
     if (fin_blocks) hipLaunchKernelGGL(gemm_splitk_reduce_g, dim3(fin_blocks, 1), dim3(256), 0, stream, G);
     return tt2_check_launch(hipGetLastError(), "tt2_gemm_grouped");
   }
@@ -1846,7 +1848,10 @@ extern "C" int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int n, const tt2
   else if (ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<false, true>), dim3(G.items), dim3(G7_NT), 0, stream, G);
   else hipLaunchKernelGGL((gemm7g_kernel<false, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
   if (main_only) reduce_blocks = 0;
-  if (reduce_blocks > 0 || fin_blocks > 0)
+  G.fin_only = reduce_blocks == 0 && fin_blocks > 0;
+  if (G.fin_only)
+    hipLaunchKernelGGL(gemm_splitk_reduce_g, dim3(fin_blocks, 1), dim3(256), 0, stream, G);
+  else if (reduce_blocks > 0)
     hipLaunchKernelGGL(gemm_splitk_reduce_g, dim3(std::max(reduce_blocks, fin_blocks), G.np + (fin_blocks ? 1 : 0)),
                        dim3(256), 0, stream, G);
   return tt2_check_launch(hipGetLastError(), "tt2_gemm_grouped");
