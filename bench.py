@@ -4,6 +4,11 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+With --gpus N > 1 and no torchrun environment (WORLD_SIZE unset), this process starts the
+N rank processes itself (fresh interpreters; it makes no GPU call of its own), waits for
+them and forwards rank 0's JSON line; it exits non-zero if any rank fails, and a line
+whose n_gpus differs from N is never printed.
+
 Workload (BASELINE.json configs[1], the metric's single-GPU config): one
 training step = forward + loss + backward + (RCCL gradient all-reduce when
 N > 1) + fused Adam/clip, bf16 compute with f32 master weights, B = 16
@@ -22,6 +27,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -346,6 +353,60 @@ def longform_bench(model):
                          "algo_bytes": algo, "note": "weights per step + running utterances' KV bytes only"}}
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """Start n rank processes of this script (torchrun's env contract: RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR/PORT), wait for all of them, forward rank 0's JSON line.
+    Any rank failing ends the others and the launch (non-zero exit)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    log(f"[bench] launched {n} ranks (pids {[p.pid for p in procs]}), rendezvous 127.0.0.1:{port}")
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p for p in procs if p.poll() not in (None, 0)]
+        if bad:
+            rc = bad[0].returncode
+            log(f"[bench] rank process {procs.index(bad[0])} exited with {rc}; stopping the others")
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    out = procs[0].stdout.read()
+    codes = [p.wait() for p in procs]
+    if rc == 0 and any(codes):
+        rc = next(c for c in codes if c)
+    if rc != 0:
+        return rc if rc > 0 else 1
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    if not lines:
+        log("[bench] rank 0 printed no JSON line")
+        return 1
+    rec = json.loads(lines[-1])
+    if rec.get("n_gpus") != n:
+        log(f"[bench] rank 0 reported n_gpus={rec.get('n_gpus')} for a {n}-GPU launch; not printing it")
+        return 1
+    print(lines[-1], flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -359,15 +420,18 @@ def main():
     ap.add_argument("--force-dp", action="store_true", help="dev: run the DP path (bucketed RCCL all-reduce, "
                     "segmented graph) even at world size 1")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))    # before anything touches the GPU
 
     from tt2.config import TTSConfig
-    from tt2.dist import attach, broadcast_params, init_from_env
+    from tt2.dist import attach, broadcast_params, init_from_env, rccl_env
     from tt2.model import TransformerTTS
 
     rank, world, local = init_from_env()
-    torch.cuda.set_device(local % torch.cuda.device_count())   # ranks > GPUs: a 1-GPU gloo rehearsal
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}")
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to report a dp{world} run "
+                         f"for a {args.gpus}-GPU request")
+    torch.cuda.set_device(local % torch.cuda.device_count())   # ranks > GPUs: a 1-GPU gloo rehearsal
     torch.manual_seed(0)
     model = TransformerTTS(TTSConfig(), dtype=torch.bfloat16)
     # random init of the architecture (seeded), then the standard Transformer-TTS Adam/Noam setup
@@ -429,6 +493,13 @@ def main():
     frames = world * B_PER_GPU * TY * args.steps
     value = frames / dt
     log(f"[bench] {dt / args.steps * 1e3:.2f} ms/step, loss {lval:.4f}")
+    comm = None
+    if sync is not None:   # every rank: the bucketed exchange alone (outside the timed region)
+        comm = {"sync": "rccl in-graph (libtt2 communicator, comm stream inside the step graph)" if sync.in_graph
+                else "segmented (torch.distributed between graph segments)",
+                "backend": dist.get_backend(), "bucket_mb": round((sync.buckets[0][1] - sync.buckets[0][0]) * 4 / 2**20, 2),
+                "rccl_env": rccl_env(), "allreduce_alone": sync.bench_allreduce()}
+        log(f"[bench] all-reduce alone: {comm['allreduce_alone']}")
 
     rag = None
     if rank == 0 and world == 1 and not args.no_ragged:
@@ -461,6 +532,7 @@ def main():
                        "text_len": TX, "n_mels": NMEL, "params": model.n_params(), "parallelism": f"dp{world}",
                        "graph": not args.no_graph},
             "loss": round(lval, 5),
+            "grad_exchange": comm,
             "roofline": rl,
             "train_ragged": rag,
             "cpu_baseline": cpu,
@@ -468,6 +540,8 @@ def main():
             "decode_longform": lf,
         }
         print(json.dumps(out), flush=True)
+    if sync is not None:
+        sync.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 

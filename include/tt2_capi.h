@@ -253,7 +253,7 @@ typedef struct tt2_decode_desc {
   const void* fc2_w; const float* fc2_b;
   const void* proj_w; const float* proj_b;
   const float* alpha;                        /* decoder PE scale (device scalar) */
-  const float* pe_table;                     /* [>= t_max][d] */
+  const float* pe_table;                     /* [>= t_max + 1][d] */
   tt2_dec_layer layers[TT2_MAX_DEC_LAYERS];
   const void* heads_w; const float* heads_b; /* [n_mels + 1, d]: mel rows, then the stop row */
   const void* mem_kv;        /* [batch * text_len, n_layers * 2d]: layer l's K at column 2dl, V at 2dl + d */
@@ -274,7 +274,8 @@ int tt2_decode_reset(const tt2_decode_desc* d, uint32_t seed0, hipStream_t strea
 /* one step as eager launches */
 int tt2_decode_step(const tt2_decode_desc* d, hipStream_t stream);
 int tt2_decode_graph_create(const tt2_decode_desc* d, hipStream_t stream, tt2_decode_graph_t* out);
-/* n_steps replays; frames past t_max are not emitted */
+/* n_steps replays.  The device step counter saturates at t_max: replays past it write no
+ * KV-cache row, emit no frame and leave every output unchanged. */
 int tt2_decode_graph_launch(tt2_decode_graph_t g, int32_t n_steps, hipStream_t stream);
 int tt2_decode_graph_destroy(tt2_decode_graph_t g);
 

@@ -54,3 +54,26 @@ def test_longform_algo_bytes_counts_running_utterances_only():
     got = bench.longform_algo_bytes(lens, 3)
     want = 3 * bench.LF_W_BYTES + 4 * bench.LF_CROSS_BYTES + bench.LF_KEY_BYTES * (1 + (1 + 2 + 3))
     assert abs(got - want) < 1e-6 * want
+
+
+def test_multi_gpu_request_without_torchrun_spawns_ranks_and_fails_loudly():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts 2 rank processes itself.  Here (no GPU)
+    the ranks rendezvous over gloo and then fail at their first device call: the launcher
+    must exit non-zero and print no JSON line (never a dp1 line for a dp2 request)."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["TT2_DIST_TIMEOUT_S"] = "60"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "1"], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "launched 2 ranks" in r.stderr
+
+
+def test_world_size_mismatch_is_refused():
+    """Under torchrun with WORLD_SIZE != --gpus the rank refuses to report."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "refusing" in r.stderr

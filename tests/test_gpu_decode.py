@@ -1,4 +1,5 @@
-"""AR decode path vs the CPU oracle (GPU): forced length, prenet dropout off.
+"""AR decode path vs the CPU oracle (GPU): forced length, prenet dropout switched off for
+parity (it is on by default at inference, as Tacotron2 decodes).
 fp32 mode must match within 1e-3; the hipGraph replay must equal eager launches."""
 import pytest
 import torch
@@ -35,7 +36,7 @@ def test_decode_matches_oracle(dtype, tol):
     oracle, model, text, tl = setup(dtype)
     T = 14
     ref_after, _, ref_before, ref_stop = oracle.infer(text, tl, T, force_len=True)
-    after, out_len = model.infer(text, tl, T, stop_threshold=None)
+    after, out_len = model.infer(text, tl, T, stop_threshold=None, prenet_dropout=False)
     assert after.shape == ref_after.shape
     assert rel(after, ref_after) < tol
     dec = model._decoders[(3, 17, T, False)]
@@ -47,8 +48,8 @@ def test_decode_matches_oracle(dtype, tol):
 def test_graph_replay_equals_eager():
     _, model, text, tl = setup(torch.bfloat16)
     T = 10
-    a1, _ = model.infer(text, tl, T, stop_threshold=None, use_graph=True)
-    a2, _ = model.infer(text, tl, T, stop_threshold=None, use_graph=False)
+    a1, _ = model.infer(text, tl, T, stop_threshold=None, use_graph=True, prenet_dropout=False)
+    a2, _ = model.infer(text, tl, T, stop_threshold=None, use_graph=False, prenet_dropout=False)
     assert torch.equal(a1, a2)
 
 
@@ -59,8 +60,8 @@ def test_decode_schedules_match():
     _, model, text, tl = setup(torch.bfloat16)
     T = 10
     model.eval()
-    ref = Decoder(model.engine, 3, 17, T, schedule=SCHEDULE_PLAIN)
-    out = Decoder(model.engine, 3, 17, T, schedule=SCHEDULE_SPLIT)
+    ref = Decoder(model.engine, 3, 17, T, schedule=SCHEDULE_PLAIN, prenet_dropout=False)
+    out = Decoder(model.engine, 3, 17, T, schedule=SCHEDULE_SPLIT, prenet_dropout=False)
     a, _ = ref.run(text.cuda(), tl.cuda(), T, stop_threshold=None)
     b, _ = out.run(text.cuda(), tl.cuda(), T, stop_threshold=None)
     assert rel(b, a) < 2e-2
@@ -73,7 +74,7 @@ def test_stop_token_early_exit():
     with torch.no_grad():   # push the stop logit up so every utterance stops immediately
         e.P("heads.b")[80] = 50.0
         e.sync_shadow()
-    after, out_len = model.infer(text, tl, 64, stop_threshold=0.5)
+    after, out_len = model.infer(text, tl, 64, stop_threshold=0.5, prenet_dropout=False)
     assert (out_len.cpu() == 1).all()
     assert after.shape[1] < 64
 
@@ -104,7 +105,7 @@ def test_decode_wide_batch_matches_oracle():
     for b in range(B):
         text[b, tl[b]:] = 0
     ref_after, _, ref_before, ref_stop = oracle.infer(text, tl, T, force_len=True)
-    after, out_len = model.infer(text, tl, T, stop_threshold=None)
+    after, out_len = model.infer(text, tl, T, stop_threshold=None, prenet_dropout=False)
     assert rel(after, ref_after) < 6e-2
     dec = model._decoders[(B, Tx, T, False)]
     assert rel(dec.mel_seq[:, :T], ref_before) < 6e-2
@@ -121,13 +122,13 @@ def test_long_form_limits_early_exit():
     text = torch.randint(1, 80, (B, Tx), generator=g).cuda()
     tl = torch.full((B,), Tx, dtype=torch.long, device="cuda")
     caps = torch.randint(300, 700, (B,), generator=g)
-    dec = Decoder(model.engine, B, Tx, Tm)
+    dec = Decoder(model.engine, B, Tx, Tm, prenet_dropout=False)
     after, out_len = dec.run(text, tl, Tm, stop_threshold=None, limits=caps)
     n = after.shape[1]
     assert int(caps.max()) <= n < int(caps.max()) + 32
     assert torch.equal(out_len.cpu(), caps)
     assert torch.isfinite(dec.mel_seq[:, :n]).all()
-    short = Decoder(model.engine, B, Tx, 8)
+    short = Decoder(model.engine, B, Tx, 8, prenet_dropout=False)
     short.run(text, tl, 8, stop_threshold=None)
     assert rel(short.mel_seq[:, :8], dec.mel_seq[:, :8]) < 1e-6
 
@@ -141,7 +142,7 @@ def test_decode_fp16_matches_oracle():
     ref_after, _, ref_before, ref_stop = oracle.infer(text, tl, T, force_len=True)
     errs = {}
     for dt in (torch.float16, torch.bfloat16):
-        dec = Decoder(model.engine, 3, 17, T, dtype=dt)
+        dec = Decoder(model.engine, 3, 17, T, dtype=dt, prenet_dropout=False)
         after, out_len = dec.run(text.cuda(), tl.cuda(), T, stop_threshold=None)
         errs[dt] = rel(dec.mel_seq[:, :T], ref_before)
         assert rel(after, ref_after) < 6e-2
@@ -176,7 +177,7 @@ def test_injected_stop_matches_oracle(use_graph):
     oracle, model, text, tl = setup(torch.float32)
     T = 16
     lens = torch.tensor([5, 9, 12])
-    dec = Decoder(model.engine, 3, 17, T)
+    dec = Decoder(model.engine, 3, 17, T, prenet_dropout=False)
     dec.inject_stop(lens)
     bias = dec.stop_bias.cpu()
     ref_after, ref_len, ref_before, _ = oracle.infer(text, tl, T, stop_bias=bias)
@@ -193,7 +194,7 @@ def test_injected_stop_matches_oracle(use_graph):
         # batch length (as a zero-padded batch in the reference would)
         padded = torch.cat([ref_before[b:b + 1, :n], torch.zeros(1, after.shape[1] - n, 80)], 1)
         assert rel(after[b, :n], oracle.postnet(padded)[0, :n]) < 1e-3
-    forced = Decoder(model.engine, 3, 17, T)
+    forced = Decoder(model.engine, 3, 17, T, prenet_dropout=False)
     forced.run(text.cuda(), tl.cuda(), T, stop_threshold=None)
     assert rel(dec.mel_seq[2, :12], forced.mel_seq[2, :12]) < 1e-6
 
@@ -228,7 +229,7 @@ def test_cfg3_full_workload(dtype, tol):
     B, Tx, T = 32, 128, 800
     text = torch.randint(1, 80, (B, Tx), generator=g)
     tl = torch.full((B,), Tx, dtype=torch.long)
-    dec = Decoder(model.engine, B, Tx, T)
+    dec = Decoder(model.engine, B, Tx, T, prenet_dropout=False)
     after, out_len = dec.run(text.cuda(), tl.cuda(), T, stop_threshold=None)
     assert after.shape == (B, T, 80) and (out_len.cpu() == T).all()
     frames = dec.mel_seq.cpu()
@@ -257,7 +258,7 @@ def test_cfg5_full_workload():
     text = torch.randint(1, 80, (B, Tx), generator=g)
     tl = torch.full((B,), Tx, dtype=torch.long)
     lens = torch.randint(1000, Tm + 1, (B,), generator=g)
-    dec = Decoder(model.engine, B, Tx, Tm, dtype=torch.float16)
+    dec = Decoder(model.engine, B, Tx, Tm, dtype=torch.float16, prenet_dropout=False)
     dec.inject_stop(lens)
     after, out_len = dec.run(text.cuda(), tl.cuda(), Tm, stop_threshold=0.5)
     n = after.shape[1]
@@ -275,3 +276,30 @@ def test_cfg5_full_workload():
         assert rel(after[b, :k], ma[0, :k]) < 3e-2
         if k < n:
             assert float(frames[b, k:n].abs().max()) == 0.0
+
+
+def test_replay_past_t_max_leaves_buffers_unchanged():
+    """The device step counter saturates at t_max: graph replays beyond it (through the C
+    ABI directly, past the host-side clamp) write no KV-cache row -- the next utterance's
+    cache rows and the row past the last layer stay as they were -- emit no frame and do
+    not advance the counter or the dropout seed."""
+    import ctypes as C
+    from tt2._lib import check, lib, stream_ptr
+    _, model, text, tl = setup(torch.bfloat16)
+    T = 6
+    for sched in (SCHEDULE_SPLIT, SCHEDULE_PLAIN):
+        dec = Decoder(model.engine, 3, 17, T, schedule=sched)
+        dec.run(text.cuda(), tl.cuda(), T + 5, stop_threshold=None)    # host clamp: T frames
+        assert dec.t.item() == T
+        ws0, mel0, stop0, seed0 = dec.ws.clone(), dec.mel_seq.clone(), dec.stop_seq.clone(), dec.seed.clone()
+        g = dec.capture(None)
+        check(lib().tt2_decode_graph_launch(C.c_void_p(g), 4, C.c_void_p(stream_ptr())), "launch")
+        torch.cuda.synchronize()
+        assert dec.t.item() == T and torch.equal(dec.seed, seed0)
+        assert torch.equal(dec.mel_seq, mel0) and torch.equal(dec.stop_seq, stop0)
+        # the KV cache [layer][b][t][K|V] is the workspace's tail: bit-identical (only scratch
+        # before it differs); a row-t_max write would land in the next utterance's rows
+        c = model.engine.cfg
+        cache_bytes = c.n_dec * 3 * T * 2 * c.d_model * 2
+        assert cache_bytes % 256 == 0
+        assert torch.equal(dec.ws[-cache_bytes:], ws0[-cache_bytes:])

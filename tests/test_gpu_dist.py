@@ -1,7 +1,8 @@
-"""Data-parallel train step on the GPU with a 1-rank RCCL group: the captured step is cut
-into graph segments at gradient-bucket boundaries so each bucket's all-reduce can start
-while the rest of the backward replays.  With one rank the all-reduce is the identity,
-so the segmented DP step must reproduce the single-graph step bit for bit."""
+"""Data-parallel train step on the GPU with a 1-rank RCCL group, both exchange paths:
+'rccl' (libtt2's communicator; the bucket all-reduces forked onto a comm stream INSIDE
+the one captured step graph) and 'segmented' (torch.distributed all-reduces between graph
+segments cut at bucket boundaries).  With one rank the all-reduce is the identity, so
+either DP step must reproduce the single-graph step bit for bit."""
 import os
 import socket
 
@@ -12,7 +13,7 @@ import torch.distributed as dist
 pytestmark = pytest.mark.gpu
 
 from tt2.config import TTSConfig  # noqa: E402
-from tt2.dist import GradSync, attach  # noqa: E402
+from tt2.dist import GradSync, RcclGradSync, attach  # noqa: E402
 from tt2.model import TransformerTTS  # noqa: E402
 
 
@@ -43,7 +44,8 @@ def _model():
     return m.train()
 
 
-def test_segmented_dp_graph_matches_single_graph(nccl_group):
+@pytest.mark.parametrize("kind", ["rccl", "segmented"])
+def test_dp_graph_matches_single_graph(nccl_group, kind):
     g = torch.Generator().manual_seed(3)
     B, Tx, Ty = 2, 24, 48
     text = torch.randint(1, 80, (B, Tx), generator=g).cuda()
@@ -51,24 +53,28 @@ def test_segmented_dp_graph_matches_single_graph(nccl_group):
     mel = torch.randn(B, Ty, 80, generator=g).cuda()
     ml = torch.tensor([48, 30]).cuda()
     ref, dp = _model(), _model()
-    sync = attach(dp)
-    assert len(sync.buckets) > 2
+    sync = attach(dp, kind=kind)
+    assert len(sync.buckets) > 2 and sync.in_graph == (kind == "rccl")
     for _ in range(2):   # eager warm-up (sizes workspaces)
         ref.train_step(text, tl, mel, ml)
         dp.train_step(text, tl, mel, ml, sync_grads=sync.finish)
     run_ref = ref.capture_train_step(B, Tx, Ty)
     run_dp = dp.capture_train_step(B, Tx, Ty, sync_grads=sync.finish)
     segs, g2 = dp._graphs[(B, Tx, Ty)]
-    assert g2 is not None and len(segs) > 2          # cut at bucket boundaries
+    if kind == "rccl":
+        assert g2 is None and len(segs) == 1          # one graph: all-reduces captured inside
+    else:
+        assert g2 is not None and len(segs) > 2      # cut at bucket boundaries
     for _ in range(3):
         la = run_ref(text, tl, mel, ml).clone()
         lb = run_dp(text, tl, mel, ml).clone()
         assert torch.equal(la, lb)
     torch.cuda.synchronize()
     assert torch.equal(ref.engine.params, dp.engine.params)
+    sync.close()
 
 
-class SnapshotSync(GradSync):
+class _Snap:
     """GradSync that snapshots each bucket on the compute stream at the moment its
     all-reduce is launched (what RCCL would read) and, in finish(), compares every snapshot
     with the final gradients.  A kernel that writes into a bucket after it was handed to
@@ -76,8 +82,7 @@ class SnapshotSync(GradSync):
     in an already-launched bucket -- shows up as a mismatch even on one rank, where the
     all-reduce itself is the identity."""
 
-    def __init__(self, *a, **kw):
-        super().__init__(*a, **kw)
+    def _init_snap(self):
         self.snaps, self.bad, self.steps = [], [], 0
 
     def _launch(self, lo, hi):
@@ -94,8 +99,23 @@ class SnapshotSync(GradSync):
         self.steps += 1
 
 
-@pytest.mark.parametrize("bucket_mb", [4, 25])
-def test_buckets_final_when_launched_cfg2(nccl_group, bucket_mb):
+class SnapshotSync(_Snap, GradSync):
+    def __init__(self, *a, **kw):
+        GradSync.__init__(self, *a, **kw)
+        self._init_snap()
+
+
+class RcclSnapshotSync(_Snap, RcclGradSync):
+    """The same check for the in-graph path, eagerly (its launch points are the same hook
+    calls; inside a capture the comm stream is ordered by the same stream waits)."""
+
+    def __init__(self, *a, **kw):
+        RcclGradSync.__init__(self, *a, **kw)
+        self._init_snap()
+
+
+@pytest.mark.parametrize("bucket_mb,cls", [(4, SnapshotSync), (25, SnapshotSync), (25, RcclSnapshotSync)])
+def test_buckets_final_when_launched_cfg2(nccl_group, bucket_mb, cls):
     """At the cfg2 shape (B = 16, 128 phonemes, 800 frames, dropout on): every gradient
     bucket is final when its all-reduce is launched, eagerly (hook during the backward)
     and in the segmented captured step (launches between graph segments)."""
@@ -107,7 +127,7 @@ def test_buckets_final_when_launched_cfg2(nccl_group, bucket_mb):
     ml = torch.full((B,), Ty, dtype=torch.int32).cuda()
     m = _model()
     eng = m.engine
-    sync = SnapshotSync(eng.grads, bucket_mb << 20)
+    sync = cls(eng.grads, bucket_mb << 20)
     eng.grad_scale = 1.0 / sync.world
     eng.grad_ready_hook = sync.ready
     assert len(sync.buckets) >= 3
@@ -115,6 +135,9 @@ def test_buckets_final_when_launched_cfg2(nccl_group, bucket_mb):
         m.train_step(text, tl, mel, ml, sync_grads=sync.finish)
     torch.cuda.synchronize()
     assert sync.steps == 2 and sync.bad == [], f"eager: buckets written after launch {sync.bad}"
+    if cls is RcclSnapshotSync:
+        sync.close()
+        return
     run = m.capture_train_step(B, Tx, Ty, sync_grads=sync.finish)
     for _ in range(2):
         run(text, tl, mel, ml)

@@ -1072,12 +1072,10 @@ extern "C" int tt2_attn_bwd(const tt2_attn_args* p, hipStream_t s) {
   dim3 gprep((p->batch * p->tq + 3) / 4);
   if (p->dtype == TT2_DT_BF16) {
     const int nq = v3_waves(p, p->tq, false), nk = v3_waves(p, p->tk, false);
-    // the v3 dQ kernel computes delta = rowsum(dO * O) itself (and stores it for dK / dV)
-    static const int fused_mode = [] {   // TT2_ATTN_FUSED: 0 off, 1 non-causal (default), 2 all
-      const char* e = getenv("TT2_ATTN_FUSED");
-      return e ? atoi(e) : 1;
-    }();
-    if (nq == 4 && nk == 4 && (fused_mode == 2 || (fused_mode == 1 && !p->causal))) {
+    // the v3 dQ kernel computes delta = rowsum(dO * O) itself (and stores it for dK / dV).
+    // Non-causal: dQ and dK / dV workgroups in one launch (the causal case gained nothing
+    // from the same fusion)
+    if (nq == 4 && nk == 4 && !p->causal) {
       const int nkb = (p->tk + 127) / 128, nqb = (p->tq + 127) / 128;
       hipLaunchKernelGGL(attn_bwd_fused3_kernel<4>, dim3(BH, nkb + nqb), dim3(256), 0, s, a, nkb);
       return tt2_check_launch(hipGetLastError(), "tt2_attn_bwd");

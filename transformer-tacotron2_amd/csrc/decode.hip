@@ -190,6 +190,7 @@ template <typename T>
 __global__ void kv_append_kernel(const T* src, int64_t src_ld, T* cache, int64_t c_bstride, int64_t c_ld, int n,
                                  int B, const int32_t* t_ptr) {
   const int t = *t_ptr;
+  if ((int64_t)t * c_ld >= c_bstride) return;   // t >= t_max: past the cache, nothing to append
   const int64_t total = (int64_t)B * n;
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
     const int b = (int)(i / n), c = (int)(i % n);
@@ -219,7 +220,7 @@ __global__ void decode_emit_kernel(const float* heads, int64_t hld, int B, int N
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && t < tmax) {   // the counter saturates at t_max
     t_ptr[0] = t + 1;
     if (seed) seed[0] += 1u;
   }

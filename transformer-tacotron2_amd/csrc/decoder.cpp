@@ -12,7 +12,9 @@
 //  * plain (f32 parity mode, or batch > 64): one launch per op (GEMM, KV append,
 //    LayerNorm, PE, emit), no slabs.
 // The step reads the frame index from the device counter d->step and bumps it in the
-// emit, so one captured step replays for every frame with no host round trip.
+// emit, so one captured step replays for every frame with no host round trip.  The counter
+// saturates at t_max: a replay past it writes no KV-cache row and emits no frame (the
+// pe_table must hold t_max + 1 rows, since such a replay still reads row t_max).
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -96,6 +98,8 @@ int validate(const tt2_decode_desc* d) {
   if (!d->mem_kv || !d->text_lens || !d->mel_seq || !d->stop_seq || !d->stop_len || !d->step || !d->seed ||
       !d->pe_table || !d->alpha)
     return tt2_set_error(TT2_E_INVALID, "tt2_decode: null buffer in the descriptor");
+  if (!(d->prenet_dropout >= 0.f && d->prenet_dropout < 1.f))
+    return tt2_set_error(TT2_E_INVALID, "tt2_decode: prenet_dropout must be in [0, 1)");
   if (!d->workspace || d->ws_bytes < tt2_decode_workspace_size(d))
     return tt2_set_error(TT2_E_INVALID, "tt2_decode: workspace smaller than tt2_decode_workspace_size()");
   return TT2_OK;

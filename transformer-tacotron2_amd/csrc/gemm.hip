@@ -817,7 +817,8 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const TE* X, int64_t ld
       float y = epi_value(Ep, seed, m, nn, E.alpha * v + e_bias + e_res[hrow]);
       y += e_pe;
       st_any(E.c, (int64_t)m * E.ldc + nn, E.c_dt, y);
-      if (F.kv && nn >= F.kv_col0)
+      // a row past the batch stride (t >= t_max: a replay beyond the cache) is not written
+      if (F.kv && nn >= F.kv_col0 && (int64_t)kv_t * F.kv_ld < F.kv_bstride)
         reinterpret_cast<TE*>(F.kv)[(int64_t)m * F.kv_bstride + (int64_t)kv_t * F.kv_ld + (nn - F.kv_col0)] = (TE)y;
       if (F.emit_mel && em_t < F.emit_tmax) {
         if (nn < F.emit_nmels) {
@@ -844,8 +845,10 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const TE* X, int64_t ld
       const int prev = __hip_atomic_fetch_add(F.emit_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       if (prev == (int)gridDim.x - 1) {
         *F.emit_done = 0;
-        *F.emit_t = em_t + 1;
-        if (F.emit_seed) *F.emit_seed += 1u;
+        if (em_t < F.emit_tmax) {   // the counter saturates at t_max (replays past it emit nothing)
+          *F.emit_t = em_t + 1;
+          if (F.emit_seed) *F.emit_seed += 1u;
+        }
       }
     }
   }
@@ -1366,22 +1369,13 @@ G7Prob g7_prob(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int 
   return P;
 }
 
-// loader-wave residual / gate staging (TT2_G7_PRE=0: the epilogue loads them itself; a
-// measurement switch, default on)
-bool g7_pre_on() {
-  static const bool on = [] {
-    const char* e = getenv("TT2_G7_PRE");
-    return !e || atoi(e) != 0;
-  }();
-  return on;
-}
-
 template <bool AK, bool BKC>
 hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
                    hipStream_t s, bool lds_epi) {
   G7Prob P = g7_prob(A, B, E, M, N, K, splits, ws);
   P.lds_epi = lds_epi && P.splits == 1 && E.c_dt == TT2_BF16 && E.vec && (N % 8) == 0;
-  P.pre_x = !P.lds_epi || !g7_pre_on() ? 0 : (E.res && E.res_dt == TT2_BF16) ? 1 : (E.gate && E.gate_dt == TT2_BF16) ? 2 : 0;
+  // the loader waves stage a bf16 residual / gate tile in LDS during the last K steps
+  P.pre_x = !P.lds_epi ? 0 : (E.res && E.res_dt == TT2_BF16) ? 1 : (E.gate && E.gate_dt == TT2_BF16) ? 2 : 0;
   hipEvent_t e0, e1;
   if (probe_take(e0, e1))
     hipExtLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, e0, e1, 0, P);
@@ -1589,17 +1583,9 @@ extern "C" size_t tt2_gemm_workspace_size(const tt2_gemm_args* a) {
   return (size_t)a->splits * a->m * (a->n + (a->a_ksum ? 1 : 0)) * sizeof(float);
 }
 
-// v7 epilogue form: 14 = through the LDS C image, 13 = straight from registers; auto
-// follows TT2_G7_EPI (measurement switch, default 1)
-static bool g7_lds_epi(int variant) {
-  if (variant == 14) return true;
-  if (variant == 13) return false;
-  static const int env = [] {
-    const char* e = getenv("TT2_G7_EPI");
-    return e ? atoi(e) : 1;
-  }();
-  return env != 0;
-}
+// v7 epilogue form: 13 = straight from registers; auto (and 14) = through the LDS C image
+// (-1.7 % step time)
+static bool g7_lds_epi(int variant) { return variant != 13; }
 
 // Kernel selection (also exported as tt2_gemm_plan): 1 v1 register-staged, 2 v2
 // LDS-DMA 128^2, 3 skinny (M <= 64), 13 v7 warp-specialised 256x128 (auto; variant 14
@@ -1648,7 +1634,9 @@ static int gemm_plan(const tt2_gemm_args* a) {
                     (int64_t)(a->trans_a ? a->k : a->m) * a->lda * 2 < (1LL << 31) &&
                     (int64_t)(a->trans_b ? a->k : a->n) * a->ldb * 2 < (1LL << 31);
   // v8 (64 x 64 tiles): K-contiguous A (conv allowed), no k-sums, bf16 C; forced by variant 15
+  // (v8 never writes split-K slabs: a request for raw partial slabs stays on v7)
   const bool v8ok = !a->trans_a && !a->a_ksum && a->b_conv_t == 0 && a->dtype_out == TT2_BF16 && a->n % 8 == 0 &&
+                    !(a->splits > 1 && a->main_only) &&
                     (int64_t)a->m * a->lda * 2 < (1LL << 31) &&
                     (int64_t)(a->trans_b ? a->k : a->n) * a->ldb * 2 < (1LL << 31);
   // auto: v8 when v7 would run at most 64 tiles (the encoder's 2048-row products with N = 512,
@@ -1710,7 +1698,15 @@ static int gemm_prep(const tt2_gemm_args* a, OpDesc& A, OpDesc& B, EpiParams& ep
   return TT2_OK;
 }
 
+// An armed launch probe belongs to the next main GEMM launch of this call only: whatever
+// path the call takes, it is disarmed on return (tt2_probe_ms then reports -1 for a slot
+// no probe-capable kernel consumed).
+struct ProbeDisarm {
+  ~ProbeDisarm() { g_probe_armed = -1; }
+};
+
 extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
+  ProbeDisarm disarm;
   if (a->m <= 0 || a->n <= 0) return TT2_OK;
   OpDesc A, B;
   EpiParams ep;
@@ -1793,6 +1789,7 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
 
 extern "C" int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int n, const tt2_ln_args* fin,
                                     hipStream_t stream) {
+  ProbeDisarm disarm;
   if (n <= 0 && !fin) return TT2_OK;
   if ((n > 0 && !probs) || n > G7_MAXP) return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: 1..8 problems");
   G7Group G{};

@@ -1,37 +1,66 @@
 """Data parallelism: utterance sharding + bucketed gradient all-reduce.
 
-One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).
-Rank r trains on its own B utterances; the loss kernel pre-scales every
-gradient by 1/world_size, so a SUM all-reduce of the flat f32 gradient buffer
-yields the data-parallel mean.  The buffer is cut into ~25 MB buckets from the
-END of the flat layout, because the backward produces gradients roughly in
+One process per GPU (torch.distributed for rendezvous, barriers and timing; the gradient
+exchange itself is RCCL over xGMI).  Rank r trains on its own B utterances; the loss
+kernel pre-scales every gradient by 1/world_size, so a SUM all-reduce of the flat f32
+gradient buffer yields the data-parallel mean.  The buffer is cut into ~25 MB buckets
+from the END of the flat layout, because the backward produces gradients roughly in
 reverse layout order (post-net, heads, decoder 5..0, ..., encoder embedding):
 ``ready(offset)`` is called by the engine whenever every gradient at flat index
->= offset is final and launches the buckets that became complete, so the
-all-reduce of late layers overlaps the backward of early ones (RCCL runs on its
-own stream, ordered after the producing kernels).  ``finish()`` launches the
-rest and makes the current stream wait for all of them before the optimizer.
+>= offset is final and launches the buckets that became complete, so the all-reduce of
+late layers overlaps the backward of early ones.  ``finish()`` launches the rest and
+makes the current stream wait for all of them before the optimizer.
+
+Two implementations of that contract:
+
+* ``RcclGradSync`` (the default with the ``nccl`` backend): libtt2's own RCCL
+  communicator (``tt2_comm_init`` / ``tt2_allreduce_bucket``, include/tt2_capi.h).  Each
+  bucket's all-reduce is issued on a dedicated comm stream that waits for an event on
+  the compute stream, and ``finish()`` joins the comm stream back.  Nothing touches the
+  host, so the whole step -- forward, backward, the bucket all-reduces overlapped with
+  it, Adam -- is captured as ONE hipGraph (``in_graph``): no graph split per bucket.
+* ``GradSync`` (gloo, or ``TT2_DP_SYNC=segmented``): torch.distributed async
+  all-reduces; a captured step is cut into graph segments at bucket boundaries and the
+  all-reduces run between segment replays (gloo work cannot be captured).
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
 
+# RCCL channel floor for the bucket all-reduce (read by RCCL at communicator init).  A
+# ring is bound by one xGMI link (~153 GB/s); more channels spread the ring traffic over
+# the 7 links of an MI355X.  Only a floor: an explicit NCCL_MIN_NCHANNELS wins.
+RCCL_MIN_CHANNELS = 32
+RCCL_ENV_KEYS = ("NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS", "NCCL_ALGO", "NCCL_PROTO", "RCCL_MSCCL_ENABLE",
+                 "NCCL_P2P_LEVEL")
+
+
+def rccl_env() -> dict:
+    """The RCCL environment in effect (recorded in bench.py's JSON line)."""
+    return {k: os.environ[k] for k in RCCL_ENV_KEYS if k in os.environ}
+
+
+def _buckets(n: int, per: int) -> list[tuple[int, int]]:
+    out, hi = [], n
+    while hi > 0:
+        lo = max(0, hi - per)
+        out.append((lo, hi))
+        hi = lo
+    return out
+
 
 class GradSync:
+    in_graph = False
+
     def __init__(self, flat_grads: torch.Tensor, bucket_bytes: int = 25 << 20, group=None):
         self.flat = flat_grads
         self.group = group
-        n = flat_grads.numel()
-        per = max(1, bucket_bytes // flat_grads.element_size())
-        self.buckets = []
-        hi = n
-        while hi > 0:
-            lo = max(0, hi - per)
-            self.buckets.append((lo, hi))
-            hi = lo
+        self.buckets = _buckets(flat_grads.numel(), max(1, bucket_bytes // flat_grads.element_size()))
         self.reset()
 
     @property
@@ -74,6 +103,89 @@ class GradSync:
             w.wait()
         self.reset()
 
+    def close(self):
+        pass
+
+    def bench_allreduce(self, reps: int = 5) -> dict:
+        """Times the bucketed all-reduce of the whole gradient buffer on its own (a copy,
+        outside any training step): algorithm and bus bandwidth of the exchange."""
+        buf = self.flat.clone()
+        saved, self.flat = self.flat, buf
+        try:
+            self.reset()
+            self.finish()                      # warm
+            torch.cuda.synchronize()
+            if dist.is_initialized():
+                dist.barrier(group=self.group)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            for _ in range(reps):
+                self.finish()
+            ev[1].record()
+            torch.cuda.synchronize()
+            t = ev[0].elapsed_time(ev[1]) / 1e3 / reps
+        finally:
+            self.flat = saved
+            self.reset()
+        nbytes = buf.numel() * buf.element_size()
+        w = self.world
+        return {"bytes": nbytes, "buckets": len(self.buckets), "ms": round(t * 1e3, 3),
+                "algbw_GBps": round(nbytes / t / 1e9, 1),
+                "busbw_GBps": round(2 * (w - 1) / w * nbytes / t / 1e9, 1) if w > 1 else None}
+
+
+class RcclGradSync(GradSync):
+    """Bucketed SUM all-reduce over libtt2's RCCL communicator on a comm stream, ordered
+    after the producing kernels by stream waits only (capturable: ``in_graph``)."""
+    in_graph = True
+
+    def __init__(self, flat_grads: torch.Tensor, bucket_bytes: int = 25 << 20, group=None):
+        from . import _lib
+        self._lib = _lib
+        super().__init__(flat_grads, bucket_bytes, group)
+        os.environ.setdefault("NCCL_MIN_NCHANNELS", str(RCCL_MIN_CHANNELS))
+        L = _lib.lib()
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        uid = (C.c_ubyte * 128)()   # ncclUniqueId
+        if rank == 0:
+            _lib.check(L.tt2_comm_unique_id(uid), "tt2_comm_unique_id")
+        if dist.is_initialized() and self.world > 1:
+            obj = [bytes(uid)]
+            dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                       group=group)
+            C.memmove(uid, obj[0], 128)
+        self.comm = C.c_void_p()
+        _lib.check(L.tt2_comm_init(C.byref(self.comm), self.world, uid, rank), "tt2_comm_init")
+        self.stream = torch.cuda.Stream()
+        self.pending = False
+
+    def _launch(self, lo, hi):
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)          # the bucket's gradients are final on `cur`
+        L = self._lib.lib()
+        base = self.flat.data_ptr() + lo * self.flat.element_size()
+        self._lib.check(L.tt2_allreduce_bucket(C.c_void_p(base), hi - lo, self._lib.dt(self.flat), self.comm,
+                                               C.c_void_p(self.stream.cuda_stream)), "tt2_allreduce_bucket")
+        self.pending = True
+
+    def finish(self):
+        while self.next < len(self.buckets):
+            self._launch(*self.buckets[self.next])
+            self.next += 1
+        if self.pending:
+            torch.cuda.current_stream().wait_stream(self.stream)
+        self.reset()
+
+    def reset(self):
+        super().reset()
+        self.pending = False
+
+    def close(self):
+        if getattr(self, "comm", None) and self.comm.value:
+            torch.cuda.synchronize()
+            self._lib.check(self._lib.lib().tt2_comm_destroy(self.comm), "tt2_comm_destroy")
+            self.comm = C.c_void_p()
+
 
 def init_from_env(backend: str | None = None):
     """Initialise torch.distributed from torchrun's env (RANK, WORLD_SIZE,
@@ -86,17 +198,33 @@ def init_from_env(backend: str | None = None):
             # TT2_DIST_BACKEND=gloo: rehearse the multi-rank control flow on one GPU
             backend = os.environ.get("TT2_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
+            # before any communicator exists: RCCL caches its parameters at first use
+            os.environ.setdefault("NCCL_MIN_NCHANNELS", str(RCCL_MIN_CHANNELS))
             torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
+        dist.init_process_group(backend=backend,
+                                timeout=timedelta(seconds=int(os.environ.get("TT2_DIST_TIMEOUT_S", "600"))))
     return rank, world, local
 
 
-def attach(model, group=None, bucket_bytes: int = 25 << 20) -> GradSync:
+def sync_kind(group=None) -> str:
+    """'rccl' (in-graph, libtt2's communicator) with the nccl backend, else 'segmented'
+    (torch.distributed work between graph segments); TT2_DP_SYNC overrides."""
+    env = os.environ.get("TT2_DP_SYNC")
+    if env in ("rccl", "segmented"):
+        return env
+    if dist.is_initialized() and dist.get_backend(group) == "nccl":
+        return "rccl"
+    return "segmented"
+
+
+def attach(model, group=None, bucket_bytes: int = 25 << 20, kind: str | None = None) -> GradSync:
     """Wire a TransformerTTS for data parallelism: gradient pre-scaling and the
-    bucket hook.  Returns the GradSync whose finish() goes between backward and
+    bucket hook.  Returns the sync object whose finish() goes between backward and
     the optimizer step (pass it as train_step(..., sync_grads=sync.finish))."""
     eng = model.engine
-    sync = GradSync(eng.grads, bucket_bytes, group)
+    kind = kind or sync_kind(group)
+    cls = RcclGradSync if kind == "rccl" else GradSync
+    sync = cls(eng.grads, bucket_bytes, group)
     eng.grad_scale = 1.0 / sync.world
     eng.grad_ready_hook = sync.ready
     return sync

@@ -34,26 +34,34 @@ STOP_FORCE = 1e4   # |injected stop logit|: dominates any logit the heads produc
 
 
 def stop_logit(threshold: float | None) -> float:
-    """Probability threshold -> logit (None: never stop)."""
+    """Probability threshold -> logit (None: never stop).  sigmoid(s) >= threshold, so a
+    threshold of 1 never stops (+inf) and 0 stops at the first frame (-inf)."""
     if threshold is None:
         return math.inf
+    if not 0.0 <= threshold <= 1.0:
+        raise ValueError(f"stop_threshold must be in [0, 1], got {threshold}")
+    if threshold >= 1.0:
+        return math.inf
+    if threshold <= 0.0:
+        return -math.inf
     return math.log(threshold / (1.0 - threshold))
 
 
 class Decoder:
-    def __init__(self, engine: TTSEngine, batch: int, text_len: int, t_max: int, prenet_dropout: bool = False,
+    def __init__(self, engine: TTSEngine, batch: int, text_len: int, t_max: int, prenet_dropout: bool = True,
                  seed: int = 0, dtype: torch.dtype | None = None, schedule: int = SCHEDULE_AUTO):
         """dtype: the decode step's storage type -- the engine's (bf16 / f32) by default, or
         torch.float16 on a bf16 engine: the step then runs on an f16 copy of
         the weights (refreshed from the f32 master at every encode()), an f16 KV cache and the
         encoder memory's K/V cast to f16; the encoder and post-net stay in the engine's dtype.
         prenet_dropout: Tacotron2's always-on pre-net dropout at inference (sites 128 / 129,
-        seed `seed` + frame index)."""
+        seed `seed` + frame index); on by default, False for parity runs against a
+        dropout-free reference."""
         self.e = e = engine
         c = e.cfg
         self.B, self.Tx, self.Tmax = batch, text_len, t_max
-        if t_max > c.max_len:
-            raise ValueError(f"t_max {t_max} exceeds the positional table ({c.max_len})")
+        if t_max >= c.max_len:   # a replay at the saturated counter reads PE row t_max
+            raise ValueError(f"t_max {t_max} must be below the positional table's {c.max_len} rows")
         self.prenet_dropout = prenet_dropout
         self.seed0 = seed
         dev = e.dev
@@ -190,6 +198,7 @@ class Decoder:
         stop probability >= threshold (tracked on the device, its attention then reads no keys)
         or at its own frame limit (limits: [B] caps).  The loop ends once every utterance is
         done (polled every check_every frames).  Returns frames run."""
+        n_steps = min(n_steps, self.Tmax)   # the cache holds t_max frames
         if limits is not None:
             limits = limits.to(device=self.stop_len.device, dtype=torch.long)
             n_steps = min(n_steps, int(limits.max()))
@@ -243,7 +252,7 @@ class Decoder:
             use_graph: bool = True, limits: torch.Tensor | None = None):
         """Greedy decode; returns (mel_after [B, T, 80] f32, out_len [B]).  limits: optional
         per-utterance frame caps [B] (out_len <= limits)."""
-        max_len = max_len or self.Tmax
+        max_len = min(max_len or self.Tmax, self.Tmax)
         self.encode(text, text_len)
         self.reset()
         n = self.decode_loop(max_len, use_graph, stop_threshold, limits=limits)

@@ -289,10 +289,11 @@ class TransformerTTS(nn.Module):
 
     # ------------------------------------------------------------ inference
     def infer(self, text, text_len, max_len: int, stop_threshold: float | None = 0.5, use_graph: bool = True,
-              prenet_dropout: bool = False):
+              prenet_dropout: bool = True):
         """Greedy AR synthesis (hipGraph-replayed decode step, KV cache, cached
         cross K/V).  Returns (mel_after [B, T, 80] f32, out_len [B]).
-        stop_threshold=None forces max_len frames."""
+        stop_threshold=None forces max_len frames.  prenet_dropout: Tacotron2's pre-net
+        dropout stays on at inference; False switches it off (parity runs)."""
         from .infer import Decoder
         self._sync_shadow()
         B, Tx = text.shape
@@ -368,6 +369,8 @@ class TransformerTTS(nn.Module):
         nbt_saved = dict(e.nbt)
         hook, e.grad_ready_hook = e.grad_ready_hook, None
         sync = getattr(sync_grads, "__self__", None)   # a GradSync's bound finish(): overlap buckets
+        if sync is not None and getattr(sync, "in_graph", False):
+            return self._capture_in_graph(A, sync, hook, nbt_saved)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g2 = torch.cuda.CUDAGraph() if sync_grads is not None else None
@@ -421,6 +424,41 @@ class TransformerTTS(nn.Module):
             if g2 is not None:
                 sync_grads()          # remaining buckets, then wait for all of them
                 g2.replay()
+            for k in e.nbt:
+                e.nbt[k] += 1
+            self._last = A
+            return A["loss"]
+
+        return run
+
+    def _capture_in_graph(self, A: Arena, sync, hook, nbt_saved):
+        """The data-parallel step as ONE hipGraph: the bucket all-reduces (RcclGradSync)
+        fork onto the comm stream inside the capture as each bucket's gradients become
+        final, overlap the rest of the backward, and join before Adam."""
+        e = self.engine
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        sync.reset()
+        try:
+            with torch.cuda.graph(g, stream=s, capture_error_mode=ops.CAPTURE_MODE):
+                e.grad_ready_hook = sync.ready
+                e.forward(A)
+                e.loss(A)
+                e.backward(A)
+                sync.finish()
+                e.optimizer_step()
+        finally:
+            e.grad_ready_hook = hook
+            sync.reset()
+        torch.cuda.current_stream().wait_stream(s)
+        e.nbt = nbt_saved
+        self._graphs[(A.B, A.Tx, A.Ty)] = ([(g, [])], None)
+
+        def run(text, text_len, mel, mel_len):
+            e.stage_inputs(A, text, text_len.to(torch.int32), mel, mel_len.to(torch.int32))
+            g.replay()
             for k in e.nbt:
                 e.nbt[k] += 1
             self._last = A
