@@ -237,8 +237,48 @@ def gemm_kernel_name(plan: int, ta: int, tb: int) -> str:
     return f"gemm plan {plan}"
 
 
-def roofline(model, text, tl, mel, ml):
-    """Live per-launch timing of the dominant kernel family in one eager step."""
+def graph_probe(model, text, tl, mel, ml, reps: int = 5):
+    """Per-launch GEMM times inside GRAPH-REPLAYED steps: the training step is captured once
+    more with libtt2's launch probe armed for every GEMM (under capture the probe brackets
+    each main kernel node with external event-record nodes), replayed `reps` times, and each
+    replay's probe events read back.  Returns {key: [launches/step, flops, seconds, bytes]}
+    averaged over the replays, or None if this runtime cannot capture the probe."""
+    from tt2 import ops
+    eng = model.engine
+    B, Tx, Ty = text.shape[0], text.shape[1], mel.shape[1]
+    A = eng.arena(B, Tx, Ty)
+    eng.stage_inputs(A, text, tl.to(torch.int32), mel, ml.to(torch.int32))
+    probe = ops.LaunchProbe()
+    g, s = torch.cuda.CUDAGraph(), torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    nbt = dict(eng.nbt)
+    ops.PROBE = probe
+    try:
+        with torch.cuda.graph(g, stream=s, capture_error_mode=ops.CAPTURE_MODE):
+            model._step_body(A)
+    finally:
+        ops.PROBE = None
+        eng.nbt = nbt
+    torch.cuda.current_stream().wait_stream(s)
+    acc: dict = {}
+    try:
+        for _ in range(reps):
+            g.replay()
+            for k, v in probe.summary().items():
+                d = acc.setdefault(k, [0, 0.0, 0.0, 0.0])
+                for i in range(4):
+                    d[i] += v[i] / reps
+    finally:
+        probe.close()
+        del g
+    return acc
+
+
+def roofline(model, text, tl, mel, ml, replay: bool = True):
+    """Live per-launch timing of the dominant kernel family: inside graph-replayed steps
+    (graph_probe; what the timed region runs) and, beside it, in one eager step (replay:
+    also re-time its launches back to back, reported for reference)."""
     from tt2 import ops
     # rank 0 only: the DP gradient hook must not fire (its all-reduces would have no peers)
     eng = model.engine
@@ -247,18 +287,26 @@ def roofline(model, text, tl, mel, ml):
     try:
         model.train_step(text, tl, mel, ml)
         summ = probe.summary()
+        gsum = graph_probe(model, text, tl, mel, ml) if text is not None else None
     finally:
         ops.PROBE = None
         eng.grad_ready_hook = hook
         if hasattr(probe, "close"):
             probe.close()
+    eager = summ
+    timing = "in-step kernel dispatch events (tt2_probe_arm), eager step"
+    if gsum:
+        summ = gsum
+        timing = ("external event-record nodes around each GEMM kernel node inside 5 graph-replayed steps "
+                  "(tt2_probe_arm under capture)")
     # dominant = the GEMM variant with the most device time
     key, (n, flops, secs, abytes) = max(summ.items(), key=lambda kv: kv[1][2])
-    # achieved uses the in-step kernel durations (libtt2's launch probe: start / stop events
-    # recorded by the kernel dispatch itself, inside an eager step, so cache state and
-    # neighbours are the step's own); a back-to-back replay of the same launches (warm
-    # caches) is reported beside it for reference only
-    replay = probe.replay_time(key)
+    n = round(n)
+    ek = eager.get(key)
+    # achieved uses the in-step kernel durations of graph-replayed steps (cache state and
+    # neighbours are the timed step's own); the eager-step figure and a back-to-back replay
+    # of the same launches (warm caches) are reported beside it for reference only
+    replay = probe.replay_time(key) if replay else None
     tot_t = sum(v[2] for v in summ.values())
     tot_f = sum(v[1] for v in summ.values())
     achieved = flops / secs / 1e12
@@ -284,9 +332,10 @@ def roofline(model, text, tl, mel, ml):
         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "traffic_source": tsrc,
         "mfma_busy_under_profiler": busy, "mfma_busy_source": bsrc,
         "algo_bytes_per_launch": round(abytes / n), "launches_per_step": n, "flops_per_launch": flops / n,
-        "avg_launch_us": round(secs / n * 1e6, 2), "timing": "in-step kernel dispatch events (tt2_probe_arm)",
-        "replay_avg_launch_us": round(replay / n * 1e6, 2),
-        "all_gemms": {"launches": sum(v[0] for v in summ.values()), "ms_per_step": round(tot_t * 1e3, 3),
+        "avg_launch_us": round(secs / n * 1e6, 2), "timing": timing,
+        "eager_avg_launch_us": round(ek[2] / ek[0] * 1e6, 2) if ek else None,
+        "replay_avg_launch_us": round(replay / ek[0] * 1e6, 2) if (replay is not None and ek) else None,
+        "all_gemms": {"launches": round(sum(v[0] for v in summ.values())), "ms_per_step": round(tot_t * 1e3, 3),
                       "tflops": round(tot_f / tot_t / 1e12, 1)},
     }
 
@@ -417,9 +466,13 @@ def main():
     ap.add_argument("--no-decode", action="store_true", help="skip the cfg3 / cfg5 decode measurements")
     ap.add_argument("--no-longform", action="store_true", help="skip the cfg5 long-form decode measurement")
     ap.add_argument("--no-ragged", action="store_true", help="skip the cfg2 ragged-length variant")
+    ap.add_argument("--profile-run", action="store_true", help="the run a rocprofv3 kernel trace is taken of: "
+                    "training step only (no ragged / decode / CPU legs, no back-to-back probe replays)")
     ap.add_argument("--force-dp", action="store_true", help="dev: run the DP path (bucketed RCCL all-reduce, "
                     "segmented graph) even at world size 1")
     args = ap.parse_args()
+    if args.profile_run:
+        args.no_ragged = args.no_decode = args.no_longform = args.no_cpu_baseline = True
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))    # before anything touches the GPU
 
@@ -506,7 +559,7 @@ def main():
         log("[bench] cfg2 ragged variant")
         rag = ragged_bench(run, rank, max(5, args.steps // 2))
         log(f"[bench] ragged {rag['value']:.0f} valid frames/s ({rag['ms_per_step']} ms/step)")
-    rl = roofline(model, text, tl, mel, ml) if rank == 0 else None
+    rl = roofline(model, text, tl, mel, ml, replay=not args.profile_run) if rank == 0 else None
     dec = None
     if rank == 0 and world == 1 and not args.no_decode:
         log("[bench] decode (cfg3)")

@@ -136,10 +136,13 @@ int tt2_gemm_plan(const tt2_gemm_args* a);
 int tt2_gemm_grouped(const tt2_gemm_args* probs, int32_t n, hipStream_t stream);
 
 /* Measurement probe (bench.py's live roofline): tt2_probe_arm() makes the next main GEMM
- * kernel (v7 / grouped v7 / LDS-DMA 128x128) launched on this thread record its own
- * start / stop timestamps (the kernel's execution, as rocprofv3 reports it) and returns the
- * slot; tt2_probe_ms(slot) waits for it and returns the duration in ms (-1 if the armed
- * launch did not happen); tt2_probe_reset() frees every slot. */
+ * kernel (v7 / grouped v7 / v8 / LDS-DMA 128x128) launched on this thread by the NEXT
+ * tt2_gemm / tt2_gemm_grouped call record start / stop timestamps and returns the slot.
+ * Eager: the kernel's own dispatch records them (its execution, as rocprofv3 reports it).
+ * Under stream capture: external event-record nodes bracket the kernel node, so each replay
+ * of the captured graph re-times it.  Any path of that call disarms the probe.
+ * tt2_probe_ms(slot) waits for the stop event and returns the duration in ms (-1 if no
+ * probe-capable kernel consumed the slot); tt2_probe_reset() frees every slot. */
 int tt2_probe_arm(void);
 float tt2_probe_ms(int slot);
 void tt2_probe_reset(void);

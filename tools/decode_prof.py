@@ -1,5 +1,5 @@
-"""Short AR decode run for kernel-trace profiling (dev tool, GPU): bench's cfg3
-decoder (B=32, 128 phonemes), 40 graph-replayed steps."""
+"""AR decode run for kernel-trace profiling (dev tool, GPU): bench's cfg3 decoder (B=32,
+128 phonemes), 800 graph-replayed steps (tools/summarize_decode_step.py)."""
 import os
 import sys
 
@@ -23,6 +23,6 @@ dec = Decoder(model.engine, bench.DEC_B, bench.TX, bench.DEC_T)
 dec.encode(text, tl)
 dec.capture(None)
 dec.reset()
-dec.decode_loop(40, stop_threshold=None)
+dec.decode_loop(bench.DEC_T, stop_threshold=None)
 torch.cuda.synchronize()
 print("ok")

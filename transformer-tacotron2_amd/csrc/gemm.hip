@@ -50,6 +50,29 @@ bool probe_take(hipEvent_t& e0, hipEvent_t& e1) {
   return true;
 }
 
+// The probe around one main-kernel launch.  Eager: the events ride in the kernel's own
+// dispatch (hipExtLaunchKernelGGL, ext()).  Under stream capture (a hipGraph of the step,
+// bench.py's roofline leg): external event-record nodes right before and after the kernel
+// node, so every replay of the graph re-times the launch inside the replayed step.
+struct ProbeScope {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipStream_t s;
+  bool capt = false;
+  explicit ProbeScope(hipStream_t st) : s(st) {
+    if (!probe_take(e0, e1)) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) {
+      capt = true;
+      (void)hipEventRecordWithFlags(e0, s, hipEventRecordExternal);
+    }
+  }
+  bool ext() const { return e0 && !capt; }
+  void done() {
+    if (capt) (void)hipEventRecordWithFlags(e1, s, hipEventRecordExternal);
+    capt = false;
+  }
+};
+
 
 constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
 
@@ -864,13 +887,14 @@ hipError_t launch2(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   }
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
   dim3 grid(ntm * ntn, splits);
-  hipEvent_t e0, e1;
-  if (probe_take(e0, e1))
-    hipExtLaunchKernelGGL((gemm2_kernel<AK, BKC>), grid, dim3(NT), 0, s, e0, e1, 0, A, B, E, M, N, K, k_split,
+  ProbeScope ps(s);
+  if (ps.ext())
+    hipExtLaunchKernelGGL((gemm2_kernel<AK, BKC>), grid, dim3(NT), 0, s, ps.e0, ps.e1, 0, A, B, E, M, N, K, k_split,
                      splits > 1 ? ws : nullptr, ntm, ntn);
   else
     hipLaunchKernelGGL((gemm2_kernel<AK, BKC>), grid, dim3(NT), 0, s, A, B, E, M, N, K, k_split,
                      splits > 1 ? ws : nullptr, ntm, ntn);
+  ps.done();
   if (splits > 1 && !E.main_only) {
     const int64_t total = (int64_t)M * N;
     int64_t nb = (total + 255) / 256;
@@ -1376,11 +1400,12 @@ hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   P.lds_epi = lds_epi && P.splits == 1 && E.c_dt == TT2_BF16 && E.vec && (N % 8) == 0;
   // the loader waves stage a bf16 residual / gate tile in LDS during the last K steps
   P.pre_x = !P.lds_epi ? 0 : (E.res && E.res_dt == TT2_BF16) ? 1 : (E.gate && E.gate_dt == TT2_BF16) ? 2 : 0;
-  hipEvent_t e0, e1;
-  if (probe_take(e0, e1))
-    hipExtLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, e0, e1, 0, P);
+  ProbeScope ps(s);
+  if (ps.ext())
+    hipExtLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, ps.e0, ps.e1, 0, P);
   else
     hipLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, P);
+  ps.done();
   if (P.splits > 1 && !E.main_only) {
     const int64_t total = (int64_t)M * N;
     int64_t nb = (total + 255) / 256;
@@ -1567,12 +1592,13 @@ __global__ __launch_bounds__(G8_NT, 2) void gemm8_kernel(OpDesc A, OpDesc B, Epi
 template <bool BKC>
 hipError_t launch8(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, hipStream_t s) {
   const int ntn = (N + 63) / 64, items = ((M + 63) / 64) * ntn;
-  hipEvent_t e0, e1;
-  if (probe_take(e0, e1))
-    hipExtLaunchKernelGGL((gemm8_kernel<BKC>), dim3(items), dim3(G8_NT), 0, s, e0, e1, 0, A, B, E, M, N, K, ntn,
+  ProbeScope ps(s);
+  if (ps.ext())
+    hipExtLaunchKernelGGL((gemm8_kernel<BKC>), dim3(items), dim3(G8_NT), 0, s, ps.e0, ps.e1, 0, A, B, E, M, N, K, ntn,
                           items);
   else
     hipLaunchKernelGGL((gemm8_kernel<BKC>), dim3(items), dim3(G8_NT), 0, s, A, B, E, M, N, K, ntn, items);
+  ps.done();
   return hipGetLastError();
 }
 
@@ -1832,9 +1858,9 @@ extern "C" int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int n, const tt2
     if (fin_blocks) hipLaunchKernelGGL(gemm_splitk_reduce_g, dim3(fin_blocks, 1), dim3(256), 0, stream, G);
     return tt2_check_launch(hipGetLastError(), "tt2_gemm_grouped");
   }
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (probe_take(e0, e1)) {
-#define TT2_G7G(A_, B_) hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_>), dim3(G.items), dim3(G7_NT), 0, stream, e0, e1, 0, G)
+  ProbeScope ps(stream);
+  if (ps.ext()) {
+#define TT2_G7G(A_, B_) hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_>), dim3(G.items), dim3(G7_NT), 0, stream, ps.e0, ps.e1, 0, G)
     if (!ta && !tb) TT2_G7G(true, true);
     else if (!ta && tb) TT2_G7G(true, false);
     else if (ta && !tb) TT2_G7G(false, true);
@@ -1844,6 +1870,7 @@ extern "C" int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int n, const tt2
   else if (!ta && tb) hipLaunchKernelGGL((gemm7g_kernel<true, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
   else if (ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<false, true>), dim3(G.items), dim3(G7_NT), 0, stream, G);
   else hipLaunchKernelGGL((gemm7g_kernel<false, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
+  ps.done();
   if (main_only) reduce_blocks = 0;
   G.fin_only = reduce_blocks == 0 && fin_blocks > 0;
   if (G.fin_only)
