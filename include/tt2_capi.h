@@ -201,6 +201,14 @@ typedef struct tt2_attn_decode_args {
   const void* wo;
   int64_t wo_ld;
   float* slab;
+  /* optional fused query projection (wq != NULL): q is then the projection INPUT x [batch][q_ld]
+   * (heads * head_dim wide) and the head's query is
+   * q[b, h, j] = sum_k x[b, k] * wq[(h * head_dim + j) * wq_ld + k] + bq[h * head_dim + j]
+   * (f32 accumulation, the query kept in f32): the decoder's cross-attention query GEMM
+   * rides in the attention launch */
+  const void* wq;
+  int64_t wq_ld;
+  const float* bq;
 } tt2_attn_decode_args;
 int tt2_attn_decode(const tt2_attn_decode_args* a, hipStream_t stream);
 /* cache[b*c_bstride + (*t_ptr)*c_ld + c] = src[b*src_ld + c], c < n */

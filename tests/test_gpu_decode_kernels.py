@@ -70,9 +70,9 @@ def test_skinny_pe_epilogue():
 
 
 def test_skinny_emit_advances_step():
-    """Three heads GEMMs with the emit epilogue: frames land at t = 0, 1, 2, the
+    """Three heads GEMMs with the emit epilogue (t_max = 2): frames land at t = 0, 1, the
     previous-frame buffer holds the last one, the seed advances, the arrival counter is
-    re-armed, and frames past t_max are not written."""
+    re-armed; the third call (t = t_max) writes no frame and the counter and seed saturate."""
     g = torch.Generator().manual_seed(5)
     m, n, k, nm, Tm = 32, 81, 512, 80, 2
     W = _bf((n, k), g, 0.1)
@@ -92,7 +92,7 @@ def test_skinny_emit_advances_step():
         ref = A.double() @ W.double().t() + bias.double()
         outs.append(ref)
         assert rel(heads[:, :n], ref) < 1e-5
-        assert t.item() == step + 1 and seed.item() == 8 + step and done.item() == 0
+        assert t.item() == min(step + 1, Tm) and seed.item() == 7 + min(step + 1, Tm) and done.item() == 0
     for s in range(Tm):
         assert rel(mel[:, s], outs[s][:, :nm]) < 1e-5
         assert rel(stop[:, s], outs[s][:, nm]) < 1e-5
@@ -193,6 +193,30 @@ def test_attn_decode_fused_oproj(dtype):
     assert rel(slab, ref) < 1e-2
     assert slab[:, 2].abs().sum().item() == 0
     assert rel(slab.sum(0), ref_o @ w.t()) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_attn_decode_fused_qproj(dtype):
+    """The cross-attention query projection fused into the decode attention launch (with the
+    output projection): q = x W_q^T + b_q per head in f32, then attention over ragged memory
+    keys, then the per-head output slabs (float64 reference)."""
+    g = torch.Generator().manual_seed(12)
+    B, H, d, Tx = 5, 8, 512, 128
+    mk = (lambda sh, sc=1.0: _bf(sh, g, sc)) if dtype == torch.bfloat16 else (lambda sh, sc=1.0: _h(sh, g, sc))
+    x, mem = mk((B, d)), mk((B, Tx, 2 * d))
+    wq, wo = mk((d, d), 1 / math.sqrt(d)), mk((d, d), 1 / math.sqrt(d))
+    bq = torch.randn(d, generator=g).cuda()
+    kl = torch.tensor([128, 1, 0, 77, 9], dtype=torch.int32, device="cuda")
+    slab = torch.full((H, B, d), float("nan"), device="cuda")
+    ops.attn_decode(x, mem, mem[:, :, d:], None, d, Tx * 2 * d, 2 * d, Tx * 2 * d, 2 * d, d, B, H, Tx, key_len=kl,
+                    scale=0.125, wo=wo, wo_ld=d, slab=slab, wq=wq, wq_ld=d, bq=bq)
+    q = x.double().cpu() @ wq.double().cpu().t() + bq.double().cpu()
+    ref_o = _attn_ref(q, mem[:, :, :d], mem[:, :, d:], kl.tolist(), 0.125)
+    w = wo.double().cpu()
+    ref = torch.stack([ref_o[:, h * 64:(h + 1) * 64] @ w[:, h * 64:(h + 1) * 64].t() for h in range(H)])
+    assert torch.isfinite(slab).all()
+    assert rel(slab, ref) < 1e-2
+    assert slab[:, 2].abs().sum().item() == 0   # no keys -> zero output, never NaN
 
 
 def _h(shape, gen, scale=1.0):

@@ -51,7 +51,36 @@ struct DecArgs {
   int tk, H, B;
   float scale;
   const void* wo; int64_t wo_ld; float* slab;   // fused output projection (wo != null)
+  const void* wq; int64_t wq_ld; const float* bq;   // fused query projection (wq != null; q = its input)
 };
+
+// q-prologue (wq != null): this head's 64 query values from the projection input row x[b]
+// (H*64 wide): wave w computes output rows 8w .. 8w+7 (NW = 8), eight lanes per row, each lane
+// 64 consecutive k (8 x 16-B chunks of W and of x, all issued before the first FMA); the eight
+// partials of a row meet by xor shuffles.  Result (f32, + bias) in sq[64].
+template <typename T, int NW>
+TT2_DEV void qproj(const DecArgs& a, int b, int h, float* sq) {
+  static_assert(NW == 8, "one wave per 8 query rows");
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 7, g = lane >> 3;
+  const int r = h * D + 8 * w + g;   // output feature
+  const T* x = reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld + 64 * c;
+  const T* wr = reinterpret_cast<const T*>(a.wq) + (int64_t)r * a.wq_ld + 64 * c;
+  float xv[8][8], wv[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    load8f(wr + 8 * i, wv[i]);
+    load8f(x + 8 * i, xv[i]);
+  }
+  float p = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p += xv[i][j] * wv[i][j];
+  p += __shfl_xor(p, 1, 64);
+  p += __shfl_xor(p, 2, 64);
+  p += __shfl_xor(p, 4, 64);
+  if (c == 0) sq[8 * w + g] = p + (a.bq ? a.bq[r] : 0.f);
+}
 
 // slab[(h*B + b)*H*64 + n] = sum_j o[j] * Wo[n][h*64 + j] for the H*64 output columns.
 // Eight lanes cover one 128-B row of Wo's head slice (lane & 7 = 16-B chunk), so a wave
@@ -84,7 +113,7 @@ TT2_DEV void oproj_slab(const DecArgs& a, int b, int h, const float (&o)[8], flo
 template <typename T, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
   constexpr int U = 4;   // 8-key groups per wave per iteration: 2*U 16-B loads in flight per lane
-  __shared__ float sm[NW], sl[NW], so[NW][D], sfin[D], sres[512];
+  __shared__ float sm[NW], sl[NW], so[NW][D], sfin[D], sres[512], sq[D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
   const int dc = lane & 7, kg = lane >> 3;   // 8-dim chunk, key slot within an 8-key group
@@ -96,8 +125,6 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
       for (int n = threadIdx.x; n < a.H * D; n += NW * 64) a.slab[((int64_t)h * a.B + b) * a.H * D + n] = 0.f;
     return;
   }
-  float qv[8];
-  load8f(reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld + h * D + dc * 8, qv);
   int nk = a.tk;
   if (a.t_ptr) nk = min(nk, *a.t_ptr + 1);
   if (a.key_len) nk = min(nk, a.key_len[b]);
@@ -108,16 +135,30 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
   const int k0 = w * per, k1 = min(nk, k0 + per);
   const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)b * a.k_bstride + h * D + dc * 8;
   const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)b * a.v_bstride + h * D + dc * 8;
-  float m = -INFINITY, l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int kb = k0; kb < k1; kb += 8 * U) {
-    float kv[U][8], vv[U][8];
-    // every load of the iteration first (clamped to the last valid key: branch-free)
+  float kv[U][8], vv[U][8];
+  // every load of an iteration first (clamped to the last valid key: branch-free)
+  auto load_keys = [&](int kb) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int key = min(kb + 8 * u + kg, k1 - 1);
       load8f(K + (int64_t)key * a.k_ld, kv[u]);
       load8f(V + (int64_t)key * a.v_ld, vv[u]);
     }
+  };
+  // the first iteration's keys do not depend on the query: in flight during its projection
+  if (k0 < k1) load_keys(k0);
+  float qv[8];
+  if (a.wq) {
+    qproj<T, NW>(a, b, h, sq);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qv[j] = sq[dc * 8 + j];
+  } else {
+    load8f(reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld + h * D + dc * 8, qv);
+  }
+  float m = -INFINITY, l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int kb = k0; kb < k1; kb += 8 * U) {
+    if (kb != k0) load_keys(kb);
     float s[U];
     float mx = -INFINITY;
 #pragma unroll
@@ -242,6 +283,10 @@ extern "C" int tt2_attn_decode(const tt2_attn_decode_args* p, hipStream_t s) {
   a.step = p->step ? p->step : p->t_ptr;
   a.B = p->batch;
   a.wo = p->wo; a.wo_ld = p->wo_ld; a.slab = p->slab;
+  a.wq = p->wq; a.wq_ld = p->wq_ld; a.bq = p->bq;
+  if (a.wq && ((p->wq_ld * esz) % 16 || p->heads * D != 512))
+    return tt2_set_error(TT2_E_INVALID, "tt2_attn_decode: the fused query projection needs a 16-B wq_ld and "
+                                       "heads * head_dim == 512");
   if (a.wo && (!a.slab || (p->wo_ld * esz) % 16 || p->heads * D > 512))
     return tt2_set_error(TT2_E_INVALID, "tt2_attn_decode: the fused projection needs slab, a 16-B wo_ld and "
                                        "heads * head_dim <= 512");

@@ -6,9 +6,10 @@
 // Two schedules over the same kernels:
 //  * split (bf16 / f16, batch <= 64, the default): the skinny weight-streaming GEMM
 //    carries the KV-cache scatter (QKV projection), the scaled PE (pre-net projection)
-//    and the frame emit (heads); the K = 512 / 2048 output projections o, co, ffn2 run
-//    split-K into raw f32 slabs that tt2_ln_combine folds with bias + residual into the
-//    sublayer's LayerNorm.  11 launches per layer + 4.
+//    and the frame emit (heads); the attention launches carry the output projections o / co
+//    (one f32 slab per head) and the cross-attention's query projection cq; ffn2 runs split-K
+//    into raw f32 slabs; tt2_ln_combine folds each sublayer's slabs with bias + residual
+//    into its LayerNorm.  8 launches per layer + 4.
 //  * plain (f32 parity mode, or batch > 64): one launch per op (GEMM, KV append,
 //    LayerNorm, PE, emit), no slabs.
 // The step reads the frame index from the device counter d->step and bumps it in the
@@ -165,7 +166,8 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
   }
 
   auto attn = [&](const void* q, int64_t q_ld, const void* k, const void* v, int64_t bstride, int64_t ld, int tk,
-                  const int32_t* key_len, const int32_t* t_ptr, void* out, const void* wo) {
+                  const int32_t* key_len, const int32_t* t_ptr, void* out, const void* wo,
+                  const void* wq = nullptr, const float* bq = nullptr) {
     tt2_attn_decode_args a;
     std::memset(&a, 0, sizeof(a));
     a.q = q; a.k = k; a.v = v; a.out = out;
@@ -175,6 +177,9 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
     a.stop_len = d->stop_len; a.step = d->step;
     if (wo) {   // split schedule: the output projection rides in the attention launch (one slab per head)
       a.out = nullptr; a.wo = wo; a.wo_ld = D; a.slab = b.slab;
+    }
+    if (wq) {   // ... and the query projection (q is then its input row)
+      a.wq = wq; a.wq_ld = D; a.bq = bq;
     }
     return tt2_attn_decode(&a, s);
   };
@@ -220,14 +225,16 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
       TT2_TRY(tt2_gemm(&g, s));
       TT2_TRY(layernorm(x, b.o, L.ln1_g, L.ln1_b, b.h1));
     }
-    // cross-attention over the cached encoder memory K/V
-    {
+    // cross-attention over the cached encoder memory K/V; in the fused schedule its query
+    // projection (cq) runs inside the attention launch
+    if (!fuse_o) {
       tt2_gemm_args g = lin(b.h1, L.cq_w, b.cq, B, D, D, L.cq_b, dt, dt);
       TT2_TRY(tt2_gemm(&g, s));
     }
     const char* mk = mkv + (size_t)2 * D * l * e;
-    TT2_TRY(attn(b.cq, D, mk, mk + D * e, (int64_t)d->text_len * kvld, kvld, d->text_len, d->text_lens, nullptr,
-                 b.catt, fuse_o ? L.co_w : nullptr));
+    TT2_TRY(attn(fuse_o ? b.h1 : b.cq, D, mk, mk + D * e, (int64_t)d->text_len * kvld, kvld, d->text_len,
+                 d->text_lens, nullptr, b.catt, fuse_o ? L.co_w : nullptr, fuse_o ? L.cq_w : nullptr,
+                 fuse_o ? L.cq_b : nullptr));
     if (split) {
       if (!fuse_o) TT2_TRY(slabs(b.catt, L.co_w, D, D, SPLIT_O));
       TT2_TRY(tt2_ln_combine(b.h1, b.slab, fuse_o ? H : SPLIT_O, L.co_b, L.ln2_g, L.ln2_b, b.h2, B, D, d->ln_eps,

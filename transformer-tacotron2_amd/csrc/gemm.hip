@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "tt2_common.h"
@@ -40,14 +41,35 @@ struct ProbeSlot { hipEvent_t start, stop; bool used; };
 thread_local std::vector<ProbeSlot> g_probe;
 thread_local int g_probe_armed = -1;
 
-bool probe_take(hipEvent_t& e0, hipEvent_t& e1) {
-  if (g_probe_armed < 0) return false;
-  ProbeSlot& p = g_probe[g_probe_armed];
+int probe_take(hipEvent_t& e0, hipEvent_t& e1) {
+  if (g_probe_armed < 0) return -1;
+  const int slot = g_probe_armed;
+  ProbeSlot& p = g_probe[slot];
   e0 = p.start;
   e1 = p.stop;
   p.used = true;
   g_probe_armed = -1;
-  return true;
+  return slot;
+}
+
+// An event-record node appended to a capturing stream's graph: the runtime's own
+// hipEventRecordWithFlags(External) where it accepts one under capture, else the node is added
+// by hand (hipGraphAddEventRecordNode after the stream's current capture dependencies).
+hipError_t capture_event_node(hipStream_t s, hipEvent_t ev) {
+  hipError_t e = hipEventRecordWithFlags(ev, s, hipEventRecordExternal);
+  if (e == hipSuccess) return e;
+  (void)hipGetLastError();
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  e = hipStreamGetCaptureInfo_v2(s, &st, &id, &g, &deps, &nd);
+  if (e != hipSuccess || st != hipStreamCaptureStatusActive || !g) return e != hipSuccess ? e : hipErrorInvalidValue;
+  hipGraphNode_t node = nullptr;
+  e = hipGraphAddEventRecordNode(&node, g, deps, nd, ev);
+  if (e != hipSuccess) return e;
+  return hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies);
 }
 
 // The probe around one main-kernel launch.  Eager: the events ride in the kernel's own
@@ -59,16 +81,40 @@ struct ProbeScope {
   hipStream_t s;
   bool capt = false;
   explicit ProbeScope(hipStream_t st) : s(st) {
-    if (!probe_take(e0, e1)) return;
+    const int slot = probe_take(e0, e1);
+    if (slot < 0) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) {
-      capt = true;
-      (void)hipEventRecordWithFlags(e0, s, hipEventRecordExternal);
+      // event nodes take plain timing events (the slot's eager events skip the system fence)
+      ProbeSlot& p = g_probe[slot];
+      hipEvent_t a = nullptr, b = nullptr;
+      hipError_t e1c = hipEventCreate(&a), e2c = hipSuccess, erc = hipSuccess;
+      if (e1c == hipSuccess) e2c = hipEventCreate(&b);
+      if (e1c == hipSuccess && e2c == hipSuccess) erc = capture_event_node(s, a);
+      if (e1c == hipSuccess && e2c == hipSuccess && erc == hipSuccess) {
+        (void)hipEventDestroy(p.start);
+        (void)hipEventDestroy(p.stop);
+        p.start = e0 = a;
+        p.stop = e1 = b;
+        capt = true;
+      } else {   // this runtime cannot record the probe in a graph: the launch goes untimed
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+        p.used = false;
+        e0 = e1 = nullptr;
+        std::string m = std::string("launch probe under capture: create ") + hipGetErrorName(e1c) + " / " +
+                        hipGetErrorName(e2c) + ", record " + hipGetErrorName(erc);
+        tt2_set_error(TT2_E_HIP, m.c_str());
+      }
+      (void)hipGetLastError();   // a refused record must not fail the launch check that follows
     }
   }
   bool ext() const { return e0 && !capt; }
   void done() {
-    if (capt) (void)hipEventRecordWithFlags(e1, s, hipEventRecordExternal);
+    if (capt) {
+      (void)capture_event_node(s, e1);
+      (void)hipGetLastError();
+    }
     capt = false;
   }
 };

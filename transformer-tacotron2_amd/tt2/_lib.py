@@ -252,6 +252,7 @@ class AttnDecodeArgs(C.Structure):
         ("scale", f32),
         ("stop_len", vp), ("step", vp),
         ("wo", vp), ("wo_ld", i64), ("slab", vp),
+        ("wq", vp), ("wq_ld", i64), ("bq", vp),
     ]
 
 

@@ -199,7 +199,9 @@ class LaunchProbe:
         for key, flops, slot, _, ab, _ in self.rec:
             ms = L.tt2_probe_ms(slot)
             if ms < 0:
-                raise _lib.TT2Error(f"launch probe {slot} ({key}) recorded no kernel")
+                msg = L.tt2_last_error()
+                raise _lib.TT2Error(f"launch probe {slot} ({key}) recorded no kernel"
+                                    f"{' (' + msg.decode() + ')' if msg else ''}")
             d = out.setdefault(key, [0, 0.0, 0.0, 0.0])
             d[0] += 1
             d[1] += flops
@@ -479,10 +481,14 @@ def step_bump(step, seed=None):
 
 
 def attn_decode(q, k, v, out, q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld, batch, heads, tk, key_len=None,
-                t_ptr=None, scale=0.125, stop_len=None, step=None, wo=None, wo_ld=0, slab=None):
+                t_ptr=None, scale=0.125, stop_len=None, step=None, wo=None, wo_ld=0, slab=None, wq=None, wq_ld=0,
+                bq=None):
     """One query row per batch element over a key cache (see tt2_attn_decode_args).
-    wo / slab: the fused output projection, slab[h, b, :] = o[b, h] @ wo[:, h*64:(h+1)*64]^T (f32)."""
+    wo / slab: the fused output projection, slab[h, b, :] = o[b, h] @ wo[:, h*64:(h+1)*64]^T (f32).
+    wq / bq: the fused query projection, q is then the projection input x and the head's
+    query is x[b] @ wq[h*64:(h+1)*64]^T + bq[h*64:(h+1)*64]."""
     a = _lib.AttnDecodeArgs()
+    a.wq, a.wq_ld, a.bq = ptr(wq), wq_ld, ptr(bq)
     a.stop_len, a.step = ptr(stop_len), ptr(step)
     a.q, a.k, a.v, a.out = q.data_ptr(), k.data_ptr(), v.data_ptr(), ptr(out)
     a.wo, a.wo_ld, a.slab = ptr(wo), wo_ld, ptr(slab)
