@@ -27,6 +27,17 @@ extern "C" int tt2_check_launch(hipError_t err, const char* what) {
   return TT2_E_LAUNCH;
 }
 
+int tt2_cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    cache[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }
+  return cache[dev];
+}
+
 extern "C" int tt2_init(int device) {
   std::call_once(g_once, [&] {
     hipDeviceProp_t prop;

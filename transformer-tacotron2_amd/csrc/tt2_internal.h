@@ -6,3 +6,5 @@ extern "C" {
 int tt2_set_error(int code, const char* msg);
 int tt2_check_launch(hipError_t err, const char* what);
 }
+// compute units of the current device (cached per device; 256 on an MI355X)
+int tt2_cu_count();
