@@ -234,8 +234,6 @@ def gemm_kernel_name(plan: int, ta: int, tb: int) -> str:
         return f"gemm7_kernel<{ak}, {bk}>"
     if plan == 15:
         return f"gemm8_kernel<{bk}>"
-    if plan == 16:
-        return f"gemm9_kernel<{bk}>"
     if plan == 1:
         return "gemm_kernel"
     return f"gemm plan {plan}"

@@ -70,8 +70,7 @@ typedef struct tt2_gemm_args {
   int32_t kernel_variant;  /* 0 auto, 1 register-staged (any shape), 2 LDS-DMA 128x128 (bf16, 8-aligned inner
                               dims), 13 / 14 warp-specialised 256x128 (same, conv C, T >= 64; the auto choice
                               when eligible) with its register / LDS-image epilogue (auto: LDS image),
-                              15 64x64 (K-contiguous A; auto for <= 64 v7 tiles), 16 256x256 (K-contiguous A,
-                              no split-K; auto for wide forward products of >= 256 tiles) */
+                              15 64x64 (K-contiguous A; auto for <= 64 v7 tiles) */
   /* optional fused row sums of op(A) over k: a_ksum[m] = a_ksum_beta * a_ksum[m] + sum_k A(m, k)
    * (f32).  With A = dY^T of a weight-gradient GEMM this is the bias gradient, taken from the
    * A tiles already staged in LDS.  Requires bf16, trans_a, no conv on A. */
@@ -127,7 +126,7 @@ size_t tt2_gemm_workspace_size(const tt2_gemm_args* a);
 int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream);
 /* Kernel tt2_gemm would launch for these args (no device work): 1 register-staged
  * 128x128 (any dtype), 2 LDS-DMA 128x128 (bf16), 3 skinny decode (m <= 64),
- * 13 warp-specialised 256x128, 15 64x64, 16 256x256; -1 invalid. */
+ * 13 warp-specialised 256x128, 15 64x64; -1 invalid. */
 int tt2_gemm_plan(const tt2_gemm_args* a);
 
 /* Grouped GEMM: up to 8 independent problems in ONE launch of the v7 kernel (every

@@ -1648,172 +1648,6 @@ hipError_t launch8(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   return hipGetLastError();
 }
 
-// =====================================================================================
-// v9 (bf16, A K-contiguous): 256 x 256 tile for the multi-round products (N >= 1024 at
-// M = 12800: the decoder FFN1 forward and FFN2 dgrad, 800 v7 tiles = 3.1 rounds).  v7's
-// K loop is bound by how fast 4 loader waves move 48 KB per 64-deep step into LDS (and by
-// the LDS read traffic of 64 x 64 wave tiles); a 256 x 256 tile stages 64 KB per step for
-// twice the MFMA work.  512 threads = 8 waves (2 M x 4 N), each a 128 x 64 block (8 x 4
-// accumulators of v_mfma_f32_16x16x32_bf16, 128 VGPRs), and EVERY wave both copies and
-// multiplies: per K step each wave issues its 8 of the 64 LDS-DMA copies of the NEXT step
-// (split 4 + 4 ahead of the two 32-deep halves, so the copy issue of one wave overlaps the
-// other wave's MFMAs on its SIMD) into the other half of a 2-stage ring (128 KB), then
-// waits for them (counted, the only vmcnt in the loop) and passes one s_barrier.  Images,
-// swizzles and fragment reads are v7's (256 rows = two stacked 128-column sub-images for an
-// N-contiguous B).  Epilogue from registers (D = B A^T + permlane16 swap: 8 consecutive
-// columns per lane), then the C tile leaves through the (now free) ring as an LDS image of
-// whole 256-B row segments.
-// =====================================================================================
-constexpr int G9_NT = 512;
-constexpr int G9_OP = 256 * 128;          // bytes per operand tile: 256 rows x 64 k x 2 B
-constexpr int G9_STAGE = 2 * G9_OP;       // 64 KB
-constexpr int G9_SMEM = 2 * G9_STAGE;     // 128 KB
-
-// C image for one 128-column half of the tile: [256 rows][16 chunks], chunk c of row r at
-// c ^ (r & 15) (as v7's image)
-TT2_DEV int g9_img(int half, int r, int c) { return half * 65536 + r * 256 + ((c ^ (r & 15)) << 4); }
-
-template <bool BKC>
-__global__ __launch_bounds__(G9_NT, 1) void gemm9_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
-                                                         int ntn, int items) {
-  __shared__ __attribute__((aligned(1024))) char smem[G9_SMEM];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tile = xcd_item(blockIdx.x, items);
-  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
-  const int nkt = (K + 63) / 64;
-  const bool tail = (K & 63) != 0;
-  // this wave's copies: 4 of A's 32 (rows 32 w .. 32 w + 31) and 4 of B's 32
-  G7Lane<4> la, lb;
-  const bool cfa = g7_conv_fast(A) && !tail;
-  g7_lane_init<true>(la, A, m0, 0, lane, wave);
-  g7_lane_init<BKC>(lb, B, n0, 0, lane, wave);
-  auto issue_a = [&](int t) {
-    g7_issue<true>(A, la, smem + (t & 1) * G9_STAGE, 64 * t, K, lane, wave, tail && t == nkt - 1, cfa);
-  };
-  auto issue_b = [&](int t) {
-    g7_issue<BKC>(B, lb, smem + (t & 1) * G9_STAGE + G9_OP, 64 * t, K, lane, wave, tail && t == nkt - 1, false);
-  };
-  const int wm = wave >> 2, wn = wave & 3, q = lane >> 4;
-  // bias chunks of this lane's columns, loaded before the K loop
-  const bool pre_b = E.bias && E.vec;
-  f32x4 pbias[2][2];
-#pragma unroll
-  for (int pr = 0; pr < 2; ++pr) {
-    const int n = n0 + wn * 64 + 16 * (2 * pr + (q & 1)) + 8 * (q >> 1);
-    pbias[pr][0] = pbias[pr][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (pre_b && n + 8 <= N) {
-      pbias[pr][0] = *reinterpret_cast<const f32x4*>(E.bias + n);
-      pbias[pr][1] = *reinterpret_cast<const f32x4*>(E.bias + n + 4);
-    }
-  }
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  issue_a(0);
-  issue_b(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int t = 0; t < nkt; ++t) {
-    const char* sa = smem + (t & 1) * G9_STAGE;
-    const char* sb = sa + G9_OP;
-    const bool more = t + 1 < nkt;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      // the next step's copies go into the other stage (its reads ended before the last barrier)
-      if (more) {
-        if (kk == 0) issue_a(t + 1);
-        else issue_b(t + 1);
-      }
-      Frag8<bf16> fa[8], fb[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) g7_frag<BKC>(fb[j], sb, wn * 64 + 16 * j, kk, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) g7_frag<true>(fa[i], sa, wm * 128 + 16 * i, kk, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) mma16(fb[j], fa[i], acc[i][j]);   // D[n][m]
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this stage's reads retired (WAR)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's copies of step t + 1 landed
-    __builtin_amdgcn_s_barrier();
-  }
-  // epilogue: the ring is free; rows r of the tile, 8 consecutive columns per lane and pr
-  const uint32_t seed = E.drop.thr ? *E.drop.seed : 0u;
-  const bool img = E.c_dt == TT2_BF16 && E.vec;
-  // one 16-row block per call, with a compile-time accumulator index (a loop over i that the
-  // compiler leaves rolled would index acc at run time and demote it to scratch)
-  auto epi_rows = [&](const f32x4 (&ai)[4], int i) {
-    const int r = wm * 128 + 16 * i + (lane & 15), m = m0 + r;
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {
-      float v[8];
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(ai[2 * pr][rr]),
-                                                         __float_as_uint(ai[2 * pr + 1][rr]), false, false);
-        v[rr] = __uint_as_float(sw[0]);
-        v[4 + rr] = __uint_as_float(sw[1]);
-      }
-      const int cl = wn * 64 + 16 * (2 * pr + (q & 1)) + 8 * (q >> 1), n = n0 + cl;
-      if (m >= M || n >= N) continue;
-      const bool pb = pre_b && n + 8 <= N;
-      if (pb) {
-        const f32x4 b0 = pbias[pr][0], b1 = pbias[pr][1];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[j] = v[j] * E.alpha + b0[j];
-          v[4 + j] = v[4 + j] * E.alpha + b1[j];
-        }
-      }
-      if (!img) {
-        epi_store8(E, seed, m, n, N, v, pb);
-        continue;
-      }
-      float o[8];
-      epi_calc8(E, seed, m, n, v, pb, o);
-      bf16x8 x;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = (bf16)o[j];
-      *reinterpret_cast<bf16x8*>(smem + g9_img(cl >> 7, r, (cl >> 3) & 15)) = x;
-    }
-  };
-  epi_rows(acc[0], 0);
-  epi_rows(acc[1], 1);
-  epi_rows(acc[2], 2);
-  epi_rows(acc[3], 3);
-  epi_rows(acc[4], 4);
-  epi_rows(acc[5], 5);
-  epi_rows(acc[6], 6);
-  epi_rows(acc[7], 7);
-  if (!img) return;
-  __syncthreads();
-  // whole 256-B row segments (16 lanes per row and half), nontemporal as v7's C
-  bf16* C = reinterpret_cast<bf16*>(E.c);
-  for (int id = tid; id < 256 * 32; id += G9_NT) {
-    const int half = id >> 12, r = (id >> 4) & 255, c = id & 15;
-    const int mm = m0 + r, nn = n0 + half * 128 + 8 * c;
-    if (mm < M && nn < N)
-      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(smem + g9_img(half, r, c)),
-                                  reinterpret_cast<u32x4*>(C + (int64_t)mm * E.ldc + nn));
-  }
-}
-
-template <bool BKC>
-hipError_t launch9(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, hipStream_t s) {
-  const int ntn = (N + 255) / 256, items = ((M + 255) / 256) * ntn;
-  ProbeScope ps(s);
-  if (ps.ext())
-    hipExtLaunchKernelGGL((gemm9_kernel<BKC>), dim3(items), dim3(G9_NT), 0, s, ps.e0, ps.e1, 0, A, B, E, M, N, K, ntn,
-                          items);
-  else
-    hipLaunchKernelGGL((gemm9_kernel<BKC>), dim3(items), dim3(G9_NT), 0, s, A, B, E, M, N, K, ntn, items);
-  ps.done();
-  return hipGetLastError();
-}
-
 
 }  // namespace
 
@@ -1828,7 +1662,7 @@ static bool g7_lds_epi(int variant) { return variant != 13; }
 
 // Kernel selection (also exported as tt2_gemm_plan): 1 v1 register-staged, 2 v2
 // LDS-DMA 128^2, 3 skinny (M <= 64), 13 v7 warp-specialised 256x128 (auto; variant 14
-// forces its LDS-image epilogue, 13 its register epilogue), 15 v8 64x64, 16 v9 256x256.  Returns -1 (error set) for an unsupported fusion request.
+// forces its LDS-image epilogue, 13 its register epilogue), 15 v8 64x64.  Returns -1 (error set) for an unsupported fusion request.
 static int gemm_plan(const tt2_gemm_args* a) {
   const int var = a->kernel_variant;
   const int64_t a_inner = a->trans_a ? a->m : a->k, b_inner = a->trans_b ? a->n : a->k;
@@ -1882,14 +1716,6 @@ static int gemm_plan(const tt2_gemm_args* a) {
   // the post-net's 80-channel conv): 1.4-1.6x v7 there, slower once v7 has >= 96 tiles
   const int64_t tiles7 = (int64_t)((a->m + 255) / 256) * ((a->n + 127) / 128);
   if (v8ok && a->m >= 64 && (var == 15 || (var == 0 && tiles7 <= 64))) return 15;
-  // v9 (256 x 256 tiles, every wave loads and multiplies): K-contiguous A, no k-sums, no
-  // conv B, no split-K; forced by variant 16
-  const bool v9ok = v7ok && !a->trans_a && !a->a_ksum && a->b_conv_t == 0 && a->splits <= 1;
-  // auto: the wide forward products of >= 256 v9 tiles (the decoder FFN1: 60.6 vs 64.5 us at
-  // 12800 x 2048 x 512); v7 stays faster for N-contiguous B, N <= 1536 and fewer tiles
-  // (tools/v9_ab.py)
-  const int64_t tiles9 = (int64_t)((a->m + 255) / 256) * ((a->n + 255) / 256);
-  if (v9ok && (var == 16 || (var == 0 && !a->trans_b && a->n >= 2048 && tiles9 >= 256))) return 16;
   if ((var == 13 || var == 14 || var == 0) && v7ok) return 13;
   return 2;
 }
@@ -2003,11 +1829,6 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
 #undef TT2_SK_M
 #undef TT2_SK
     return tt2_check_launch(hipGetLastError(), "tt2_gemm(skinny)");
-  }
-  if (plan == 16) {
-    if (!a->trans_b) err = launch9<true>(A, B, ep, a->m, a->n, a->k, stream);
-    else err = launch9<false>(A, B, ep, a->m, a->n, a->k, stream);
-    return tt2_check_launch(err, "tt2_gemm(v9)");
   }
   if (plan == 15) {
     if (!a->trans_b) err = launch8<true>(A, B, ep, a->m, a->n, a->k, stream);
