@@ -136,8 +136,9 @@ struct EpiParams {
   int main_only;                  // split-K: skip the reduce launch (measurement hook)
 };
 
-// fixed-order split-K slab reduce + epilogue (defined after epi_store8)
+// fixed-order split-K slab reduce + epilogue (defined after epi_store8) and its grid size
 __global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int M, int N);
+int splitk_blocks(int M, int N, const EpiParams& E);
 
 TT2_DEV float ld_any(const void* p, int64_t i, int dt) {
   if (dt == TT2_F16) return (float)reinterpret_cast<const f16*>(p)[i];
@@ -320,11 +321,8 @@ hipError_t launch_t(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M,
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM, splits);
   hipLaunchKernelGGL((gemm_kernel<T, AK, BKC>), grid, dim3(NT), 0, s, A, B, E, M, N, K, k_split,
                      splits > 1 ? ws : nullptr);
-  if (splits > 1 && !E.main_only) {
-    const int64_t total = (int64_t)M * N;
-    int64_t nb = (total + 255) / 256; int blocks = (int)(nb < 4096 ? nb : 4096);
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, splits, E, M, N);
-  }
+  if (splits > 1 && !E.main_only)
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(splitk_blocks(M, N, E)), dim3(256), 0, s, ws, splits, E, M, N);
   return hipGetLastError();
 }
 
@@ -567,6 +565,16 @@ TT2_DEV void splitk_reduce_body(const float* ws, int splits, const EpiParams& E,
 
 __global__ void gemm_splitk_reduce(const float* ws, int splits, EpiParams E, int M, int N) {
   splitk_reduce_body(ws, splits, E, M, N, blockIdx.x, gridDim.x);
+}
+
+// reduce grid: one 256-thread block per 256 work items of splitk_reduce_body's path (8, 4 or 1
+// output elements per thread); a grid of one block per 256 ELEMENTS left 7 of 8 blocks of the
+// 8-wide path with nothing to do (dispatching them cost more than the reduce)
+int splitk_blocks(int M, int N, const EpiParams& E) {
+  const int64_t per = ((N & 7) == 0 && E.vec) ? 8 : ((N & 3) == 0 ? 4 : 1);
+  const int64_t items = std::max<int64_t>(((int64_t)M * N + per - 1) / per, M);
+  const int64_t nb = (items + 255) / 256;
+  return (int)(nb < 4096 ? nb : 4096);
 }
 
 template <bool AK, bool BKC>
@@ -941,12 +949,8 @@ hipError_t launch2(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
     hipLaunchKernelGGL((gemm2_kernel<AK, BKC>), grid, dim3(NT), 0, s, A, B, E, M, N, K, k_split,
                      splits > 1 ? ws : nullptr, ntm, ntn);
   ps.done();
-  if (splits > 1 && !E.main_only) {
-    const int64_t total = (int64_t)M * N;
-    int64_t nb = (total + 255) / 256;
-    int blocks = (int)(nb < 4096 ? nb : 4096);
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, splits, E, M, N);
-  }
+  if (splits > 1 && !E.main_only)
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(splitk_blocks(M, N, E)), dim3(256), 0, s, ws, splits, E, M, N);
   return hipGetLastError();
 }
 
@@ -1452,12 +1456,8 @@ hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   else
     hipLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, P);
   ps.done();
-  if (P.splits > 1 && !E.main_only) {
-    const int64_t total = (int64_t)M * N;
-    int64_t nb = (total + 255) / 256;
-    int blocks = (int)(nb < 4096 ? nb : 4096);
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, ws, P.splits, E, M, N);
-  }
+  if (P.splits > 1 && !E.main_only)
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(splitk_blocks(M, N, E)), dim3(256), 0, s, ws, P.splits, E, M, N);
   return hipGetLastError();
 }
 
@@ -1895,8 +1895,7 @@ extern "C" int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int n, const tt2
     G.p[G.np++] = P;
     main_only &= a->main_only;
     if (P.splits > 1) {
-      const int64_t nb = ((int64_t)a->m * a->n + 255) / 256;
-      reduce_blocks = (int)std::max<int64_t>(reduce_blocks, nb < 4096 ? nb : 4096);
+      reduce_blocks = std::max(reduce_blocks, splitk_blocks(a->m, a->n, ep));
     }
   }
   const int fin_blocks = G.fin.nb ? (3 * G.fin.C + G7_FIN_WAVES - 1) / G7_FIN_WAVES : 0;
