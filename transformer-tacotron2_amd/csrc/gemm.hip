@@ -1101,6 +1101,7 @@ struct G7Prob {
   float* ws;   // split-K slabs [splits][M][N] (+ [splits][M] k-sums); used when splits > 1
   int lds_epi; // C leaves through an LDS image in whole 256-B row segments (bf16 C, no split)
   int pre_x;     // the loader waves stage the bf16 residual (1) or gate (2) tile in LDS (lds_epi only)
+  int epi_fast;  // straight-line image epilogue for this option set (g7_epi_fast), -1: general path
 };
 constexpr int G7_MAXP = 8;
 // A deferred LayerNorm backward's column-sum finalize (tt2_ln_args with defer_finalize) that
@@ -1153,6 +1154,57 @@ TT2_DEV void g7_issue_x(const G7Prob& P, const void* x, int64_t ldx, char* smem,
     const int m = min(m0 + r, P.M - 1), c = (lane & 15) ^ (r & 15);
     __builtin_amdgcn_global_load_lds((gvoid_t*)(base + ((int64_t)m * ldx + n0 + 8 * c) * 2),
                                      (lvoid_t*)(smem + g7_img_row(nkt, r0 + inst * 4)), 16, 0, 0);
+  }
+}
+
+// Straight-line LDS-image epilogue of a FULL tile for one option set, fixed at compile time:
+// the general path (epi_calc8 over run-time options, with per-lane bounds tests) compiles to
+// a long chain of branches that took ~5k cycles of the MFMA waves per tile (tools/gemm_stamps.hip),
+// as long as three K steps.  Same operations, same order (alpha, bias, residual, ReLU, gate,
+// dropout), so the results are bit-identical to the general path.
+template <bool BIAS, bool RELU, bool DROP, int PX>
+TT2_DEV void g7_epi_fast(const EpiParams& E, const f32x4 (&acc)[4][4], const f32x4 (&pbias)[2][2], char* smem,
+                         int nkt, int m0, int n0, int wm, int wn, int lane, uint32_t seed) {
+  const int q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = wm * 64 + 16 * i + (lane & 15), m = m0 + r;
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      float v[8];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * pr][rr]),
+                                                         __float_as_uint(acc[i][2 * pr + 1][rr]), false, false);
+        v[rr] = __uint_as_float(sw[0]);
+        v[4 + rr] = __uint_as_float(sw[1]);
+      }
+      const int cl = wn * 64 + 16 * (2 * pr + (q & 1)) + 8 * (q >> 1), n = n0 + cl;
+      char* cp = smem + g7_img_row(nkt, r) + (((cl >> 3) ^ (r & 15)) << 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = BIAS ? v[j] * E.alpha + pbias[pr][0][j] : v[j] * E.alpha;
+        v[4 + j] = BIAS ? v[4 + j] * E.alpha + pbias[pr][1][j] : v[4 + j] * E.alpha;
+      }
+      if (PX) {
+        float t[8];
+        unpack_lds8(cp, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (PX == 1) v[j] += t[j];
+          else v[j] = t[j] != 0.f ? v[j] * E.gate_scale : 0.f;
+        }
+      }
+      if (RELU) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+      }
+      if (DROP) drop_apply8(E.drop, seed, (uint32_t)((int64_t)m * E.n_log + n), v);
+      bf16x8 x;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = (bf16)v[j];
+      *reinterpret_cast<bf16x8*>(cp) = x;
+    }
   }
 }
 
@@ -1298,6 +1350,24 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
     // epilogue values -> bf16 C image [256 rows][16 chunks of 16 B] (chunk c of row r at
     // c ^ (r & 15): the 16 rows of one store instruction hit 16 different bank groups),
     // then all 12 waves store whole 256-B row segments
+    const int fast = (m0 + 256 <= M && n0 + 128 <= N && (P.pre_x == 0 || px)) ? P.epi_fast : -1;
+    switch (fast) {   // wave-uniform
+#define TT2_G7F(code, B_, R_, D_, X_)                                                                       \
+  case code:                                                                                                \
+    if constexpr (!B_ || (AK && BKC)) g7_epi_fast<B_, R_, D_, X_>(E, acc, pbias, smem, nkt, m0, n0, wm, wn, lane, seed); \
+    break;
+      TT2_G7F(0, false, false, false, 0)
+      TT2_G7F(1, true, false, false, 0)
+      TT2_G7F(2, false, true, false, 0)
+      TT2_G7F(3, true, true, false, 0)
+      TT2_G7F(4, false, false, true, 0)
+      TT2_G7F(5, true, false, true, 0)
+      TT2_G7F(6, false, true, true, 0)
+      TT2_G7F(7, true, true, true, 0)
+      TT2_G7F(8, false, false, false, 1)
+      TT2_G7F(9, false, false, false, 2)
+#undef TT2_G7F
+      default:
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = wm * 64 + 16 * i + (lane & 15), m = m0 + r;
@@ -1330,7 +1400,10 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
         *reinterpret_cast<bf16x8*>(cp) = x;
       }
     }
+    }
+    G7_STAMP(nkt, 1)
     __syncthreads();
+    G7_STAMP(nkt, 2)
     g7_store_c(P, smem, m0, n0, nkt);
     G7_STAMP(nkt, 3)
     return;
@@ -1434,13 +1507,27 @@ __global__ void gemm_splitk_reduce_g(G7Group G) {
 
 G7Prob g7_prob(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits,
                             float* ws) {
-  G7Prob P{A, B, E, M, N, K, K, 1, (N + 127) / 128, 0, 0, ws, 0, 0};
+  G7Prob P{A, B, E, M, N, K, K, 1, (N + 127) / 128, 0, 0, ws, 0, 0, -1};
   if (splits > 1) {
     P.k_split = ((K + splits - 1) / splits + 63) / 64 * 64;
     P.splits = (K + P.k_split - 1) / P.k_split;
   }
   P.items = ((M + 255) / 256) * P.ntn * P.splits;
   return P;
+}
+
+// g7_epi_fast's option code for this launch, or -1 (general path): bias (forward layout, where
+// it is prefetched), ReLU, dropout, or one staged bf16 residual / gate alone; no beta.
+int g7_fast_code(const G7Prob& P, bool fwd) {
+  const EpiParams& E = P.E;
+  if (!P.lds_epi || E.beta != 0.f || E.act == ACT_TANH) return -1;
+  if (P.pre_x) {
+    const bool alone = !E.bias && E.act == ACT_NONE && !E.drop.thr && (P.pre_x == 1 ? !E.gate : !E.res);
+    return alone ? 7 + P.pre_x : -1;
+  }
+  if (E.res || E.gate) return -1;
+  if (E.bias && !fwd) return -1;
+  return (E.bias ? 1 : 0) | (E.act == ACT_RELU ? 2 : 0) | (E.drop.thr ? 4 : 0);
 }
 
 template <bool AK, bool BKC>
@@ -1450,6 +1537,7 @@ hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   P.lds_epi = lds_epi && P.splits == 1 && E.c_dt == TT2_BF16 && E.vec && (N % 8) == 0;
   // the loader waves stage a bf16 residual / gate tile in LDS during the last K steps
   P.pre_x = !P.lds_epi ? 0 : (E.res && E.res_dt == TT2_BF16) ? 1 : (E.gate && E.gate_dt == TT2_BF16) ? 2 : 0;
+  P.epi_fast = g7_fast_code(P, AK && BKC);
   ProbeScope ps(s);
   if (ps.ext())
     hipExtLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, ps.e0, ps.e1, 0, P);
