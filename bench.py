@@ -241,10 +241,10 @@ def gemm_kernel_name(plan: int, ta: int, tb: int) -> str:
 
 def graph_probe(model, text, tl, mel, ml, reps: int = 5):
     """Per-launch GEMM times inside GRAPH-REPLAYED steps: the training step is captured once
-    more with libtt2's launch probe armed for every GEMM (under capture the probe brackets
-    each main kernel node with external event-record nodes), replayed `reps` times, and each
-    replay's probe events read back.  Returns {key: [launches/step, flops, seconds, bytes]}
-    averaged over the replays, or None if this runtime cannot capture the probe."""
+    more with libtt2's launch probe armed for every GEMM (under capture each v7 / v8 kernel
+    records only its own wall-clock span; nothing is added to the graph), replayed `reps`
+    times, and each replay's spans read back.  Returns {key: [launches/step, flops, seconds,
+    bytes]} averaged over the replays, or None if a probed launch recorded no span."""
     from tt2 import ops
     eng = model.engine
     B, Tx, Ty = text.shape[0], text.shape[1], mel.shape[1]
@@ -268,7 +268,7 @@ def graph_probe(model, text, tl, mel, ml, reps: int = 5):
         for _ in range(reps):
             g.replay()
             try:
-                summ = probe.summary()
+                summ = probe.summary(span=True)
             except RuntimeError as ex:   # a probe the runtime could not record in the graph
                 log(f"[bench] graph probe unavailable ({ex}); eager-step timing only")
                 return None
@@ -283,8 +283,10 @@ def graph_probe(model, text, tl, mel, ml, reps: int = 5):
 
 
 def roofline(model, text, tl, mel, ml, replay: bool = True):
-    """Live per-launch timing of the dominant kernel family in one eager step (the kernels'
-    own dispatch events); graph_probe and (replay) a back-to-back re-launch beside it."""
+    """Live per-launch timing of the dominant kernel family: its launches inside graph-replayed
+    training steps, each timed by the kernel's own wall-clock span (graph_probe; no event or
+    node added to the graph), with the eager step's dispatch events and a back-to-back
+    re-launch beside it."""
     from tt2 import ops
     # rank 0 only: the DP gradient hook must not fire (its all-reduces would have no peers)
     eng = model.engine
@@ -299,18 +301,25 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
         eng.grad_ready_hook = hook
         if hasattr(probe, "close"):
             probe.close()
-    timing = "in-step kernel dispatch events (tt2_probe_arm: the kernel's own dispatch records them), eager step"
     # dominant = the GEMM variant with the most device time
     key, (n, flops, secs, abytes) = max(summ.items(), key=lambda kv: kv[1][2])
+    eager_us = secs / n * 1e6
     gk = (gsum or {}).get(key)
-    # achieved uses the in-step kernel durations (events recorded by the kernel dispatch
-    # itself, as rocprofv3 times it: the rocprof average over the timed graph replays agrees
-    # to 0.1 %, profiles/r03*_step_kernels.md).  Beside it, for reference only: the same
-    # launches inside graph-replayed steps bracketed by event-record nodes (each node pair
-    # adds a dispatch gap, so it reads ~10 % high) and a back-to-back replay (warm caches).
+    if gk:
+        # the launches inside the replayed step graph, as the timed steps run them (rocprofv3's
+        # average over the timed replays agrees, profiles/r03*_step_kernels.md)
+        secs = gk[2] * n / gk[0]
+        timing = ("in-step kernel spans (tt2_probe_span_ms: device wall clock, first workgroup start to last "
+                  "wave end) of the launches inside graph-replayed training steps, mean of 5 replays")
+    else:
+        timing = "in-step kernel dispatch events (tt2_probe_arm: the kernel's own dispatch records them), eager step"
+    # beside it, for reference only: the eager step's dispatch events (each carries the
+    # event's completion signal and host-gap clocks, reads high) and a back-to-back replay
+    # of the same launches (warm caches, no step context).
     replay = probe.replay_time(key) if replay else None
-    tot_t = sum(v[2] for v in summ.values())
-    tot_f = sum(v[1] for v in summ.values())
+    allg = gsum if gk else summ
+    tot_t = sum(v[2] for v in allg.values())
+    tot_f = sum(v[1] for v in allg.values())
     achieved = flops / secs / 1e12
     kname = gemm_kernel_name(*key[1:4])
     if key[0] == "gemm_grouped":
@@ -335,9 +344,9 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
         "mfma_busy_under_profiler": busy, "mfma_busy_source": bsrc,
         "algo_bytes_per_launch": round(abytes / n), "launches_per_step": n, "flops_per_launch": flops / n,
         "avg_launch_us": round(secs / n * 1e6, 2), "timing": timing,
-        "graph_node_avg_launch_us": round(gk[2] / gk[0] * 1e6, 2) if gk else None,
+        "eager_dispatch_avg_launch_us": round(eager_us, 2),
         "replay_avg_launch_us": round(replay / n * 1e6, 2) if replay is not None else None,
-        "all_gemms": {"launches": round(sum(v[0] for v in summ.values())), "ms_per_step": round(tot_t * 1e3, 3),
+        "all_gemms": {"launches": round(sum(v[0] for v in allg.values())), "ms_per_step": round(tot_t * 1e3, 3),
                       "tflops": round(tot_f / tot_t / 1e12, 1)},
     }
 

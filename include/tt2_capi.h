@@ -138,14 +138,19 @@ int tt2_gemm_grouped(const tt2_gemm_args* probs, int32_t n, hipStream_t stream);
 
 /* Measurement probe (bench.py's live roofline): tt2_probe_arm() makes the next main GEMM
  * kernel (v7 / grouped v7 / v8 / LDS-DMA 128x128) launched on this thread by the NEXT
- * tt2_gemm / tt2_gemm_grouped call record start / stop timestamps and returns the slot.
- * Eager: the kernel's own dispatch records them (its execution, as rocprofv3 reports it).
- * Under stream capture: external event-record nodes bracket the kernel node, so each replay
- * of the captured graph re-times it.  Any path of that call disarms the probe.
- * tt2_probe_ms(slot) waits for the stop event and returns the duration in ms (-1 if no
- * probe-capable kernel consumed the slot); tt2_probe_reset() frees every slot. */
+ * tt2_gemm / tt2_gemm_grouped call record its timing and returns the slot.  Eager: start /
+ * stop events ride in the kernel's own dispatch (its execution, as rocprofv3 reports it),
+ * read by tt2_probe_ms (-1 if no probe-capable kernel consumed the slot, or under capture).
+ * Eager and under stream capture alike, v7 / v8 kernels also record their own span on the
+ * device wall clock (tt2_probe_span_ms); nothing is added to a captured graph, so each
+ * replay of it re-times the launch inside the replayed step.  Any path of that call
+ * disarms the probe; tt2_probe_reset() frees every slot. */
 int tt2_probe_arm(void);
 float tt2_probe_ms(int slot);
+/* The same launch's span as the kernel records it on the device wall clock (first workgroup
+ * start to last wave end, no stream event around it): ms, -1 if unavailable.  Reading
+ * re-arms the slot's record, so a graph replayed again records afresh. */
+float tt2_probe_span_ms(int slot);
 void tt2_probe_reset(void);
 
 /* ---------------------------------------------------------------- attention

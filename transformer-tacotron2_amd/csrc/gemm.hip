@@ -40,83 +40,65 @@ namespace {
 struct ProbeSlot { hipEvent_t start, stop; bool used; };
 thread_local std::vector<ProbeSlot> g_probe;
 thread_local int g_probe_armed = -1;
+// Beside the events, every probe-capable kernel records its own span on the device's
+// constant-rate wall clock: each workgroup writes {its start, the end of its last wave after
+// that wave's stores completed} to its own pair of a slot's record (plain stores, no shared
+// address), and tt2_probe_span_ms takes the earliest start and the latest end.  Nothing is
+// added to the stream, so the span of a launch inside a replayed step graph is its in-step
+// duration, with no event node (and its dispatch gap) around it.  Records come from one
+// pool per thread, allocated (zeroed) by the first tt2_probe_arm, outside any capture.
+constexpr int64_t PROBE_SPAN_PAIRS = 1 << 20;
+thread_local unsigned long long* g_span = nullptr;
+thread_local int64_t g_span_used = 0;
+thread_local std::vector<std::pair<int64_t, int>> g_span_rec;   // per slot: pool offset, work groups
 
-int probe_take(hipEvent_t& e0, hipEvent_t& e1) {
+int probe_take(hipEvent_t& e0, hipEvent_t& e1, unsigned long long*& span, int groups) {
+  span = nullptr;
   if (g_probe_armed < 0) return -1;
   const int slot = g_probe_armed;
   ProbeSlot& p = g_probe[slot];
   e0 = p.start;
   e1 = p.stop;
   p.used = true;
+  if (g_span && groups > 0 && g_span_used + groups <= PROBE_SPAN_PAIRS) {
+    span = g_span + 2 * g_span_used;
+    g_span_rec[slot] = {g_span_used, groups};
+    g_span_used += groups;
+  }
   g_probe_armed = -1;
   return slot;
 }
 
-// An event-record node appended to a capturing stream's graph: the runtime's own
-// hipEventRecordWithFlags(External) where it accepts one under capture, else the node is added
-// by hand (hipGraphAddEventRecordNode after the stream's current capture dependencies).
-hipError_t capture_event_node(hipStream_t s, hipEvent_t ev) {
-  hipError_t e = hipEventRecordWithFlags(ev, s, hipEventRecordExternal);
-  if (e == hipSuccess) return e;
-  (void)hipGetLastError();
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  unsigned long long id = 0;
-  hipGraph_t g = nullptr;
-  const hipGraphNode_t* deps = nullptr;
-  size_t nd = 0;
-  e = hipStreamGetCaptureInfo_v2(s, &st, &id, &g, &deps, &nd);
-  if (e != hipSuccess || st != hipStreamCaptureStatusActive || !g) return e != hipSuccess ? e : hipErrorInvalidValue;
-  hipGraphNode_t node = nullptr;
-  e = hipGraphAddEventRecordNode(&node, g, deps, nd, ev);
-  if (e != hipSuccess) return e;
-  return hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies);
+TT2_DEV void span_begin(unsigned long long* span, int* done) {
+  if (span && threadIdx.x == 0) {
+    *done = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // visible before the first barrier
+    span[2 * blockIdx.x] = wall_clock64();
+  }
+}
+// every wave once its own stores have completed (stores count in vmcnt on gfx9); the last
+// wave of the workgroup to get here writes the end
+TT2_DEV void span_end(unsigned long long* span, int* done, int waves) {
+  if (span) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63) == 0 && atomicAdd(done, 1) == waves - 1) span[2 * blockIdx.x + 1] = wall_clock64();
+  }
 }
 
 // The probe around one main-kernel launch.  Eager: the events ride in the kernel's own
-// dispatch (hipExtLaunchKernelGGL, ext()).  Under stream capture (a hipGraph of the step,
-// bench.py's roofline leg): external event-record nodes right before and after the kernel
-// node, so every replay of the graph re-times the launch inside the replayed step.
+// dispatch (hipExtLaunchKernelGGL, ext()) and the kernel records its span.  Under stream
+// capture (a hipGraph of the step, bench.py's graph leg) only the span: nothing is added to
+// the graph, and every replay re-records the launch's in-step duration.
 struct ProbeScope {
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  hipStream_t s;
-  bool capt = false;
-  explicit ProbeScope(hipStream_t st) : s(st) {
-    const int slot = probe_take(e0, e1);
-    if (slot < 0) return;
+  unsigned long long* span = nullptr;   // the kernel's own span record (see g_span)
+  ProbeScope(hipStream_t s, int groups) {
+    if (probe_take(e0, e1, span, groups) < 0) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) {
-      // event nodes take plain timing events (the slot's eager events skip the system fence)
-      ProbeSlot& p = g_probe[slot];
-      hipEvent_t a = nullptr, b = nullptr;
-      hipError_t e1c = hipEventCreate(&a), e2c = hipSuccess, erc = hipSuccess;
-      if (e1c == hipSuccess) e2c = hipEventCreate(&b);
-      if (e1c == hipSuccess && e2c == hipSuccess) erc = capture_event_node(s, a);
-      if (e1c == hipSuccess && e2c == hipSuccess && erc == hipSuccess) {
-        (void)hipEventDestroy(p.start);
-        (void)hipEventDestroy(p.stop);
-        p.start = e0 = a;
-        p.stop = e1 = b;
-        capt = true;
-      } else {   // this runtime cannot record the probe in a graph: the launch goes untimed
-        if (a) (void)hipEventDestroy(a);
-        if (b) (void)hipEventDestroy(b);
-        p.used = false;
-        e0 = e1 = nullptr;
-        std::string m = std::string("launch probe under capture: create ") + hipGetErrorName(e1c) + " / " +
-                        hipGetErrorName(e2c) + ", record " + hipGetErrorName(erc);
-        tt2_set_error(TT2_E_HIP, m.c_str());
-      }
-      (void)hipGetLastError();   // a refused record must not fail the launch check that follows
-    }
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) e0 = e1 = nullptr;
+    (void)hipGetLastError();
   }
-  bool ext() const { return e0 && !capt; }
-  void done() {
-    if (capt) {
-      (void)capture_event_node(s, e1);
-      (void)hipGetLastError();
-    }
-    capt = false;
-  }
+  bool ext() const { return e0 != nullptr; }
 };
 
 
@@ -941,14 +923,13 @@ hipError_t launch2(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   }
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
   dim3 grid(ntm * ntn, splits);
-  ProbeScope ps(s);
+  ProbeScope ps(s, 0);   // no span record in this kernel
   if (ps.ext())
     hipExtLaunchKernelGGL((gemm2_kernel<AK, BKC>), grid, dim3(NT), 0, s, ps.e0, ps.e1, 0, A, B, E, M, N, K, k_split,
                      splits > 1 ? ws : nullptr, ntm, ntn);
   else
     hipLaunchKernelGGL((gemm2_kernel<AK, BKC>), grid, dim3(NT), 0, s, A, B, E, M, N, K, k_split,
                      splits > 1 ? ws : nullptr, ntm, ntn);
-  ps.done();
   if (splits > 1 && !E.main_only)
     hipLaunchKernelGGL(gemm_splitk_reduce, dim3(splitk_blocks(M, N, E)), dim3(256), 0, s, ws, splits, E, M, N);
   return hipGetLastError();
@@ -1102,6 +1083,7 @@ struct G7Prob {
   int lds_epi; // C leaves through an LDS image in whole 256-B row segments (bf16 C, no split)
   int pre_x;     // the loader waves stage the bf16 residual (1) or gate (2) tile in LDS (lds_epi only)
   int epi_fast;  // straight-line image epilogue for this option set (g7_epi_fast), -1: general path
+  unsigned long long* span;   // launch probe's span record (grouped launch: p[0]'s), else null
 };
 constexpr int G7_MAXP = 8;
 // A deferred LayerNorm backward's column-sum finalize (tt2_ln_args with defer_finalize) that
@@ -1457,9 +1439,12 @@ TT2_DEV int xcd_item(int bid, int n) {
 template <bool AK, bool BKC>
 __global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(G7Prob P) {
   __shared__ __attribute__((aligned(1024))) char smem[G7_SMEM];
+  __shared__ int span_done;
   G7_RT(0)
+  span_begin(P.span, &span_done);
   const int u = xcd_item(blockIdx.x, P.items);
   g7_item<AK, BKC>(P, u % (P.items / P.splits), u / (P.items / P.splits), smem);
+  span_end(P.span, &span_done, G7_NT / 64);
   G7_RT(1)
 }
 
@@ -1468,6 +1453,8 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(G7Prob P) {
 template <bool AK, bool BKC>
 __global__ __launch_bounds__(G7_NT, 1) void gemm7g_kernel(G7Group G) {
   __shared__ __attribute__((aligned(1024))) char smem[G7_SMEM];
+  __shared__ int span_done;
+  span_begin(G.p[0].span, &span_done);
   const int u = xcd_item(blockIdx.x, G.items);
   int p = 0;
 #pragma unroll
@@ -1476,6 +1463,7 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7g_kernel(G7Group G) {
   const G7Prob& P = G.p[p];
   const int local = u - P.item0, nt = P.items / P.splits;
   g7_item<AK, BKC>(P, local % nt, local / nt, smem);
+  span_end(G.p[0].span, &span_done, G7_NT / 64);
 }
 
 // split-K reduce of every split problem of a group (blockIdx.y = problem); plane y = np, when
@@ -1507,7 +1495,7 @@ __global__ void gemm_splitk_reduce_g(G7Group G) {
 
 G7Prob g7_prob(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits,
                             float* ws) {
-  G7Prob P{A, B, E, M, N, K, K, 1, (N + 127) / 128, 0, 0, ws, 0, 0, -1};
+  G7Prob P{A, B, E, M, N, K, K, 1, (N + 127) / 128, 0, 0, ws, 0, 0, -1, nullptr};
   if (splits > 1) {
     P.k_split = ((K + splits - 1) / splits + 63) / 64 * 64;
     P.splits = (K + P.k_split - 1) / P.k_split;
@@ -1538,12 +1526,12 @@ hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   // the loader waves stage a bf16 residual / gate tile in LDS during the last K steps
   P.pre_x = !P.lds_epi ? 0 : (E.res && E.res_dt == TT2_BF16) ? 1 : (E.gate && E.gate_dt == TT2_BF16) ? 2 : 0;
   P.epi_fast = g7_fast_code(P, AK && BKC);
-  ProbeScope ps(s);
+  ProbeScope ps(s, P.items);
+  P.span = ps.span;
   if (ps.ext())
     hipExtLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, ps.e0, ps.e1, 0, P);
   else
     hipLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, P);
-  ps.done();
   if (P.splits > 1 && !E.main_only)
     hipLaunchKernelGGL(gemm_splitk_reduce, dim3(splitk_blocks(M, N, E)), dim3(256), 0, s, ws, P.splits, E, M, N);
   return hipGetLastError();
@@ -1641,8 +1629,10 @@ TT2_DEV bf16x8 g8_frag_mc(const char* img, int col0, int s, int lane) {
 
 template <bool BKC>
 __global__ __launch_bounds__(G8_NT, 2) void gemm8_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
-                                                         int ntn, int items) {
+                                                         int ntn, int items, unsigned long long* span) {
   __shared__ __attribute__((aligned(1024))) char smem[G8_STAGES * G8_STAGE];
+  __shared__ int span_done;
+  span_begin(span, &span_done);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5;
   const int tile = xcd_item(blockIdx.x, items);
   const int m0 = (tile / ntn) * 64, n0 = (tile % ntn) * 64;
@@ -1721,18 +1711,18 @@ __global__ __launch_bounds__(G8_NT, 2) void gemm8_kernel(OpDesc A, OpDesc B, Epi
   if (mm < M && nn < N)   // nontemporal, as v7's C (g7_store_c)
     __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(smem + rr * 128 + ((c ^ g8_swz(rr)) << 4)),
                                 reinterpret_cast<u32x4*>(C + (int64_t)mm * E.ldc + nn));
+  span_end(span, &span_done, G8_NT / 64);
 }
 
 template <bool BKC>
 hipError_t launch8(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, hipStream_t s) {
   const int ntn = (N + 63) / 64, items = ((M + 63) / 64) * ntn;
-  ProbeScope ps(s);
+  ProbeScope ps(s, items);
   if (ps.ext())
     hipExtLaunchKernelGGL((gemm8_kernel<BKC>), dim3(items), dim3(G8_NT), 0, s, ps.e0, ps.e1, 0, A, B, E, M, N, K, ntn,
-                          items);
+                          items, ps.span);
   else
-    hipLaunchKernelGGL((gemm8_kernel<BKC>), dim3(items), dim3(G8_NT), 0, s, A, B, E, M, N, K, ntn, items);
-  ps.done();
+    hipLaunchKernelGGL((gemm8_kernel<BKC>), dim3(items), dim3(G8_NT), 0, s, A, B, E, M, N, K, ntn, items, ps.span);
   return hipGetLastError();
 }
 
@@ -1992,7 +1982,8 @@ extern "C" int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int n, const tt2
     if (fin_blocks) hipLaunchKernelGGL(gemm_splitk_reduce_g, dim3(fin_blocks, 1), dim3(256), 0, stream, G);
     return tt2_check_launch(hipGetLastError(), "tt2_gemm_grouped");
   }
-  ProbeScope ps(stream);
+  ProbeScope ps(stream, G.items);
+  G.p[0].span = ps.span;
   if (ps.ext()) {
 #define TT2_G7G(A_, B_) hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_>), dim3(G.items), dim3(G7_NT), 0, stream, ps.e0, ps.e1, 0, G)
     if (!ta && !tb) TT2_G7G(true, true);
@@ -2004,7 +1995,6 @@ extern "C" int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int n, const tt2
   else if (!ta && tb) hipLaunchKernelGGL((gemm7g_kernel<true, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
   else if (ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<false, true>), dim3(G.items), dim3(G7_NT), 0, stream, G);
   else hipLaunchKernelGGL((gemm7g_kernel<false, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
-  ps.done();
   if (main_only) reduce_blocks = 0;
   G.fin_only = reduce_blocks == 0 && fin_blocks > 0;
   if (G.fin_only)
@@ -2023,10 +2013,21 @@ extern "C" int tt2_probe_arm(void) {
   // timing-only events: no system-scope fence (cache write-back) at the probed kernel's end,
   // which would lengthen it beyond what it takes inside the step
   ProbeSlot p{nullptr, nullptr, false};
-  hipError_t e = hipEventCreateWithFlags(&p.start, hipEventDisableSystemFence);
+  hipError_t e = hipSuccess;
+  if (!g_span) {
+    e = hipMalloc(&g_span, 2 * sizeof(unsigned long long) * PROBE_SPAN_PAIRS);
+    if (e == hipSuccess) e = hipMemset(g_span, 0, 2 * sizeof(unsigned long long) * PROBE_SPAN_PAIRS);
+    if (e != hipSuccess) {
+      if (g_span) (void)hipFree(g_span);
+      g_span = nullptr;
+      return tt2_check_launch(e, "tt2_probe_arm (span records)");
+    }
+  }
+  e = hipEventCreateWithFlags(&p.start, hipEventDisableSystemFence);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&p.stop, hipEventDisableSystemFence);
   if (e != hipSuccess) return tt2_check_launch(e, "tt2_probe_arm");
   g_probe.push_back(p);
+  g_span_rec.push_back({-1, 0});
   g_probe_armed = (int)g_probe.size() - 1;
   return g_probe_armed;
 }
@@ -2039,7 +2040,38 @@ extern "C" float tt2_probe_ms(int slot) {
   return ms;
 }
 
+extern "C" float tt2_probe_span_ms(int slot) {
+  if (slot < 0 || slot >= (int)g_probe.size() || !g_probe[slot].used || g_span_rec[slot].first < 0) return -1.f;
+  const int64_t off = g_span_rec[slot].first;
+  const int groups = g_span_rec[slot].second;
+  std::vector<unsigned long long> h(2 * (size_t)groups);
+  if (hipDeviceSynchronize() != hipSuccess) return -1.f;
+  if (hipMemcpy(h.data(), g_span + 2 * off, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1.f;
+  // zeroed again, so the next replay of a graph must record every pair afresh
+  if (hipMemset(g_span + 2 * off, 0, h.size() * 8) != hipSuccess) return -1.f;
+  unsigned long long t0 = ~0ull, t1 = 0;
+  for (int i = 0; i < groups; ++i) {
+    if (h[2 * i] == 0 || h[2 * i + 1] < h[2 * i]) return -1.f;   // a work group left no record
+    t0 = std::min(t0, h[2 * i]);
+    t1 = std::max(t1, h[2 * i + 1]);
+  }
+  static int khz = 0;
+  if (!khz) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) {
+      khz = 0;
+      return -1.f;
+    }
+  }
+  return (float)((double)(t1 - t0) / khz);
+}
+
 extern "C" void tt2_probe_reset(void) {
+  // records of slots never read are zeroed so the pool can be handed out again
+  if (g_span && g_span_used) (void)hipMemset(g_span, 0, 2 * sizeof(unsigned long long) * g_span_used);
+  g_span_used = 0;
+  g_span_rec.clear();
   for (ProbeSlot& p : g_probe) {
     (void)hipEventDestroy(p.start);
     (void)hipEventDestroy(p.stop);

@@ -170,9 +170,9 @@ def gemm_grouped(problems, ws: Workspace | None = None, fin=None):
 
 class LaunchProbe:
     """Times each GEMM's main kernel inside the step with libtt2's launch probe
-    (tt2_probe_arm: the kernel records start / stop events at its own dispatch and
-    completion, as rocprofv3 measures it); used by bench.py for the live per-kernel
-    roofline figure."""
+    (tt2_probe_arm: eager, start / stop events at the kernel's own dispatch and completion,
+    as rocprofv3 measures it; eager or captured, the kernel's own wall-clock span); used by
+    bench.py for the live per-kernel roofline figure."""
 
     def __init__(self):
         self.rec = []
@@ -192,15 +192,19 @@ class LaunchProbe:
                 saved[i] = g
         self.rec.append((key, flops, self._s, e, algo_bytes, saved))
 
-    def summary(self):
+    def summary(self, span: bool = False):
+        """{key: [launches, flops, seconds, algorithmic bytes]}.  Seconds are the dispatch
+        events' (eager launches), or with `span` the kernels' own wall-clock spans (the only
+        record of a launch inside a captured graph; reading one re-arms it for the next
+        replay)."""
         torch.cuda.synchronize()
         out = {}
         L = lib()
         for key, flops, slot, _, ab, _ in self.rec:
-            ms = L.tt2_probe_ms(slot)
+            ms = L.tt2_probe_span_ms(slot) if span else L.tt2_probe_ms(slot)
             if ms < 0:
                 msg = L.tt2_last_error()
-                raise _lib.TT2Error(f"launch probe {slot} ({key}) recorded no kernel"
+                raise _lib.TT2Error(f"launch probe {slot} ({key}) recorded no {'span' if span else 'kernel'}"
                                     f"{' (' + msg.decode() + ')' if msg else ''}")
             d = out.setdefault(key, [0, 0.0, 0.0, 0.0])
             d[0] += 1
