@@ -151,6 +151,11 @@ float tt2_probe_ms(int slot);
  * start to last wave end, no stream event around it): ms, -1 if unavailable.  Reading
  * re-arms the slot's record, so a graph replayed again records afresh. */
 float tt2_probe_span_ms(int slot);
+/* The raw span record of a slot (measurement tools): per work group {start, end} on the device
+ * wall clock (hipDeviceAttributeWallClockRate kHz), copied to out[2 * groups]; returns the
+ * number of work groups, -groups - 1 if cap is too small, -1 if the slot has no record.  Read
+ * it before tt2_probe_span_ms, which clears the record. */
+int tt2_probe_span_records(int slot, unsigned long long* out, int cap);
 void tt2_probe_reset(void);
 
 /* ---------------------------------------------------------------- attention

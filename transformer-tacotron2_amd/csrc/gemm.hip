@@ -2067,6 +2067,17 @@ extern "C" float tt2_probe_span_ms(int slot) {
   return (float)((double)(t1 - t0) / khz);
 }
 
+extern "C" int tt2_probe_span_records(int slot, unsigned long long* out, int cap) {
+  if (slot < 0 || slot >= (int)g_probe.size() || !g_probe[slot].used || g_span_rec[slot].first < 0 || !out)
+    return -1;
+  const int64_t off = g_span_rec[slot].first;
+  const int groups = g_span_rec[slot].second;
+  if (cap < groups) return -groups - 1;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(out, g_span + 2 * off, (size_t)groups * 16, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return groups;
+}
+
 extern "C" void tt2_probe_reset(void) {
   // records of slots never read are zeroed so the pool can be handed out again
   if (g_span && g_span_used) (void)hipMemset(g_span, 0, 2 * sizeof(unsigned long long) * g_span_used);
