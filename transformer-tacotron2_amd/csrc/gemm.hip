@@ -1143,10 +1143,12 @@ TT2_DEV void g7_issue_x(const G7Prob& P, const void* x, int64_t ldx, char* smem,
 // the general path (epi_calc8 over run-time options, with per-lane bounds tests) compiles to
 // a long chain of branches that took ~5k cycles of the MFMA waves per tile (tools/gemm_stamps.hip),
 // as long as three K steps.  Same operations, same order (alpha, bias, residual, ReLU, gate,
-// dropout), so the results are bit-identical to the general path.
+// dropout), so the results are bit-identical to the general path.  The dropout keep bits
+// (drop_bits8 of the lane's 8 groups of 8 columns, group 2 i + pr at bits 8 (2 i + pr)) were
+// hashed during the K loop, where the MFMA waves' VALU is otherwise idle.
 template <bool BIAS, bool RELU, bool DROP, int PX>
 TT2_DEV void g7_epi_fast(const EpiParams& E, const f32x4 (&acc)[4][4], const f32x4 (&pbias)[2][2], char* smem,
-                         int nkt, int m0, int n0, int wm, int wn, int lane, uint32_t seed) {
+                         int nkt, int m0, int n0, int wm, int wn, int lane, uint64_t dbits) {
   const int q = lane >> 4;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1181,7 +1183,11 @@ TT2_DEV void g7_epi_fast(const EpiParams& E, const f32x4 (&acc)[4][4], const f32
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
       }
-      if (DROP) drop_apply8(E.drop, seed, (uint32_t)((int64_t)m * E.n_log + n), v);
+      if (DROP) {
+        const uint32_t kb = (uint32_t)(dbits >> (8 * (2 * i + pr)));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (kb >> j) & 1u ? v[j] * E.drop.scale : 0.f;
+      }
       bf16x8 x;
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] = (bf16)v[j];
@@ -1281,6 +1287,13 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
+  const bool px = P.pre_x && n0 + 128 <= N;
+  // the straight-line image epilogue's option set (wave-uniform), -1: the general path
+  const int fast = (P.lds_epi && m0 + 256 <= M && n0 + 128 <= N && (P.pre_x == 0 || px)) ? P.epi_fast : -1;
+  const bool pre_drop = fast >= 4 && fast <= 7;   // its dropout keep bits are hashed in the K loop
+  const int gps = (8 + nkt - 1) / nkt;            // keep-bit groups per K step
+  uint64_t dbits = 0;
   __builtin_amdgcn_s_barrier();
   int stage = 0;
   for (int t = 0; t < nkt; ++t) {
@@ -1301,6 +1314,15 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
       if (!AK && do_ks) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) mma16(fones, fa[i], ksa[i]);
+      }
+    }
+    if (pre_drop) {   // VALU work beside this step's MFMAs
+      const int g1 = min(8, (t + 1) * gps);
+      for (int gi = t * gps; gi < g1; ++gi) {
+        const int m = m0 + wm * 64 + 16 * (gi >> 1) + (lane & 15);
+        const int n = n0 + wn * 64 + 16 * (2 * (gi & 1) + (ql & 1)) + 8 * (ql >> 1);
+        const uint32_t kb = drop_bits8(seed, E.drop.site, (uint32_t)((int64_t)m * E.n_log + n), E.drop.thr);
+        dbits |= (uint64_t)kb << (8 * gi);
       }
     }
     stage = stage == 2 ? 0 : stage + 1;
@@ -1324,19 +1346,16 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
 
   // lane (q = lane >> 4) holds C[m][n0 + wn*64 + 16 j + 4 q + r] in acc[i][j][r]; swapping
   // column blocks (2p, 2p+1) between row pairs q, q^1 leaves 8 consecutive columns per lane
-  const uint32_t seed = (!ws && E.drop.thr) ? *E.drop.seed : 0u;
   const int q = ql;
-  const bool px = P.pre_x && n0 + 128 <= N;
   if (px) __builtin_amdgcn_s_barrier();   // the loaders' staged residual / gate tile has landed
   if (P.lds_epi) {
     // epilogue values -> bf16 C image [256 rows][16 chunks of 16 B] (chunk c of row r at
     // c ^ (r & 15): the 16 rows of one store instruction hit 16 different bank groups),
     // then all 12 waves store whole 256-B row segments
-    const int fast = (m0 + 256 <= M && n0 + 128 <= N && (P.pre_x == 0 || px)) ? P.epi_fast : -1;
     switch (fast) {   // wave-uniform
 #define TT2_G7F(code, B_, R_, D_, X_)                                                                       \
   case code:                                                                                                \
-    if constexpr (!B_ || (AK && BKC)) g7_epi_fast<B_, R_, D_, X_>(E, acc, pbias, smem, nkt, m0, n0, wm, wn, lane, seed); \
+    if constexpr (!B_ || (AK && BKC)) g7_epi_fast<B_, R_, D_, X_>(E, acc, pbias, smem, nkt, m0, n0, wm, wn, lane, dbits); \
     break;
       TT2_G7F(0, false, false, false, 0)
       TT2_G7F(1, true, false, false, 0)
