@@ -220,6 +220,17 @@ typedef struct tt2_attn_decode_args {
   const void* wq;
   int64_t wq_ld;
   const float* bq;
+  /* optional fused residual combine + LayerNorm of the projection input (ln_part != NULL; needs
+   * wq, 8 heads, q_ld == 512, bf16 / f16): the input row is x[b] = LN(q[b] + ln_bias +
+   * sum_{s<8} ln_part[(s * batch + b) * 512 + :]) exactly as tt2_ln_combine(splits = 8) computes
+   * it (the self-attention's output-projection slabs), and the workgroup of head 0 writes it to
+   * ln_out[b] (the next sublayer's residual): the decoder's first post-LN rides in this launch */
+  const float* ln_part;
+  const float* ln_bias;
+  const float* ln_gamma;
+  const float* ln_beta;
+  void* ln_out;
+  float ln_eps;
 } tt2_attn_decode_args;
 int tt2_attn_decode(const tt2_attn_decode_args* a, hipStream_t stream);
 /* cache[b*c_bstride + (*t_ptr)*c_ld + c] = src[b*src_ld + c], c < n */

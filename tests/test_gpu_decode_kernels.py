@@ -219,6 +219,39 @@ def test_attn_decode_fused_qproj(dtype):
     assert slab[:, 2].abs().sum().item() == 0   # no keys -> zero output, never NaN
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_attn_decode_fused_ln_prologue(dtype):
+    """The self-attention sublayer's residual combine + LayerNorm inside the cross-attention
+    launch (the decode step's fused schedule): bitwise the same row as tt2_ln_combine followed by
+    the fused query projection on that row, written to ln_out by head 0; a finished utterance
+    (stop_len) still gets its row."""
+    g = torch.Generator().manual_seed(21)
+    B, H, d, Tx = 6, 8, 512, 128
+    mk = (lambda sh, sc=1.0: _bf(sh, g, sc)) if dtype == torch.bfloat16 else (lambda sh, sc=1.0: _h(sh, g, sc))
+    x, mem = mk((B, d)), mk((B, Tx, 2 * d))
+    wq, wo = mk((d, d), 1 / math.sqrt(d)), mk((d, d), 1 / math.sqrt(d))
+    bq = torch.randn(d, generator=g).cuda()
+    part = (torch.randn(H, B, d, generator=g) * 0.3).cuda()
+    lb, lg, lbe = (torch.randn(d, generator=g).cuda() for _ in range(3))
+    kl = torch.tensor([128, 5, 77, 128, 9, 64], dtype=torch.int32, device="cuda")
+    step = torch.tensor([3], dtype=torch.int32, device="cuda")
+    stop = torch.tensor([100, 100, 2, 100, 100, 100], dtype=torch.int32, device="cuda")   # row 2 finished
+    h1 = torch.empty(B, d, dtype=dtype, device="cuda")
+    ops.ln_combine(x, part, H, lb, lg, lbe, h1, B)
+    slab_ref = torch.full((H, B, d), float("nan"), device="cuda")
+    ops.attn_decode(h1, mem, mem[:, :, d:], None, d, Tx * 2 * d, 2 * d, Tx * 2 * d, 2 * d, d, B, H, Tx, key_len=kl,
+                    scale=0.125, wo=wo, wo_ld=d, slab=slab_ref, wq=wq, wq_ld=d, bq=bq, stop_len=stop, step=step)
+    out = torch.full((B, d), float("nan"), device="cuda").to(dtype)
+    slab = torch.full((H, B, d), float("nan"), device="cuda")
+    ops.attn_decode(x, mem, mem[:, :, d:], None, d, Tx * 2 * d, 2 * d, Tx * 2 * d, 2 * d, d, B, H, Tx, key_len=kl,
+                    scale=0.125, wo=wo, wo_ld=d, slab=slab, wq=wq, wq_ld=d, bq=bq, stop_len=stop, step=step,
+                    ln=(part, lb, lg, lbe, out, 1e-5))
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int16), h1.view(torch.int16))      # every row, the finished one too
+    assert torch.equal(slab, slab_ref)
+    assert slab[:, 2].abs().sum().item() == 0
+
+
 def _h(shape, gen, scale=1.0):
     return (torch.randn(shape, generator=gen) * scale).half().cuda()
 

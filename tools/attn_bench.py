@@ -1,81 +1,53 @@
-"""Attention kernel micro-benchmark on the GPU (dev tool).
+"""The training step's attention launches on their own (dev tool, GPU): decoder causal
+self-attention (B=16, H=8, 800 x 800), cross-attention (800 queries x 128 keys) and encoder
+self-attention (128 x 128), forward and backward, bf16, each as 10 launches replayed from a
+hipGraph (best of 3); prints us, TFLOP/s (causal counted half) and a checksum.
 
-Times tt2_attn_fwd / tt2_attn_bwd at the three attention shapes of the bench
-workload (B=16, H=8, text 128, mel 800) for each kernel variant and prints
-achieved TFLOP/s (causal FLOPs counted over the visible triangle only).
-
-    python tools/attn_bench.py [variants...]      (default: 1 2 3)
+    python tools/attn_bench.py [reps]
 """
-import math
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "transformer-tacotron2_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 import torch  # noqa: E402
 
-from tt2 import ops  # noqa: E402
-
-
-def timeit(fn, iters=20):
-    for _ in range(3):
-        fn()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters * 1e-3
-
+from v9_ab import graph_of, time_graph, ops  # noqa: E402
 
 B, H, D = 16, 8, 64
-SHAPES = [  # name, Tq, Tk, causal, packed
-    ("enc self", 128, 128, False, True),
-    ("dec self", 800, 800, True, True),
-    ("cross", 800, 128, False, False),
-]
+CASES = [("dec self causal", 800, 800, True), ("cross", 800, 128, False), ("enc self", 128, 128, False)]
 
 
-def run(variant):
-    ops.ATTN_VARIANT = variant
-    g = torch.Generator(device="cuda").manual_seed(0)
-    HD = H * D
-    for name, Tq, Tk, causal, packed in SHAPES:
-        if packed:
-            qkv = torch.randn(B * Tq, 3 * HD, device="cuda", generator=g).bfloat16()
-            q, k, v = qkv[:, :HD], qkv[:, HD:2 * HD], qkv[:, 2 * HD:]
-            lq = lk = lv = 3 * HD
-        else:
-            q = torch.randn(B * Tq, HD, device="cuda", generator=g).bfloat16()
-            kv = torch.randn(B * Tk, 2 * HD, device="cuda", generator=g).bfloat16()
-            k, v = kv[:, :HD], kv[:, HD:]
-            lq, lk, lv = HD, 2 * HD, 2 * HD
-        klen = torch.full((B,), Tk, dtype=torch.int32, device="cuda")
-        out = torch.empty(B * Tq, HD, dtype=torch.bfloat16, device="cuda")
-        lse = torch.empty(B * H, Tq, device="cuda")
-        dout = torch.randn(B * Tq, HD, device="cuda", generator=g).bfloat16()
-        delta = torch.empty(B * H, Tq, device="cuda")
-        dq = torch.empty(B * Tq, HD, dtype=torch.bfloat16, device="cuda")
-        dkv = torch.empty(B * Tk, 2 * HD, dtype=torch.bfloat16, device="cuda")
-        scale = 1.0 / math.sqrt(D)
-
-        def fwd():
-            ops.attn_fwd(q, k, v, out, lse, lq, lk, lv, HD, B, H, Tq, Tk, klen, causal, scale)
-
-        def bwd():
-            ops.attn_bwd(q, k, v, out, dout, lse, delta, dq, dkv[:, :HD], dkv[:, HD:], lq, lk, lv, HD, HD, HD,
-                         2 * HD, 2 * HD, B, H, Tq, Tk, klen, causal, scale)
-
-        pairs = B * H * (Tq * (Tq + 1) / 2 if causal else Tq * Tk)
-        tf = timeit(fwd)
-        fwd()
-        tb = timeit(bwd)
-        print(f"v{variant} {name:9s} fwd {tf * 1e6:7.1f} us {4 * pairs * D / tf / 1e12:6.1f} TF | "
-              f"bwd {tb * 1e6:7.1f} us {10 * pairs * D / tb / 1e12:6.1f} TF", flush=True)
+def main():
+    torch.manual_seed(0)
+    for name, tq, tk, causal in CASES:
+        d = H * D
+        qkv = (torch.randn(B * tq, 3 * d, device="cuda") * 0.5).bfloat16()
+        kv = (torch.randn(B * tk, 2 * d, device="cuda") * 0.5).bfloat16()
+        q, k, v = (qkv, qkv[:, d:], qkv[:, 2 * d:]) if tq == tk else (qkv, kv, kv[:, d:])
+        qld, kld = 3 * d, (3 * d if tq == tk else 2 * d)
+        out = torch.empty(B * tq, d, device="cuda", dtype=torch.bfloat16)
+        lse = torch.empty(B * H, tq, device="cuda")
+        klen = torch.full((B,), tk, dtype=torch.int32, device="cuda")
+        fwd = lambda: ops.attn_fwd(q, k, v, out, lse, qld, kld, kld, d, B, H, tq, tk, klen, causal, 0.125)  # noqa
+        g = graph_of(fwd)
+        tf = min(time_graph(g) for _ in range(3))
+        del g
+        dout = (torch.randn(B * tq, d, device="cuda") * 0.1).bfloat16()
+        dq = torch.empty(B * tq, d, device="cuda", dtype=torch.bfloat16)
+        dk = torch.empty(B * tk, d, device="cuda", dtype=torch.bfloat16)
+        dv = torch.empty(B * tk, d, device="cuda", dtype=torch.bfloat16)
+        delta = torch.empty(B * H, max(tq, tk), device="cuda")
+        bwd = lambda: ops.attn_bwd(q, k, v, out, dout, lse, delta, dq, dk, dv, qld, kld, kld, d, d, d, d, d,  # noqa
+                                   B, H, tq, tk, klen, causal, 0.125)
+        g = graph_of(bwd)
+        tb = min(time_graph(g) for _ in range(3))
+        del g
+        fl = 4.0 * B * H * tq * tk * D * (0.5 if causal else 1.0)
+        print(f"{name:16s} fwd {tf * 1e6:6.1f} us {fl / tf / 1e12:5.0f} TF | bwd {tb * 1e6:6.1f} us "
+              f"{2.5 * fl / tb / 1e12:5.0f} TF | sum {out.float().sum().item():.5e} {dq.float().sum().item():.5e}",
+              flush=True)
 
 
 if __name__ == "__main__":
-    for v in [int(x) for x in sys.argv[1:]] or [1, 2, 3]:
-        run(v)
+    main()

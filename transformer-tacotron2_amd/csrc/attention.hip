@@ -622,7 +622,9 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
     }
     const bf16* cK = sK[BUF];
     const bf16* cV = sV[BUF];
-    if (!(a.causal && k0 > qw + 31)) {   // wave-uniform: some key of the tile is visible
+    // wave-uniform: the wave has a query row (the last block of a head is partly past Tq:
+    // 800 queries give 6.25 blocks of 128) and some key of the tile is visible
+    if (qw < a.Tq && !(a.causal && k0 > qw + 31)) {
       f32x16 s[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -756,7 +758,7 @@ TT2_DEV void attn_bwd_dq3_body(const AttnArgs& a, int bx, int by, int ny, char* 
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       const int kb0 = k0 + 32 * kb;
-      if (a.causal && kb0 > qw + 31) continue;   // wave-uniform
+      if (qw >= a.Tq || (a.causal && kb0 > qw + 31)) continue;   // wave-uniform (no query row, or masked)
       f32x16 s, dp;
       zero16(s);
       zero16(dp);

@@ -52,24 +52,42 @@ struct DecArgs {
   float scale;
   const void* wo; int64_t wo_ld; float* slab;   // fused output projection (wo != null)
   const void* wq; int64_t wq_ld; const float* bq;   // fused query projection (wq != null; q = its input)
+  // fused residual combine + LayerNorm of the projection input (ln_part != null): x[b] =
+  // LN(q[b] + ln_bias + sum_s ln_part[s][b]) (ln_combine_row), written to ln_out by head 0
+  const float* ln_part; const float* ln_bias; const float* ln_gamma; const float* ln_beta; void* ln_out;
+  float ln_eps;
 };
 
 // q-prologue (wq != null): this head's 64 query values from the projection input row x[b]
 // (H*64 wide): wave w computes output rows 8w .. 8w+7 (NW = 8), eight lanes per row, each lane
 // 64 consecutive k (8 x 16-B chunks of W and of x, all issued before the first FMA); the eight
 // partials of a row meet by xor shuffles.  Result (f32, + bias) in sq[64].
+// The projection weights are loaded first (qproj_w: they do not depend on x, so their latency
+// overlaps the fused LayerNorm prologue); sx: the input row already in LDS (f32 values of T,
+// that prologue), or null (x read from q).
 template <typename T, int NW>
-TT2_DEV void qproj(const DecArgs& a, int b, int h, float* sq) {
+TT2_DEV void qproj_w(const DecArgs& a, int h, float (&wv)[8][8]) {
   static_assert(NW == 8, "one wave per 8 query rows");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 7, g = lane >> 3;
   const int r = h * D + 8 * w + g;   // output feature
-  const T* x = reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld + 64 * c;
   const T* wr = reinterpret_cast<const T*>(a.wq) + (int64_t)r * a.wq_ld + 64 * c;
-  float xv[8][8], wv[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) load8f(wr + 8 * i, wv[i]);
+}
+template <typename T, int NW>
+TT2_DEV void qproj(const DecArgs& a, int b, int h, float* sq, const float* sx, const float (&wv)[8][8]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 7, g = lane >> 3;
+  const int r = h * D + 8 * w + g;   // output feature
+  const T* x = reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld + 64 * c;
+  float xv[8][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    load8f(wr + 8 * i, wv[i]);
-    load8f(x + 8 * i, xv[i]);
+    if (sx) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[i][j] = sx[64 * c + 8 * i + j];
+    } else {
+      load8f(x + 8 * i, xv[i]);
+    }
   }
   float p = 0.f;
 #pragma unroll
@@ -113,11 +131,28 @@ TT2_DEV void oproj_slab(const DecArgs& a, int b, int h, const float (&o)[8], flo
 template <typename T, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
   constexpr int U = 4;   // 8-key groups per wave per iteration: 2*U 16-B loads in flight per lane
-  __shared__ float sm[NW], sl[NW], so[NW][D], sfin[D], sres[512], sq[D];
+  __shared__ float sm[NW], sl[NW], so[NW][D], sfin[D], sres[512], sq[D], sx[512];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
   const int dc = lane & 7, kg = lane >> 3;   // 8-dim chunk, key slot within an 8-key group
+  // fused prologue (ln_part): wave 0 combines + normalises the projection input row into sx
+  // (f32 values of T) and head 0's workgroup writes it to ln_out
+  auto ln_prologue = [&]() {
+    if (w != 0) return;
+    float o[8];
+    ln_combine_row<8, T>(reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld, a.ln_part + (int64_t)b * 512,
+                         (int64_t)a.B * 512, a.ln_bias, a.ln_gamma, a.ln_beta, a.ln_eps, lane, o);
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    t8 y;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      y[j] = from_f32<T>(o[j]);
+      sx[lane * 8 + j] = (float)y[j];
+    }
+    if (h == 0) *reinterpret_cast<t8*>(reinterpret_cast<T*>(a.ln_out) + (int64_t)b * 512 + lane * 8) = y;
+  };
   if (a.stop_len && *a.step >= a.stop_len[b]) {
+    if (a.ln_part) ln_prologue();   // the row stays defined for the sublayers after this one
     // a finished utterance: its frames past the stop are discarded, so skip the key stream
     if (a.out && threadIdx.x < D)
       reinterpret_cast<T*>(a.out)[(int64_t)b * a.o_ld + h * D + threadIdx.x] = from_f32<T>(0.f);
@@ -149,7 +184,13 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
   if (k0 < k1) load_keys(k0);
   float qv[8];
   if (a.wq) {
-    qproj<T, NW>(a, b, h, sq);
+    float wv[8][8];
+    qproj_w<T, NW>(a, h, wv);
+    if (a.ln_part) {   // the projection input row: residual combine + LayerNorm, rounded to T
+      ln_prologue();
+      __syncthreads();
+    }
+    qproj<T, NW>(a, b, h, sq, a.ln_part ? sx : nullptr, wv);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 8; ++j) qv[j] = sq[dc * 8 + j];
@@ -284,6 +325,12 @@ extern "C" int tt2_attn_decode(const tt2_attn_decode_args* p, hipStream_t s) {
   a.B = p->batch;
   a.wo = p->wo; a.wo_ld = p->wo_ld; a.slab = p->slab;
   a.wq = p->wq; a.wq_ld = p->wq_ld; a.bq = p->bq;
+  a.ln_part = p->ln_part; a.ln_bias = p->ln_bias; a.ln_gamma = p->ln_gamma; a.ln_beta = p->ln_beta;
+  a.ln_out = p->ln_out; a.ln_eps = p->ln_eps;
+  if (a.ln_part && (!a.wq || p->heads != 8 || !p->ln_bias || !p->ln_gamma || !p->ln_beta || !p->ln_out ||
+                    p->q_ld != 512 || p->dtype == TT2_DT_F32))
+    return tt2_set_error(TT2_E_INVALID, "tt2_attn_decode: the fused LayerNorm prologue needs the fused query "
+                                       "projection, 8 heads, bias / gamma / beta / ln_out and a packed bf16 / f16 q");
   if (a.wq && ((p->wq_ld * esz) % 16 || p->heads * D != 512))
     return tt2_set_error(TT2_E_INVALID, "tt2_attn_decode: the fused query projection needs a 16-B wq_ld and "
                                        "heads * head_dim == 512");

@@ -9,7 +9,8 @@
 //    and the frame emit (heads); the attention launches carry the output projections o / co
 //    (one f32 slab per head) and the cross-attention's query projection cq; ffn2 runs split-K
 //    into raw f32 slabs; tt2_ln_combine folds each sublayer's slabs with bias + residual
-//    into its LayerNorm.  8 launches per layer + 4.
+//    into its LayerNorm, except the first post-LN of a layer, which rides in the cross-attention
+//    launch's prologue (it feeds that launch's query projection).  7 launches per layer + 4.
 //  * plain (f32 parity mode, or batch > 64): one launch per op (GEMM, KV append,
 //    LayerNorm, PE, emit), no slabs.
 // The step reads the frame index from the device counter d->step and bumps it in the
@@ -165,9 +166,12 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
     TT2_TRY(tt2_posenc_fwd(&pa, s));
   }
 
+  // slab: where the fused output projection writes (one f32 slab per head); ln: the fused
+  // residual combine + LayerNorm of the query projection's input (tt2_attn_decode_args.ln_part)
+  struct LnIn { const float* part; const float* bias; const float* gamma; const float* beta; void* out; };
   auto attn = [&](const void* q, int64_t q_ld, const void* k, const void* v, int64_t bstride, int64_t ld, int tk,
-                  const int32_t* key_len, const int32_t* t_ptr, void* out, const void* wo,
-                  const void* wq = nullptr, const float* bq = nullptr) {
+                  const int32_t* key_len, const int32_t* t_ptr, void* out, const void* wo, float* slab,
+                  const void* wq = nullptr, const float* bq = nullptr, const LnIn* ln = nullptr) {
     tt2_attn_decode_args a;
     std::memset(&a, 0, sizeof(a));
     a.q = q; a.k = k; a.v = v; a.out = out;
@@ -176,10 +180,14 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
     a.batch = B; a.heads = H; a.head_dim = D / H; a.tk = tk; a.dtype = dt; a.scale = scale;
     a.stop_len = d->stop_len; a.step = d->step;
     if (wo) {   // split schedule: the output projection rides in the attention launch (one slab per head)
-      a.out = nullptr; a.wo = wo; a.wo_ld = D; a.slab = b.slab;
+      a.out = nullptr; a.wo = wo; a.wo_ld = D; a.slab = slab;
     }
     if (wq) {   // ... and the query projection (q is then its input row)
       a.wq = wq; a.wq_ld = D; a.bq = bq;
+    }
+    if (ln) {   // ... whose input row is the previous sublayer's residual combine + LayerNorm
+      a.ln_part = ln->part; a.ln_bias = ln->bias; a.ln_gamma = ln->gamma; a.ln_beta = ln->beta;
+      a.ln_out = ln->out; a.ln_eps = d->ln_eps;
     }
     return tt2_attn_decode(&a, s);
   };
@@ -214,12 +222,16 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
       TT2_TRY(tt2_gemm(&g, s));
       if (!split) TT2_TRY(tt2_kv_append(b.qkv + D * e, 3 * D, cache, cb, 2 * D, 2 * D, B, d->step, dt, s));
     }
+    // fused schedule: the self-attention's slabs go to slab[0 .. H B D), the cross-attention's
+    // (which reads them in its LayerNorm prologue) to slab2 = slab + H B D
+    float* slab2 = b.slab + (size_t)H * B * D;
     TT2_TRY(attn(b.qkv, 3 * D, cache, cache + D * e, cb, 2 * D, d->t_max, nullptr, d->step, b.att,
-                 fuse_o ? L.o_w : nullptr));
+                 fuse_o ? L.o_w : nullptr, b.slab));
     if (split) {
-      if (!fuse_o) TT2_TRY(slabs(b.att, L.o_w, D, D, SPLIT_O));
-      TT2_TRY(tt2_ln_combine(x, b.slab, fuse_o ? H : SPLIT_O, L.o_b, L.ln1_g, L.ln1_b, b.h1, B, D, d->ln_eps, dt,
-                             s));
+      if (!fuse_o) {
+        TT2_TRY(slabs(b.att, L.o_w, D, D, SPLIT_O));
+        TT2_TRY(tt2_ln_combine(x, b.slab, SPLIT_O, L.o_b, L.ln1_g, L.ln1_b, b.h1, B, D, d->ln_eps, dt, s));
+      }
     } else {
       tt2_gemm_args g = lin(b.att, L.o_w, b.o, B, D, D, L.o_b, dt, dt);
       TT2_TRY(tt2_gemm(&g, s));
@@ -232,13 +244,18 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
       TT2_TRY(tt2_gemm(&g, s));
     }
     const char* mk = mkv + (size_t)2 * D * l * e;
-    TT2_TRY(attn(fuse_o ? b.h1 : b.cq, D, mk, mk + D * e, (int64_t)d->text_len * kvld, kvld, d->text_len,
-                 d->text_lens, nullptr, b.catt, fuse_o ? L.co_w : nullptr, fuse_o ? L.cq_w : nullptr,
-                 fuse_o ? L.cq_b : nullptr));
+    if (fuse_o) {   // h1 = LN1(x + o_b + self slabs) in the prologue; q = cq(h1); co slabs to slab2
+      const LnIn ln{b.slab, L.o_b, L.ln1_g, L.ln1_b, b.h1};
+      TT2_TRY(attn(x, D, mk, mk + D * e, (int64_t)d->text_len * kvld, kvld, d->text_len, d->text_lens, nullptr,
+                   b.catt, L.co_w, slab2, L.cq_w, L.cq_b, &ln));
+    } else {
+      TT2_TRY(attn(b.cq, D, mk, mk + D * e, (int64_t)d->text_len * kvld, kvld, d->text_len, d->text_lens, nullptr,
+                   b.catt, nullptr, nullptr));
+    }
     if (split) {
       if (!fuse_o) TT2_TRY(slabs(b.catt, L.co_w, D, D, SPLIT_O));
-      TT2_TRY(tt2_ln_combine(b.h1, b.slab, fuse_o ? H : SPLIT_O, L.co_b, L.ln2_g, L.ln2_b, b.h2, B, D, d->ln_eps,
-                             dt, s));
+      TT2_TRY(tt2_ln_combine(b.h1, fuse_o ? slab2 : b.slab, fuse_o ? H : SPLIT_O, L.co_b, L.ln2_g, L.ln2_b, b.h2, B,
+                             D, d->ln_eps, dt, s));
     } else {
       tt2_gemm_args g = lin(b.catt, L.co_w, b.co, B, D, D, L.co_b, dt, dt);
       TT2_TRY(tt2_gemm(&g, s));

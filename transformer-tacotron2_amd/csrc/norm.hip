@@ -163,32 +163,10 @@ __global__ __launch_bounds__(NT) void ln_combine_kernel(const T* x, const float*
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
-  const int c0 = lane * 8;
-  float v[8], p[S][8], bb[8], g[8], be[8];
-  ld8(x + (int64_t)row * C + c0, v);
-#pragma unroll
-  for (int s = 0; s < S; ++s) ld8(part + ((int64_t)s * M + row) * C + c0, p[s]);
-  ld8(bias + c0, bb);
-  ld8(gamma + c0, g);
-  ld8(beta + c0, be);
-  float sum = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float a = bb[j];
-#pragma unroll
-    for (int s = 0; s < S; ++s) a += p[s][j];   // fixed order: reproducible
-    v[j] += a;
-    sum += v[j];
-  }
-  const float mean = wave_sum(sum) / C;
-  float sq = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { const float d = v[j] - mean; sq += d * d; }
-  const float rstd = rsqrtf(wave_sum(sq) / C + eps);
   float o[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (v[j] - mean) * rstd * g[j] + be[j];
-  st8(y + (int64_t)row * C + c0, o);
+  ln_combine_row<S, T>(x + (int64_t)row * C, part + (int64_t)row * C, (int64_t)M * C, bias, gamma, beta, eps, lane,
+                       o);
+  st8(y + (int64_t)row * C + lane * 8, o);
 }
 
 // Backward: 8 waves per workgroup, one 512-wide row per wave at a time, software-

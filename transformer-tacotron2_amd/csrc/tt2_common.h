@@ -160,6 +160,54 @@ TT2_DEV float wave_sum(float v) {
   const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
+// 8 consecutive elements as f32
+template <typename T> TT2_DEV void ld8f(const T* p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 4) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+  } else {
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    const t8 x = *reinterpret_cast<const t8*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)x[j];
+  }
+}
+
+// The decode step's residual combine + LayerNorm of one 512-wide row by one wave (lane =
+// 8-column chunk c0 = 8 lane): y = LN(x + (bias + sum_s part[s])) with the slab sum in fixed
+// order.  tt2_ln_combine and the cross-attention launch's fused prologue both call it, so
+// the two round identically.  part: this row's slab 0 (slabs part_stride floats apart).
+template <int S, typename T>
+TT2_DEV void ln_combine_row(const T* x, const float* part, int64_t part_stride, const float* bias,
+                            const float* gamma, const float* beta, float eps, int lane, float (&o)[8]) {
+  constexpr int C = 512;
+  const int c0 = lane * 8;
+  float v[8], p[S][8], bb[8], g[8], be[8];
+  ld8f(x + c0, v);
+#pragma unroll
+  for (int s = 0; s < S; ++s) ld8f(part + s * part_stride + c0, p[s]);
+  ld8f(bias + c0, bb);
+  ld8f(gamma + c0, g);
+  ld8f(beta + c0, be);
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float a = bb[j];
+#pragma unroll
+    for (int s = 0; s < S; ++s) a += p[s][j];   // fixed order: reproducible
+    v[j] += a;
+    sum += v[j];
+  }
+  const float mean = wave_sum(sum) / C;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { const float d = v[j] - mean; sq += d * d; }
+  const float rstd = rsqrtf(wave_sum(sq) / C + eps);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (v[j] - mean) * rstd * g[j] + be[j];
+}
+
 TT2_DEV float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -255,6 +255,7 @@ class AttnDecodeArgs(C.Structure):
         ("stop_len", vp), ("step", vp),
         ("wo", vp), ("wo_ld", i64), ("slab", vp),
         ("wq", vp), ("wq_ld", i64), ("bq", vp),
+        ("ln_part", vp), ("ln_bias", vp), ("ln_gamma", vp), ("ln_beta", vp), ("ln_out", vp), ("ln_eps", f32),
     ]
 
 

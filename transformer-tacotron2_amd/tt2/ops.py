@@ -486,13 +486,19 @@ def step_bump(step, seed=None):
 
 def attn_decode(q, k, v, out, q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld, batch, heads, tk, key_len=None,
                 t_ptr=None, scale=0.125, stop_len=None, step=None, wo=None, wo_ld=0, slab=None, wq=None, wq_ld=0,
-                bq=None):
+                bq=None, ln=None):
     """One query row per batch element over a key cache (see tt2_attn_decode_args).
     wo / slab: the fused output projection, slab[h, b, :] = o[b, h] @ wo[:, h*64:(h+1)*64]^T (f32).
     wq / bq: the fused query projection, q is then the projection input x and the head's
-    query is x[b] @ wq[h*64:(h+1)*64]^T + bq[h*64:(h+1)*64]."""
+    query is x[b] @ wq[h*64:(h+1)*64]^T + bq[h*64:(h+1)*64].
+    ln = (part, bias, gamma, beta, out, eps): with wq, the projection input row is first
+    LN(q[b] + bias + sum of the 8 slabs part[s, b]) (as ln_combine), written to out[b]."""
     a = _lib.AttnDecodeArgs()
     a.wq, a.wq_ld, a.bq = ptr(wq), wq_ld, ptr(bq)
+    if ln is not None:
+        part, lb, lg, lbe, lo, eps = ln
+        a.ln_part, a.ln_bias, a.ln_gamma, a.ln_beta, a.ln_out, a.ln_eps = ptr(part), ptr(lb), ptr(lg), ptr(lbe), \
+            ptr(lo), eps
     a.stop_len, a.step = ptr(stop_len), ptr(step)
     a.q, a.k, a.v, a.out = q.data_ptr(), k.data_ptr(), v.data_ptr(), ptr(out)
     a.wo, a.wo_ld, a.slab = ptr(wo), wo_ld, ptr(slab)
