@@ -576,6 +576,11 @@ TT2_DEV void zero16(f32x16& x) {
   for (int i = 0; i < 16; ++i) x[i] = 0.f;
 }
 
+// in-kernel timeline hooks of the v3 forward (tools/attn_stamps.hip defines them; empty here)
+#ifndef ATTN_STAMP
+#define ATTN_STAMP(slot)
+#endif
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
   constexpr int NTH = NW * 64, PER = Stage3<NTH>::PER, QB = 32 * NW;
@@ -586,6 +591,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
   const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;   // x = (batch, head): block index on y
   const int qblk = a.causal ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;   // heavy blocks first
   const int q0 = qblk * QB, qw = q0 + 32 * w, qv = qw + ql;
+  ATTN_STAMP(0)
   const RowBuf Q = row_buf(reinterpret_cast<const bf16*>(a.q) + (int64_t)b * a.Tq * a.q_ld + h * D, a.q_ld, a.Tq);
   const RowBuf K = row_buf(reinterpret_cast<const bf16*>(a.k) + (int64_t)b * a.Tk * a.k_ld + h * D, a.k_ld, a.Tk);
   const RowBuf V = row_buf(reinterpret_cast<const bf16*>(a.v) + (int64_t)b * a.Tk * a.v_ld + h * D, a.v_ld, a.Tk);
@@ -611,6 +617,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
     r2s3<NTH>(rv, sV[0], tid);
   }
   __syncthreads();
+  ATTN_STAMP(1)
   // one 64-key tile; BUF is compile-time so every LDS address is lane base + immediate
   auto tile = [&](auto BUFC, int t) {
     constexpr int BUF = decltype(BUFC)::value;
@@ -646,6 +653,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
       mx = xor32_max(mx);
+      ATTN_STAMP(2 + 4 * t)
       const float mn = fmaxf(m_r, mx * c);
       const float base = mn == -INFINITY ? 0.f : mn;
       if (__any(mn != m_r)) {   // exact: skipped lanes would multiply by 1
@@ -673,11 +681,14 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
 #pragma unroll
           for (int db = 0; db < 2; ++db) mma32(trfrag(cV, 32 * kb + 16 * hh, db, lane), pf[kb][hh], o[db]);
     }
+    ATTN_STAMP(3 + 4 * t)
     if (more) {
       r2s3<NTH>(rk, sK[BUF ^ 1], tid);
       r2s3<NTH>(rv, sV[BUF ^ 1], tid);
     }
+    ATTN_STAMP(4 + 4 * t)
     __syncthreads();
+    ATTN_STAMP(5 + 4 * t)
   };
   for (int t = 0; t < ntile; t += 2) {
     tile(std::integral_constant<int, 0>{}, t);
