@@ -326,7 +326,8 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
         kname = kname.replace("gemm7_kernel", "gemm7g_kernel")
     traffic, tsrc = None, None
     prof = os.path.join(ROOT, "profiles")
-    tfiles = sorted(f for f in os.listdir(prof) if f.endswith("_traffic.json")) if os.path.isdir(prof) else []
+    tfiles = sorted(f for f in os.listdir(prof) if f.endswith("_traffic.json")
+                    and not f.endswith("_decode_traffic.json")) if os.path.isdir(prof) else []
     if tfiles:
         t = json.load(open(os.path.join(prof, tfiles[-1])))
         if t.get("kernel", "") == kname:
