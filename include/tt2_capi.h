@@ -397,10 +397,28 @@ typedef struct tt2_bn_args {
   float eps, momentum;
   uint32_t drop_site, drop_thr;
   float drop_scale;
+  /* SyncBatchNorm (the *_stats / *_apply phases below; ignored by tt2_batchnorm_fwd/bwd) */
+  float* sync_buf;               /* tt2_batchnorm_sync_size bytes, 16-B aligned */
+  int32_t sync_world, sync_rank;
 } tt2_bn_args;
 size_t tt2_batchnorm_workspace_size(const tt2_bn_args* a);
 int tt2_batchnorm_fwd(const tt2_bn_args* a, hipStream_t stream);
 int tt2_batchnorm_bwd(const tt2_bn_args* a, hipStream_t stream);
+/* SyncBatchNorm over sync_world data-parallel ranks of m rows each (torch.nn.SyncBatchNorm's
+ * semantics: training statistics and the backward's column sums over all W*m rows; the
+ * dgamma / dbeta parameter gradients stay this rank's sums, for the gradient all-reduce).
+ * Each pass is two phases around a caller-issued SUM all-reduce of the first
+ * sync_world * 2 * c floats of sync_buf (this rank's slot holds its moments / sums, the
+ * other slots zeros, so the reduced slots are exact and rank-ordered on every rank):
+ *   tt2_batchnorm_fwd_stats -> all-reduce -> tt2_batchnorm_fwd_apply   (training only)
+ *   tt2_batchnorm_bwd_stats -> all-reduce -> tt2_batchnorm_bwd_apply
+ * sync_world = 1 reproduces tt2_batchnorm_fwd / _bwd (no exchange needed).  The optional
+ * SyncBN of SURVEY.md:219 (per-replica statistics stay the default). */
+size_t tt2_batchnorm_sync_size(const tt2_bn_args* a);
+int tt2_batchnorm_fwd_stats(const tt2_bn_args* a, hipStream_t stream);
+int tt2_batchnorm_fwd_apply(const tt2_bn_args* a, hipStream_t stream);
+int tt2_batchnorm_bwd_stats(const tt2_bn_args* a, hipStream_t stream);
+int tt2_batchnorm_bwd_apply(const tt2_bn_args* a, hipStream_t stream);
 
 /* -------------------------------------------------- embedding / pos. enc. */
 int tt2_embedding_fwd(const int64_t* ids, const void* table, void* out, int m, int c, int vocab, int dtype,

@@ -95,3 +95,33 @@ def _dp_oracle_case(rank, world):
 def test_dp_gradient_is_mean_of_shards():
     out = run_world(_dp_oracle_case)
     assert all(v < 1e-5 for v in out.values()), out
+
+
+def _bnsync_case(rank, world):
+    """SyncBatchNorm's exchange protocol (tt2/dist.py BnSync, the tt2_batchnorm_*_stats slot
+    layout): each rank fills only its own [2][C] slot of the [world][2][C] buffer, the SUM
+    all-reduce gives every rank every slot, and combining them in rank order the way
+    bn_sync_finalize_kernel does (mean of means, M2 + M (mean_r - mean)^2) gives the
+    statistics of the concatenated rows."""
+    from tt2.dist import BnSync
+    M, C = 37, 16
+    ys = [torch.randn(M, C, generator=torch.Generator().manual_seed(50 + r), dtype=torch.float64) * (1 + r) + r
+          for r in range(world)]
+    s = BnSync(world, rank, device="cpu")
+    buf = s.buffer((world + 1) * 2 * C * 4)
+    slots = buf[:world * 2 * C].view(world, 2, C)
+    slots.zero_()
+    y = ys[rank]
+    slots[rank, 0] = y.mean(0).float()
+    slots[rank, 1] = ((y - y.mean(0)) ** 2).sum(0).float()
+    s.exchange(buf[:world * 2 * C])
+    mu = slots[:, 0].double().mean(0)
+    m2 = (slots[:, 1].double() + M * (slots[:, 0].double() - mu) ** 2).sum(0)
+    full = torch.cat(ys)
+    return max((mu - full.mean(0)).abs().max().item(),
+               (m2 / (world * M) - full.var(0, unbiased=False)).abs().max().item() / full.var(0).max().item())
+
+
+def test_syncbn_exchange_gloo():
+    out = run_world(_bnsync_case)
+    assert all(v < 1e-6 for v in out.values()), out

@@ -347,6 +347,11 @@ struct BnArgs {
   int M, C, R, rows_per, act, out_dt, res_dt, training;
   float eps, momentum;
   DropDesc drop;
+  // SyncBatchNorm exchange (tt2_batchnorm_{fwd,bwd}_{stats,apply}): [W][2][C] rank slots
+  // (this rank's moments or sums, zeros in the others; all-reduced by the caller) + [2][C]
+  float* sync;
+  int W, rank;
+  int64_t Mtot;   // rows behind the statistics: M, or W * M once exchanged
 };
 
 // tanh through one v_exp_f32 and one v_rcp_f32 (ocml's tanhf is a long branchy sequence and
@@ -475,6 +480,13 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
   if (g != 0 || !ok) return;
   double m2 = 0.0;
   for (int k = 0; k < BNF_GROUPS; ++k) m2 += red[k][cl];
+  if (a.sync) {   // this rank's (mean, M2) into its slot; the other ranks' slots zero
+    for (int r2 = 0; r2 < a.W; ++r2) {
+      a.sync[((int64_t)r2 * 2 + 0) * a.C + c] = r2 == a.rank ? (float)mu : 0.f;
+      a.sync[((int64_t)r2 * 2 + 1) * a.C + c] = r2 == a.rank ? (float)m2 : 0.f;
+    }
+    return;
+  }
   const double n = a.M;
   const double var = m2 / n;
   a.mean[c] = (float)mu;
@@ -484,6 +496,44 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
     a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mu);
     a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
   }
+}
+
+// SyncBatchNorm: combine the W exchanged rank moments (M rows each) in rank order, exactly
+// as bn_finalize_kernel combines chunks: mean = sum mean_r / W, M2 = sum M2_r + M (mean_r - mean)^2
+__global__ __launch_bounds__(NT) void bn_sync_finalize_kernel(BnArgs a) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= a.C) return;
+  double mu = 0.0;
+  for (int r = 0; r < a.W; ++r) mu += (double)a.sync[((int64_t)r * 2 + 0) * a.C + c];
+  mu /= a.W;
+  double m2 = 0.0;
+  for (int r = 0; r < a.W; ++r) {
+    const double d = (double)a.sync[((int64_t)r * 2 + 0) * a.C + c] - mu;
+    m2 += (double)a.sync[((int64_t)r * 2 + 1) * a.C + c] + (double)a.M * d * d;
+  }
+  const double n = (double)a.Mtot;
+  const double var = m2 / n;
+  a.mean[c] = (float)mu;
+  a.rstd[c] = (float)(1.0 / sqrt(var + a.eps));
+  if (a.run_mean) {
+    const double unb = n > 1 ? m2 / (n - 1) : var;
+    a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mu);
+    a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
+  }
+}
+
+// SyncBatchNorm backward: the global column sums (sum dpre, sum dpre * xhat) from the W
+// exchanged rank slots, in rank order, into the [2][C] region after the slots
+__global__ __launch_bounds__(NT) void bn_bwd_sync_kernel(BnArgs a) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= a.C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int r = 0; r < a.W; ++r) {
+    s1 += a.sync[((int64_t)r * 2 + 0) * a.C + c];
+    s2 += a.sync[((int64_t)r * 2 + 1) * a.C + c];
+  }
+  a.sync[((int64_t)a.W * 2 + 0) * a.C + c] = s1;
+  a.sync[((int64_t)a.W * 2 + 1) * a.C + c] = s2;
 }
 
 // per-column constants of 8 consecutive columns
@@ -605,8 +655,14 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(BnArgs a) {
   if (g != 0 || c >= a.C) return;
   float t1 = 0.f, t2 = 0.f;
   for (int k = 0; k < BNF_GROUPS; ++k) { t1 += red[0][k][cl]; t2 += red[1][k][cl]; }
-  a.dbeta[c] = t1;
+  a.dbeta[c] = t1;    // this rank's parameter gradients (the DP all-reduce sums them)
   a.dgamma[c] = t2;
+  if (a.sync) {
+    for (int r2 = 0; r2 < a.W; ++r2) {
+      a.sync[((int64_t)r2 * 2 + 0) * a.C + c] = r2 == a.rank ? t1 : 0.f;
+      a.sync[((int64_t)r2 * 2 + 1) * a.C + c] = r2 == a.rank ? t2 : 0.f;
+    }
+  }
 }
 
 template <typename T, typename TD>
@@ -616,7 +672,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
   const T* y = reinterpret_cast<const T*>(a.y);
   const TD* dout = reinterpret_cast<const TD*>(a.dout);
   const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
-  const float invM = 1.f / a.M;
+  const float invM = 1.f / (float)a.Mtot;
   for (int q = blockIdx.x * NT + threadIdx.x; q < nq; q += gridDim.x * NT) {
     const int m = q / CG, c0 = (q - m * CG) * 8;
     const int64_t i0 = (int64_t)m * a.C + c0;
@@ -760,6 +816,8 @@ static BnArgs bn_args(const tt2_bn_args* p) {
   a.rows_per = bn_rows_per(p->m);
   a.R = (p->m + a.rows_per - 1) / a.rows_per;
   a.drop = DropDesc{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
+  a.W = 1;
+  a.Mtot = p->m;
   return a;
 }
 
@@ -818,3 +876,86 @@ extern "C" int tt2_batchnorm_bwd(const tt2_bn_args* p, hipStream_t s) {
 #undef TT2_BN_DISPATCH
   return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_bwd");
 }
+
+// ------------------------------------------------------------ SyncBatchNorm phases
+// The caller SUM-all-reduces the first W * 2 * C floats of sync_buf between the phases
+// (tt2/dist.py BnSync: RCCL in the captured step, or torch.distributed).  Every rank then
+// holds the same slots and computes the same global statistics in the same order.
+extern "C" size_t tt2_batchnorm_sync_size(const tt2_bn_args* p) {
+  const int w = p->sync_world > 0 ? p->sync_world : 1;
+  return (size_t)(w + 1) * 2 * p->c * sizeof(float);
+}
+
+static int bn_sync_check(const tt2_bn_args* p, const char* what) {
+  if (bn_check(p, what)) return TT2_E_INVALID;
+  if (!p->training || p->sync_world < 1 || p->sync_rank < 0 || p->sync_rank >= p->sync_world || !p->sync_buf ||
+      (reinterpret_cast<uintptr_t>(p->sync_buf) & 15) || !p->workspace ||
+      p->ws_bytes < tt2_batchnorm_workspace_size(p))
+    return tt2_set_error(TT2_E_INVALID, what);
+  return TT2_OK;
+}
+
+static BnArgs bn_sync_args(const tt2_bn_args* p) {
+  BnArgs a = bn_args(p);
+  a.sync = p->sync_buf;
+  a.W = p->sync_world;
+  a.rank = p->sync_rank;
+  a.Mtot = (int64_t)p->sync_world * p->m;
+  return a;
+}
+
+extern "C" int tt2_batchnorm_fwd_stats(const tt2_bn_args* p, hipStream_t s) {
+  if (p->m <= 0) return tt2_set_error(TT2_E_INVALID, "tt2_batchnorm_fwd_stats: m must be > 0");
+  if (bn_sync_check(p, "tt2_batchnorm_fwd_stats: training, 1 <= sync_world, 0 <= sync_rank < sync_world, "
+                       "16-B aligned sync_buf, workspace and the tt2_batchnorm_fwd layout rules required"))
+    return TT2_E_INVALID;
+  const BnArgs a = bn_sync_args(p);
+  if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(bn_stats_kernel<bf16>, dim3(a.R), dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(a.R), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
+  return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_fwd_stats");
+}
+
+extern "C" int tt2_batchnorm_fwd_apply(const tt2_bn_args* p, hipStream_t s) {
+  if (p->m <= 0) return tt2_set_error(TT2_E_INVALID, "tt2_batchnorm_fwd_apply: m must be > 0");
+  if (bn_sync_check(p, "tt2_batchnorm_fwd_apply: the tt2_batchnorm_fwd_stats arguments required"))
+    return TT2_E_INVALID;
+  const BnArgs a = bn_sync_args(p);
+  hipLaunchKernelGGL(bn_sync_finalize_kernel, dim3((p->c + NT - 1) / NT), dim3(NT), 0, s, a);
+  const int g = grid_for((int64_t)p->m * p->c / 8);
+  if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(g), dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(g), dim3(NT), 0, s, a);
+  return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_fwd_apply");
+}
+
+#define TT2_BN_DISPATCH2(KER, grid, args)                                                       \
+  if (bf && dbf) hipLaunchKernelGGL((KER<bf16, bf16>), grid, dim3(NT), 0, s, args);             \
+  else if (bf) hipLaunchKernelGGL((KER<bf16, float>), grid, dim3(NT), 0, s, args);              \
+  else if (dbf) hipLaunchKernelGGL((KER<float, bf16>), grid, dim3(NT), 0, s, args);             \
+  else hipLaunchKernelGGL((KER<float, float>), grid, dim3(NT), 0, s, args);
+
+extern "C" int tt2_batchnorm_bwd_stats(const tt2_bn_args* p, hipStream_t s) {
+  if (p->m <= 0) return tt2_set_error(TT2_E_INVALID, "tt2_batchnorm_bwd_stats: m must be > 0");
+  if (bn_sync_check(p, "tt2_batchnorm_bwd_stats: the tt2_batchnorm_fwd_stats arguments required"))
+    return TT2_E_INVALID;
+  const BnArgs a = bn_sync_args(p);
+  const bool bf = p->dtype == TT2_DT_BF16, dbf = p->dout_dtype == TT2_DT_BF16;
+  TT2_BN_DISPATCH2(bn_bwd_stats_kernel, dim3(a.R), a)
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
+  return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_bwd_stats");
+}
+
+extern "C" int tt2_batchnorm_bwd_apply(const tt2_bn_args* p, hipStream_t s) {
+  if (p->m <= 0) return tt2_set_error(TT2_E_INVALID, "tt2_batchnorm_bwd_apply: m must be > 0");
+  if (bn_sync_check(p, "tt2_batchnorm_bwd_apply: the tt2_batchnorm_fwd_stats arguments required"))
+    return TT2_E_INVALID;
+  BnArgs a = bn_sync_args(p);
+  hipLaunchKernelGGL(bn_bwd_sync_kernel, dim3((p->c + NT - 1) / NT), dim3(NT), 0, s, a);
+  a.dbeta = a.sync + (int64_t)a.W * 2 * a.C;   // the apply reads the global sums
+  a.dgamma = a.dbeta + a.C;
+  const bool bf = p->dtype == TT2_DT_BF16, dbf = p->dout_dtype == TT2_DT_BF16;
+  const int ga = grid_for((int64_t)p->m * p->c / 8);
+  TT2_BN_DISPATCH2(bn_bwd_apply_kernel, dim3(ga), a)
+  return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_bwd_apply");
+}
+#undef TT2_BN_DISPATCH2

@@ -179,6 +179,7 @@ class BnArgs(C.Structure):
         ("m", i32), ("c", i32), ("act", i32), ("dtype", i32), ("out_dtype", i32), ("res_dtype", i32),
         ("dout_dtype", i32), ("training", i32), ("eps", f32), ("momentum", f32),
         ("drop_site", u32), ("drop_thr", u32), ("drop_scale", f32),
+        ("sync_buf", vp), ("sync_world", i32), ("sync_rank", i32),
     ]
 
 
@@ -228,6 +229,11 @@ SIGNATURES.update({
     "tt2_batchnorm_workspace_size": ([P_(BnArgs)], sz),
     "tt2_batchnorm_fwd": ([P_(BnArgs), vp], C.c_int),
     "tt2_batchnorm_bwd": ([P_(BnArgs), vp], C.c_int),
+    "tt2_batchnorm_sync_size": ([P_(BnArgs)], sz),
+    "tt2_batchnorm_fwd_stats": ([P_(BnArgs), vp], C.c_int),
+    "tt2_batchnorm_fwd_apply": ([P_(BnArgs), vp], C.c_int),
+    "tt2_batchnorm_bwd_stats": ([P_(BnArgs), vp], C.c_int),
+    "tt2_batchnorm_bwd_apply": ([P_(BnArgs), vp], C.c_int),
     "tt2_embedding_fwd": ([vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp], C.c_int),
     "tt2_embedding_bwd": ([vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp], C.c_int),
     "tt2_posenc_fwd": ([P_(PeArgs), vp], C.c_int),

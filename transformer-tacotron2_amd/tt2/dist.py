@@ -187,6 +187,41 @@ class RcclGradSync(GradSync):
             self.comm = C.c_void_p()
 
 
+class BnSync:
+    """SyncBatchNorm exchange (SURVEY.md:219, optional; per-replica statistics stay the
+    default).  Each BatchNorm's forward moments and backward column sums leave the kernels as
+    [world][2][C] rank slots (this rank's values, zeros elsewhere: exact and rank-ordered once
+    summed), and ``exchange`` SUM-all-reduces them between the two kernel phases
+    (ops.batchnorm_fwd / _bwd with ``sync=``).  With libtt2's RCCL communicator the all-reduce
+    is issued on the current stream, so it is captured with the step (``in_graph``); with gloo
+    it is a blocking torch.distributed all-reduce, for eager steps only."""
+    C_MAX = 2048   # tt2_batchnorm's channel limit
+
+    def __init__(self, world: int, rank: int, group=None, comm=None, device="cuda"):
+        self.world, self.rank, self.group, self.comm = world, rank, group, comm
+        self.in_graph = comm is not None
+        # one buffer serves every BatchNorm: stats -> exchange -> apply run in stream order
+        self._buf = torch.zeros((world + 1) * 2 * self.C_MAX, dtype=torch.float32, device=device)
+
+    def buffer(self, nbytes: int) -> torch.Tensor:
+        n = (nbytes + 3) // 4
+        if n > self._buf.numel():
+            raise ValueError(f"BnSync: {nbytes} B exchange buffer requested, {self._buf.numel() * 4} B held")
+        return self._buf[:n]
+
+    def exchange(self, slots: torch.Tensor):
+        if self.world == 1:
+            return
+        if self.comm is not None:
+            from . import _lib
+            L = _lib.lib()
+            _lib.check(L.tt2_allreduce_bucket(C.c_void_p(slots.data_ptr()), slots.numel(), _lib.dt(slots), self.comm,
+                                              C.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                       "tt2_allreduce_bucket")
+        else:
+            dist.all_reduce(slots, op=dist.ReduceOp.SUM, group=self.group)
+
+
 def init_from_env(backend: str | None = None):
     """Initialise torch.distributed from torchrun's env (RANK, WORLD_SIZE,
     LOCAL_RANK, MASTER_ADDR/PORT).  Returns (rank, world, local_rank)."""
@@ -217,16 +252,22 @@ def sync_kind(group=None) -> str:
     return "segmented"
 
 
-def attach(model, group=None, bucket_bytes: int = 25 << 20, kind: str | None = None) -> GradSync:
+def attach(model, group=None, bucket_bytes: int = 25 << 20, kind: str | None = None,
+           sync_bn: bool = False) -> GradSync:
     """Wire a TransformerTTS for data parallelism: gradient pre-scaling and the
     bucket hook.  Returns the sync object whose finish() goes between backward and
-    the optimizer step (pass it as train_step(..., sync_grads=sync.finish))."""
+    the optimizer step (pass it as train_step(..., sync_grads=sync.finish)).
+    sync_bn: SyncBatchNorm (the encoder pre-net's and post-net's BatchNorms take their
+    training statistics over every rank's rows; BnSync)."""
     eng = model.engine
     kind = kind or sync_kind(group)
     cls = RcclGradSync if kind == "rccl" else GradSync
     sync = cls(eng.grads, bucket_bytes, group)
     eng.grad_scale = 1.0 / sync.world
     eng.grad_ready_hook = sync.ready
+    if sync_bn:
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        eng.bn_sync = BnSync(sync.world, rank, group, comm=sync.comm if kind == "rccl" else None, device=eng.dev)
     return sync
 
 

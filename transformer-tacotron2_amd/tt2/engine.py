@@ -224,6 +224,7 @@ class TTSEngine:
         self.dropout_enabled = True
         self.grad_scale = 1.0
         self.grad_ready_hook = None   # called as hook(flat_offset) during backward (DP bucketing)
+        self.bn_sync = None   # SyncBatchNorm exchange (tt2/dist.py BnSync), None: per-replica statistics
         self.opt = dict(lr=1.0, beta1=0.9, beta2=0.98, eps=1e-9, weight_decay=0.0, clip_norm=1.0, warmup=4000.0,
                         noam=True)
         self._init_defaults()
@@ -387,7 +388,7 @@ class TTSEngine:
             ops.batchnorm_fwd(y, self.P(f"enc.bn{i}.g"), self.P(f"enc.bn{i}.b"), A[f"ecv_mean{i}"],
                               A[f"ecv_rstd{i}"], self.S(f"enc.bn{i}.rm"), self.S(f"enc.bn{i}.rv"), A[f"ecv_o{i}"],
                               Me, d, ACT_RELU, tr, drop=self.drop(SITE_ENC_CONV + i, c.prenet_dropout),
-                              eps=c.bn_eps, momentum=c.bn_momentum, ws=self.ws)
+                              eps=c.bn_eps, momentum=c.bn_momentum, ws=self.ws, sync=self.bn_sync)
             x = A[f"ecv_o{i}"]
         self._lin(x, self.W("enc.proj.w"), A["eproj"], Me, d, d, bias=self.P("enc.proj.b"))
         ops.posenc_fwd(A["eproj"], self.P("enc.alpha"), self.pe, A["ex0"], Me, Tx,
@@ -485,7 +486,7 @@ class TTSEngine:
                               ACT_NONE if last else ACT_TANH, tr,
                               drop=self.drop(SITE_POSTNET + i, c.postnet_dropout),
                               res=res if last else None, res_ld=res_ld, eps=c.bn_eps, momentum=c.bn_momentum,
-                              ws=self.ws)
+                              ws=self.ws, sync=self.bn_sync)
             x = out
 
     # ------------------------------------------------------------ loss
@@ -522,7 +523,7 @@ class TTSEngine:
             ops.batchnorm_bwd(A[f"pcv_y{i}"], g, self.P(f"post.bn{i}.g"), self.P(f"post.bn{i}.b"),
                               A[f"pcv_mean{i}"], A[f"pcv_rstd{i}"], dyv, self.G(f"post.bn{i}.g"),
                               self.G(f"post.bn{i}.b"), Md, cout, ACT_NONE if last else ACT_TANH,
-                              drop=self.drop(SITE_POSTNET + i, c.postnet_dropout), ws=self.ws)
+                              drop=self.drop(SITE_POSTNET + i, c.postnet_dropout), ws=self.ws, sync=self.bn_sync)
             x_in = A[f"pcv_o{i - 1}"] if i > 0 else A["pin"]
             self._wgrad(dyv, x_in, self.G(f"post.conv{i}.w").view(cout, K * cin), cout, K * cin, Md, ldx=cin,
                         b_conv=(Ty, cin, pad), gb=self.G(f"post.conv{i}.b"))
@@ -673,7 +674,8 @@ class TTSEngine:
         for i in reversed(range(c.enc_conv_layers)):
             ops.batchnorm_bwd(A[f"ecv_y{i}"], gc, self.P(f"enc.bn{i}.g"), self.P(f"enc.bn{i}.b"), A[f"ecv_mean{i}"],
                               A[f"ecv_rstd{i}"], gdy, self.G(f"enc.bn{i}.g"), self.G(f"enc.bn{i}.b"), Me, d,
-                              ACT_RELU, drop=self.drop(SITE_ENC_CONV + i, c.prenet_dropout), ws=self.ws)
+                              ACT_RELU, drop=self.drop(SITE_ENC_CONV + i, c.prenet_dropout), ws=self.ws,
+                              sync=self.bn_sync)
             x_in = A[f"ecv_o{i - 1}"] if i > 0 else A["emb"]
             self._wgrad(gdy, x_in, self.G(f"enc.conv{i}.w").view(d, K * d), d, K * d, Me, ldx=d,
                         b_conv=(Tx, d, pad), gb=self.G(f"enc.conv{i}.b"))

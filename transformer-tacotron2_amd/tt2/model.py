@@ -362,6 +362,10 @@ class TransformerTTS(nn.Module):
         torch.cuda.CUDAGraph, which records our kernels on its capture stream).
         Returns a callable run(text, text_len, mel, mel_len) -> loss vector."""
         e = self.engine
+        if e.bn_sync is not None and not e.bn_sync.in_graph:
+            raise RuntimeError("capture_train_step: SyncBatchNorm over torch.distributed (gloo) exchanges "
+                               "inside the forward and backward and cannot be captured; use train_step, or "
+                               "the nccl backend (RCCL, captured)")
         if e.exp_avg is None:
             e.init_optimizer()
         A = e.arena(B, Tx, Ty)

@@ -373,8 +373,19 @@ def _bn(y, gamma, beta, mean, rstd, m, c, act, training, drop, eps, momentum, ws
     return a
 
 
+def _bn_sync_into(L, a, sync):
+    """SyncBatchNorm exchange buffer of `sync` (tt2/dist.py BnSync: world, rank, buffer(nbytes),
+    exchange(tensor)) into the args; returns the slot view that exchange() all-reduces."""
+    a.sync_world, a.sync_rank = sync.world, sync.rank
+    buf = sync.buffer(L.tt2_batchnorm_sync_size(C.byref(a)))
+    a.sync_buf = buf.data_ptr()
+    return buf[:sync.world * 2 * a.c]
+
+
 def batchnorm_fwd(y, gamma, beta, mean, rstd, run_mean, run_var, out, m, c, act, training, drop: Drop = NO_DROP,
-                  res=None, res_ld=0, eps=1e-5, momentum=0.1, ws: Workspace | None = None):
+                  res=None, res_ld=0, eps=1e-5, momentum=0.1, ws: Workspace | None = None, sync=None):
+    """sync (training only): SyncBatchNorm over the data-parallel ranks -- the statistics of
+    all ranks' rows (tt2_batchnorm_fwd_stats, exchange, tt2_batchnorm_fwd_apply)."""
     L = lib()
     a = _bn(y, gamma, beta, mean, rstd, m, c, act, training, drop, eps, momentum, ws)
     a.run_mean, a.run_var = ptr(run_mean), ptr(run_var)
@@ -382,18 +393,32 @@ def batchnorm_fwd(y, gamma, beta, mean, rstd, run_mean, run_var, out, m, c, act,
     a.res, a.res_dtype, a.res_ld = ptr(res), (dt(res) if res is not None else 0), res_ld
     buf = (ws or _WS).get(L.tt2_batchnorm_workspace_size(C.byref(a)))
     a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
-    check(L.tt2_batchnorm_fwd(C.byref(a), stream_ptr()), "tt2_batchnorm_fwd")
+    if sync is None or not training:
+        check(L.tt2_batchnorm_fwd(C.byref(a), stream_ptr()), "tt2_batchnorm_fwd")
+        return
+    slots = _bn_sync_into(L, a, sync)
+    check(L.tt2_batchnorm_fwd_stats(C.byref(a), stream_ptr()), "tt2_batchnorm_fwd_stats")
+    sync.exchange(slots)
+    check(L.tt2_batchnorm_fwd_apply(C.byref(a), stream_ptr()), "tt2_batchnorm_fwd_apply")
 
 
 def batchnorm_bwd(y, dout, gamma, beta, mean, rstd, dy, dgamma, dbeta, m, c, act, drop: Drop = NO_DROP,
-                  ws: Workspace | None = None):
+                  ws: Workspace | None = None, sync=None):
+    """sync: SyncBatchNorm backward (the column sums over all ranks' rows; dgamma / dbeta
+    stay this rank's sums for the gradient all-reduce)."""
     L = lib()
     a = _bn(y, gamma, beta, mean, rstd, m, c, act, True, drop, 1e-5, 0.1, ws)
     a.dout, a.dout_dtype, a.dy = dout.data_ptr(), dt(dout), dy.data_ptr()
     a.dgamma, a.dbeta = dgamma.data_ptr(), dbeta.data_ptr()
     buf = (ws or _WS).get(L.tt2_batchnorm_workspace_size(C.byref(a)))
     a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
-    check(L.tt2_batchnorm_bwd(C.byref(a), stream_ptr()), "tt2_batchnorm_bwd")
+    if sync is None:
+        check(L.tt2_batchnorm_bwd(C.byref(a), stream_ptr()), "tt2_batchnorm_bwd")
+        return
+    slots = _bn_sync_into(L, a, sync)
+    check(L.tt2_batchnorm_bwd_stats(C.byref(a), stream_ptr()), "tt2_batchnorm_bwd_stats")
+    sync.exchange(slots)
+    check(L.tt2_batchnorm_bwd_apply(C.byref(a), stream_ptr()), "tt2_batchnorm_bwd_apply")
 
 
 def embedding_fwd(ids, table, out, m, vocab):
