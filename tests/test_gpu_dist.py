@@ -143,3 +143,35 @@ def test_buckets_final_when_launched_cfg2(nccl_group, bucket_mb, cls):
         run(text, tl, mel, ml)
     torch.cuda.synchronize()
     assert sync.steps == 4 and sync.bad == [], f"captured: buckets written after launch {sync.bad}"
+
+
+def test_syncbn_rccl_exchange_in_graph_one_rank(nccl_group):
+    """SyncBatchNorm over libtt2's RCCL communicator (attach(sync_bn=True), nccl): the 16
+    BatchNorm exchanges per step are captured in the one step graph with the bucket
+    all-reduces; with one rank the exchange is the identity, so the step follows the plain
+    one up to the slot's f32 rounding of M2 (no host sync anywhere: replays only)."""
+    g = torch.Generator().manual_seed(4)
+    B, Tx, Ty = 2, 24, 48
+    text = torch.randint(1, 80, (B, Tx), generator=g).cuda()
+    tl = torch.tensor([24, 19]).cuda()
+    mel = torch.randn(B, Ty, 80, generator=g).cuda()
+    ml = torch.tensor([48, 33]).cuda()
+    ref, dp = _model(), _model()
+    sync = attach(dp, kind="rccl", sync_bn=True)
+    assert dp.engine.bn_sync is not None and dp.engine.bn_sync.in_graph
+    for _ in range(2):
+        ref.train_step(text, tl, mel, ml)
+        dp.train_step(text, tl, mel, ml, sync_grads=sync.finish)
+    run_ref = ref.capture_train_step(B, Tx, Ty)
+    run_dp = dp.capture_train_step(B, Tx, Ty, sync_grads=sync.finish)
+    segs, g2 = dp._graphs[(B, Tx, Ty)]
+    assert g2 is None and len(segs) == 1
+    for _ in range(3):
+        la = run_ref(text, tl, mel, ml).clone()
+        lb = run_dp(text, tl, mel, ml).clone()
+        assert ((la - lb).abs() <= 1e-3 * la.abs() + 1e-5).all(), (la, lb)
+    torch.cuda.synchronize()
+    d = (ref.engine.params - dp.engine.params).abs().max().item()
+    assert d < 1e-3, d
+    assert torch.allclose(ref.engine.stats, dp.engine.stats, rtol=1e-3, atol=1e-5)
+    sync.close()
