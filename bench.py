@@ -234,6 +234,8 @@ def gemm_kernel_name(plan: int, ta: int, tb: int) -> str:
         return f"gemm7_kernel<{ak}, {bk}>"
     if plan == 15:
         return f"gemm8_kernel<{bk}>"
+    if plan == 16:
+        return "gemm10_kernel"
     if plan == 1:
         return "gemm_kernel"
     return f"gemm plan {plan}"

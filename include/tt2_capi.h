@@ -70,7 +70,9 @@ typedef struct tt2_gemm_args {
   int32_t kernel_variant;  /* 0 auto, 1 register-staged (any shape), 2 LDS-DMA 128x128 (bf16, 8-aligned inner
                               dims), 13 / 14 warp-specialised 256x128 (same, conv C, T >= 64; the auto choice
                               when eligible) with its register / LDS-image epilogue (auto: LDS image),
-                              15 64x64 (K-contiguous A; auto for <= 64 v7 tiles) */
+                              15 64x64 (K-contiguous A; auto for <= 64 v7 tiles), 16 256x256 (NT, bf16 C,
+                              N % 256 == 0, K % 64 == 0, bias / ReLU / dropout epilogues only; auto when
+                              its rounds of the chip cost less than v7's) */
   /* optional fused row sums of op(A) over k: a_ksum[m] = a_ksum_beta * a_ksum[m] + sum_k A(m, k)
    * (f32).  With A = dY^T of a weight-gradient GEMM this is the bias gradient, taken from the
    * A tiles already staged in LDS.  Requires bf16, trans_a, no conv on A. */

@@ -1,0 +1,60 @@
+"""tt2_gemm_plan's kernel choice (host logic, CPU: the plan reads only sizes, flags and pointer
+alignment): v10 (16) takes the NT products whose 256 x 256 tiles' rounds of the chip cost
+less than v7's (the decoder FFN1 forward, the memory K/V projection), v7 (13) the N = 512 and
+dgrad / residual / split products, v8 (15) the small ones; explicit variants win."""
+import ctypes as C
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "transformer-tacotron2_amd"))
+from tt2 import _lib  # noqa: E402
+from tt2._lib import ACT_RELU, ACT_TANH, DT_BF16  # noqa: E402
+
+_A = torch.empty(64, dtype=torch.bfloat16)
+_C = torch.empty(64, dtype=torch.bfloat16)
+_BIAS = torch.empty(16, dtype=torch.float32)
+_L = C.CDLL(_lib.LIB_PATH)   # the plan is host code: no HIP device needed
+_L.tt2_gemm_plan.argtypes = [C.POINTER(_lib.GemmArgs)]
+_L.tt2_gemm_plan.restype = C.c_int
+
+
+def plan(m, n, k, trans_a=False, trans_b=False, bias=None, res=None, ldr=0, act=0, beta=0.0, splits=1,
+         variant=0):
+    g = _lib.GemmArgs()
+    g.a, g.b, g.c = _A.data_ptr(), _A.data_ptr(), _C.data_ptr()
+    g.bias = bias.data_ptr() if bias is not None else None
+    g.res, g.ldr, g.res_dtype = (res.data_ptr(), ldr, DT_BF16) if res is not None else (None, 0, 0)
+    g.m, g.n, g.k = m, n, k
+    g.lda, g.ldb, g.ldc = m if trans_a else k, n if trans_b else k, n
+    g.dtype_in = g.dtype_out = DT_BF16
+    g.trans_a, g.trans_b = int(trans_a), int(trans_b)
+    g.act, g.alpha, g.beta = act, 1.0, beta
+    g.splits, g.kernel_variant = splits, variant
+    return _L.tt2_gemm_plan(C.byref(g))
+
+
+def test_v10_takes_the_wide_forward_products():
+    assert plan(12800, 2048, 512, bias=_BIAS, act=ACT_RELU) == 16   # FFN1 forward: 2 rounds vs 4
+    assert plan(2048, 6144, 512, bias=_BIAS) == 16                  # memory K/V: 1 round vs 2
+    assert plan(8192, 8192, 8192) == 16
+
+
+def test_v7_and_v8_keep_the_rest():
+    assert plan(12800, 512, 512, bias=_BIAS) == 13                  # 200 vs 100 tiles: one round either way
+    assert plan(12800, 512, 2048) == 13
+    assert plan(12800, 1536, 512, bias=_BIAS) == 13                 # QKV: 2 v10 rounds cost more than 3 of v7
+    assert plan(12800, 2048, 512, trans_b=True) == 13               # dgrad (N-contiguous B)
+    assert plan(12800, 2048, 512, res=_C, ldr=2048) == 13           # residual epilogue
+    assert plan(12800, 2048, 512, act=ACT_TANH) == 13
+    assert plan(12800, 2048, 512, beta=1.0) == 13
+    assert plan(512, 2048, 12800, trans_a=True, splits=2) == 13     # weight gradient
+    assert plan(12800, 2040, 512) == 13                             # N % 256 != 0
+    assert plan(2048, 512, 512) == 15                               # <= 64 v7 tiles: v8
+
+
+def test_explicit_variants():
+    assert plan(12800, 2048, 512, variant=13) == 13
+    assert plan(12800, 512, 512, variant=16) == 16
+    assert plan(12800, 2048, 512, trans_b=True, variant=16) != 16   # v10 is NT only

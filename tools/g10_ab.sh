@@ -1,5 +1,5 @@
 #!/bin/bash
-# v10 A/B (v10 lives in commit 103f89b; check it out to rerun): correctness tests, per-shape auto vs variant 16, then the bench step with v10 auto on/off
+# v10 A/B (forced variant 16 vs auto; step with the v10 route built on / off via TT2_G10_AUTO): correctness tests, per-shape auto vs variant 16, then the bench step with v10 auto on/off
 set -e
 OUT=gpurun_out/g10; mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_gemm10.py > $OUT/tests.log 2>&1

@@ -968,6 +968,9 @@ TT2_DEV void g7_frag(Frag8<bf16>& f, const char* img, int r0, int kk, int lane) 
 // ksum (row sums of an M-contiguous A): the wn == 0 waves multiply their A fragments by an
 // all-ones fragment (one extra MFMA each).
 // =====================================================================================
+#ifndef TT2_G10_AUTO
+#define TT2_G10_AUTO 1
+#endif
 constexpr int G7_NT = 768;                          // 8 MFMA waves + 4 loader waves
 constexpr int G7_A = 256 * 128, G7_B = 128 * 128;   // bytes per stage: 64 k x 2 B per row
 constexpr int G7_STAGE = G7_A + G7_B;               // 48 KB
@@ -1746,6 +1749,202 @@ hipError_t launch8(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
 }
 
 
+// =====================================================================================
+// v10 (bf16, NT: A and B K-contiguous): 256 x 256 tile for the wide forward products.  v7's
+// K loop is bound by how fast its loader waves fill LDS (48 KB per 256 x 128 x 64 step against
+// 1,024 MFMA cycles); a 256 x 256 tile stages 64 KB for twice the MFMA work.  768 threads as
+// v7: 8 MFMA waves (2 M x 4 N, 128 x 64 each: 128 accumulators per lane, the bias loaded after
+// the K loop to stay within 168 VGPRs) and 4 loader waves.  The ring is 5 slots of one
+// operand's 64-deep tile (32 KB: all 160 KB of LDS), filled in the order A_0 B_0 A_1 B_1 A_2
+// ...: after the barrier that ends step t - 1 its two slots take B_{t+1} and A_{t+2}, so the
+// activation operand (cold: just written by the previous kernel) is issued two steps ahead and
+// the weight operand (L2-resident) one step ahead.  Images, swizzles and fragment reads are
+// v7's; the epilogue is v7's straight-line form into an LDS C image of two 128-column halves.
+// =====================================================================================
+constexpr int G10_NT = 768;
+constexpr int G10_SLOT = 256 * 128;              // one operand's 64-deep tile: 256 rows x 128 B
+constexpr int G10_SLOTS = 5;
+constexpr int G10_SMEM = G10_SLOTS * G10_SLOT;   // 160 KB: the whole LDS
+
+TT2_DEV int g10_img(int r, int cl) {
+  return (cl >> 7) * 65536 + r * 256 + ((((cl >> 3) & 15) ^ (r & 15)) << 4);
+}
+
+TT2_DEV void g10_wait(int n) {   // s_waitcnt vmcnt(n), n a multiple of 8 (one item per loader wave)
+  if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int CODE>   // g7_fast_code: bit 0 bias, bit 1 ReLU, bit 2 dropout
+__global__ __launch_bounds__(G10_NT, 1) void gemm10_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
+                                                           int ntn, int items, unsigned long long* span) {
+  constexpr bool BIAS = CODE & 1, RELU = CODE & 2, DROP = CODE & 4;
+  __shared__ __attribute__((aligned(1024))) char smem[G10_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (span && tid == 0) span[2 * blockIdx.x] = wall_clock64();
+  const int tile = xcd_item(blockIdx.x, items);
+  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
+  const int nkt = K / 64, nit = 2 * nkt;   // ring items: A_t = 2 t, B_t = 2 t + 1
+  if (wave >= 8) {   // ------------------------------------------------ loader waves
+    const int lw = wave - 8;
+    G7Lane<8> la, lb;   // 8 of each operand tile's 32 copies
+    g7_lane_init<true>(la, A, m0, 0, lane, lw);
+    g7_lane_init<true>(lb, B, n0, 0, lane, lw);
+    auto issue = [&](int it) {
+      char* dst = smem + (it % G10_SLOTS) * G10_SLOT;
+      if (it & 1) g7_issue<true>(B, lb, dst, 64 * (it >> 1), K, lane, lw, false, false);
+      else g7_issue<true>(A, la, dst, 64 * (it >> 1), K, lane, lw, false, false);
+    };
+    const int pre = min(G10_SLOTS, nit);
+    for (int it = 0; it < pre; ++it) issue(it);
+    g10_wait(8 * (pre - 2));   // A_0, B_0 landed
+    __builtin_amdgcn_s_barrier();
+    for (int t = 0; t < nkt; ++t) {
+      if (t >= 1) {   // the slots step t - 1 read: B_{t+1}, A_{t+2}
+        if (2 * t + 3 < nit) issue(2 * t + 3);
+        if (2 * t + 4 < nit) issue(2 * t + 4);
+      }
+      if (t + 1 < nkt) {   // B_{t+1} landed: only A_{t+2}, issued after it, may stay in flight
+        const int last = min(nit - 1, max(G10_SLOTS - 1, 2 * t + 4));
+        g10_wait(8 * (last - (2 * t + 3)));
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {   // ------------------------------------------------------- MFMA waves
+    const int wm = wave >> 2, wn = wave & 3, q = lane >> 4;
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint32_t seed = DROP ? *E.drop.seed : 0u;
+    const int gps = (16 + nkt - 1) / nkt;   // keep-bit groups (16-row block i, column pair pr) per K step
+    uint64_t dbits[2] = {0, 0};
+    __builtin_amdgcn_s_barrier();
+    for (int t = 0; t < nkt; ++t) {
+      const char* sa = smem + ((2 * t) % G10_SLOTS) * G10_SLOT;
+      const char* sb = smem + ((2 * t + 1) % G10_SLOTS) * G10_SLOT;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        Frag8<bf16> fb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g7_frag<true>(fb[j], sb, wn * 64 + 16 * j, kk, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          Frag8<bf16> fa;
+          g7_frag<true>(fa, sa, wm * 128 + 16 * i, kk, lane);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) mma16(fb[j], fa, acc[i][j]);   // D[n][m]
+        }
+      }
+      if (DROP) {   // VALU work beside this step's MFMAs
+        const int g1 = min(16, (t + 1) * gps);
+        for (int gi = t * gps; gi < g1; ++gi) {
+          const int m = m0 + wm * 128 + 16 * (gi >> 1) + (lane & 15);
+          const int n = n0 + wn * 64 + 16 * (2 * (gi & 1) + (q & 1)) + 8 * (q >> 1);
+          const uint64_t kb = drop_bits8(seed, E.drop.site, (uint32_t)((int64_t)m * E.n_log + n), E.drop.thr);
+          dbits[gi >> 3] |= kb << (8 * (gi & 7));
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this step's reads retired (WAR vs its slots)
+      __builtin_amdgcn_s_barrier();
+    }
+    // epilogue: alpha, bias, ReLU, dropout (v7's order) into the C image (the ring is free)
+    f32x4 pbias[2][2];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int n = n0 + wn * 64 + 16 * (2 * pr + (q & 1)) + 8 * (q >> 1);
+      pbias[pr][0] = pbias[pr][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (BIAS) {
+        pbias[pr][0] = *reinterpret_cast<const f32x4*>(E.bias + n);
+        pbias[pr][1] = *reinterpret_cast<const f32x4*>(E.bias + n + 4);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = wm * 128 + 16 * i + (lane & 15);
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        float v[8];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * pr][rr]),
+                                                           __float_as_uint(acc[i][2 * pr + 1][rr]), false, false);
+          v[rr] = __uint_as_float(sw[0]);
+          v[4 + rr] = __uint_as_float(sw[1]);
+        }
+        const int cl = wn * 64 + 16 * (2 * pr + (q & 1)) + 8 * (q >> 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = BIAS ? v[j] * E.alpha + pbias[pr][0][j] : v[j] * E.alpha;
+          v[4 + j] = BIAS ? v[4 + j] * E.alpha + pbias[pr][1][j] : v[4 + j] * E.alpha;
+        }
+        if (RELU) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+        }
+        if (DROP) {
+          const int gi = 2 * i + pr;
+          const uint32_t kb = (uint32_t)(dbits[gi >> 3] >> (8 * (gi & 7)));
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (kb >> j) & 1u ? v[j] * E.drop.scale : 0.f;
+        }
+        bf16x8 x;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = (bf16)v[j];
+        *reinterpret_cast<bf16x8*>(smem + g10_img(r, cl)) = x;
+      }
+    }
+  }
+  __syncthreads();   // the C image is complete: all 12 waves store whole 256-B row segments
+  bf16* C = reinterpret_cast<bf16*>(E.c);
+  for (int id = tid; id < 256 * 32; id += G10_NT) {
+    const int half = id >> 12, r = (id >> 4) & 255, c = id & 15;
+    const int mm = m0 + r, nn = n0 + half * 128 + 8 * c;
+    if (mm < M)   // nontemporal, as v7's C
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(smem + half * 65536 + r * 256 + ((c ^ (r & 15)) << 4)),
+                                  reinterpret_cast<u32x4*>(C + (int64_t)mm * E.ldc + nn));
+  }
+  if (span) {   // every wave's stores completed, then one end stamp
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) span[2 * blockIdx.x + 1] = wall_clock64();
+  }
+}
+
+hipError_t launch10(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int code,
+                    hipStream_t s) {
+  const int ntn = N / 256, items = ((M + 255) / 256) * ntn;
+  ProbeScope ps(s, items);
+#define TT2_G10(C_)                                                                                               \
+  case C_:                                                                                                        \
+    if (ps.ext())                                                                                                 \
+      hipExtLaunchKernelGGL((gemm10_kernel<C_>), dim3(items), dim3(G10_NT), 0, s, ps.e0, ps.e1, 0, A, B, E, M, N, \
+                            K, ntn, items, ps.span);                                                              \
+    else                                                                                                          \
+      hipLaunchKernelGGL((gemm10_kernel<C_>), dim3(items), dim3(G10_NT), 0, s, A, B, E, M, N, K, ntn, items,       \
+                         ps.span);                                                                                \
+    break;
+  switch (code) {
+    TT2_G10(0) TT2_G10(1) TT2_G10(2) TT2_G10(3) TT2_G10(4) TT2_G10(5) TT2_G10(6) TT2_G10(7)
+    default: return hipErrorInvalidValue;
+  }
+#undef TT2_G10
+  return hipGetLastError();
+}
+
+// v10's epilogue code for this launch, or -1: bf16 C on 16-B rows, no beta / residual / gate /
+// tanh / k-sums (g7_fast_code's forward option sets)
+int g10_code(const EpiParams& E) {
+  if (E.c_dt != TT2_BF16 || !E.vec || E.beta != 0.f || E.act == ACT_TANH || E.res || E.gate || E.ksum) return -1;
+  return (E.bias ? 1 : 0) | (E.act == ACT_RELU ? 2 : 0) | (E.drop.thr ? 4 : 0);
+}
+
+
+
+
 }  // namespace
 
 extern "C" size_t tt2_gemm_workspace_size(const tt2_gemm_args* a) {
@@ -1759,7 +1958,8 @@ static bool g7_lds_epi(int variant) { return variant != 13; }
 
 // Kernel selection (also exported as tt2_gemm_plan): 1 v1 register-staged, 2 v2
 // LDS-DMA 128^2, 3 skinny (M <= 64), 13 v7 warp-specialised 256x128 (auto; variant 14
-// forces its LDS-image epilogue, 13 its register epilogue), 15 v8 64x64.  Returns -1 (error set) for an unsupported fusion request.
+// forces its LDS-image epilogue, 13 its register epilogue), 15 v8 64x64, 16 v10 256x256 NT.
+// Returns -1 (error set) for an unsupported fusion request.
 static int gemm_plan(const tt2_gemm_args* a) {
   const int var = a->kernel_variant;
   const int64_t a_inner = a->trans_a ? a->m : a->k, b_inner = a->trans_b ? a->n : a->k;
@@ -1813,6 +2013,19 @@ static int gemm_plan(const tt2_gemm_args* a) {
   // the post-net's 80-channel conv): 1.4-1.6x v7 there, slower once v7 has >= 96 tiles
   const int64_t tiles7 = (int64_t)((a->m + 255) / 256) * ((a->n + 127) / 128);
   if (v8ok && a->m >= 64 && (var == 15 || (var == 0 && tiles7 <= 64))) return 15;
+  // v10 (256 x 256, NT, bf16 C, K % 64 == 0, N % 256 == 0, no split / conv / k-sums; its epilogue
+  // options are checked at launch): forced by variant 16; auto for the wide products
+  const bool v10ok = v7ok && !a->trans_a && !a->trans_b && a->a_conv_t == 0 && !a->a_ksum &&
+                     a->dtype_out == TT2_BF16 && a->splits <= 1 && a->n % 256 == 0 && a->k % 64 == 0 &&
+                     !a->res && !a->gate && a->beta == 0.f && a->act != ACT_TANH &&
+                     reinterpret_cast<uintptr_t>(a->c) % 16 == 0 && a->ldc % 8 == 0 &&
+                     reinterpret_cast<uintptr_t>(a->bias) % 16 == 0;
+  // auto: when its rounds of the chip (one tile per CU) take less time than v7's, a v10 tile
+  // costing ~1.7 v7 tiles (in-step work-group spans, tools/gemm_wgt.py): the decoder FFN1
+  // forward (2 vs 4 rounds), the memory K/V projection (1 vs 2), large squares; not QKV (2 vs 3)
+  const int64_t cus = tt2_cu_count();
+  const int64_t rounds7 = (tiles7 + cus - 1) / cus, rounds10 = ((a->m + 255) / 256 * (a->n / 256) + cus - 1) / cus;
+  if (v10ok && (var == 16 || (var == 0 && TT2_G10_AUTO && 17 * rounds10 < 10 * rounds7))) return 16;
   if ((var == 13 || var == 14 || var == 0) && v7ok) return 13;
   return 2;
 }
@@ -1926,6 +2139,13 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
 #undef TT2_SK_M
 #undef TT2_SK
     return tt2_check_launch(hipGetLastError(), "tt2_gemm(skinny)");
+  }
+  if (plan == 16) {
+    const int code = g10_code(ep);
+    if (code >= 0) return tt2_check_launch(launch10(A, B, ep, a->m, a->n, a->k, code, stream), "tt2_gemm(v10)");
+    tt2_gemm_args b = *a;   // an epilogue v10 does not fuse (unaligned rows, ...): v7
+    b.kernel_variant = 13;
+    plan = gemm_plan(&b);
   }
   if (plan == 15) {
     if (!a->trans_b) err = launch8<true>(A, B, ep, a->m, a->n, a->k, stream);
