@@ -51,44 +51,14 @@ def test_full_length_fp32_parity():
     model.backward()
     gm = model.grads_state_dict()
     gnorm = torch.sqrt(sum((p.grad.double() ** 2).sum() for p in oracle.parameters() if p.grad is not None))
-    tol = {k: 1e-3 for k, _ in oracle.named_parameters()}
-    tol["decoder.pos.alpha"] = max(1e-3, 3 * alpha_sensitivity(text, tl, mel, ml, dict(oracle.named_parameters())["decoder.pos.alpha"].grad))
     bad = []
     for k, p in oracle.named_parameters():
         ref = p.grad if p.grad is not None else torch.zeros_like(p)
         if ref.double().norm() < 1e-6 * gnorm:
             continue      # conv biases in front of training-mode BatchNorm: analytically zero
-        if rel(gm[k], ref) >= tol[k]:
-            bad.append((k, rel(gm[k], ref), tol[k]))
+        if rel(gm[k], ref) >= 1e-3:
+            bad.append((k, rel(gm[k], ref)))
     assert not bad, bad
-
-
-def alpha_sensitivity(text, tl, mel, ml, ref):
-    """How far the f32 oracle's own decoder.pos.alpha gradient moves when only the rounding of
-    its BatchNorm statistics changes (computed in float64, cast back).  That gradient is a sum
-    over 1600 x 512 frame-channel terms that cancels to ~6e-4 (the encoder's is ~0.17), so
-    float32 rounding anywhere in the post-net moves it by ~3e-3 relative (measured on this batch:
-    3.1e-3), while every other gradient moves by <= 3e-5.  The engine's BatchNorm rounds
-    differently from torch's, so this one scalar is held to 3x the reference's own sensitivity."""
-    import torch.nn.functional as F
-    orig = F.batch_norm
-
-    def bn64(x, rm, rv, w=None, b=None, training=False, momentum=0.1, eps=1e-5):
-        c = (lambda t: None if t is None else t.double())
-        y = orig(x.double(), None if rm is None else rm.double().clone(), None if rv is None else rv.double().clone(),
-                 c(w), c(b), training, momentum, eps)
-        return y.to(x.dtype)
-
-    o = init_deterministic(TransformerTTSOracle(OracleConfig()), 21).train()
-    o.set_seed(99)
-    F.batch_norm = bn64
-    try:
-        ob, oa, os_, _ = o(text, tl, mel, ml)
-        lo, _ = o.loss((ob, oa, os_), mel, ml)
-        lo.backward()
-    finally:
-        F.batch_norm = orig
-    return rel(dict(o.named_parameters())["decoder.pos.alpha"].grad, ref)
 
 
 def test_full_length_bf16_forward():

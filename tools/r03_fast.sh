@@ -2,7 +2,7 @@
 # Quick GPU pass for a kernel change: the suites that exercise GEMM split-K, BatchNorm and the
 # bitwise graph-vs-eager step, then the default bench line and the timed-step kernel profile.
 set -euo pipefail
-TAG=${1:-r03x}
+TAG=${1:-r03u}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp

@@ -24,7 +24,6 @@
 
 #include <algorithm>
 #include <cstdlib>
-#include <mutex>
 #include <string>
 #include <vector>
 
@@ -69,52 +68,6 @@ int probe_take(hipEvent_t& e0, hipEvent_t& e1, unsigned long long*& span, int gr
   g_probe_armed = -1;
   return slot;
 }
-
-// Split-K tile counters (v7's in-kernel reduce, g7_fixup): the last of a tile's split work
-// groups to finish sums the tile's slabs in split order and applies the epilogue, so no
-// reduce launch follows the GEMM.  One zeroed pool per device, allocated outside any capture
-// (a launch captured before the pool exists keeps the reduce launch); each launch takes a
-// fresh region of one counter per tile, and the last arriver resets its counter, so a
-// captured launch replays on the same region.  Regions are handed out round-robin: two
-// launches share counters only if more than FIX_POOL tiles were launched between them, so
-// launches that run concurrently on different streams never do in practice.
-constexpr int64_t FIX_POOL = 1 << 20;
-constexpr int FIX_DEVS = 64;
-int* g_fix[FIX_DEVS] = {};
-int64_t g_fix_next[FIX_DEVS] = {};
-std::mutex g_fix_mu;
-
-int* fix_counters(int tiles, hipStream_t s) {
-  int dev = 0;
-  if (tiles <= 0 || tiles > FIX_POOL || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= FIX_DEVS)
-    return nullptr;
-  std::lock_guard<std::mutex> lk(g_fix_mu);
-  if (!g_fix[dev]) {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
-    int* p = nullptr;
-    if (hipMalloc(&p, FIX_POOL * sizeof(int)) != hipSuccess) {
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    if (hipMemsetAsync(p, 0, FIX_POOL * sizeof(int), s) != hipSuccess) {
-      (void)hipFree(p);
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    g_fix[dev] = p;
-  }
-  if (g_fix_next[dev] + tiles > FIX_POOL) g_fix_next[dev] = 0;
-  int* r = g_fix[dev] + g_fix_next[dev];
-  g_fix_next[dev] += tiles;
-  return r;
-}
-
-}  // namespace
-
-int* tt2_fix_counters(int n, hipStream_t s) { return fix_counters(n, s); }
-
-namespace {
 
 TT2_DEV void span_begin(unsigned long long* span, int* done) {
   if (span && threadIdx.x == 0) {
@@ -1134,7 +1087,6 @@ struct G7Prob {
   int pre_x;     // the loader waves stage the bf16 residual (1) or gate (2) tile in LDS (lds_epi only)
   int epi_fast;  // straight-line image epilogue for this option set (g7_epi_fast), -1: general path
   unsigned long long* span;   // launch probe's span record (grouped launch: p[0]'s), else null
-  int* fix;    // split-K: one counter per tile, the last split reduces in-kernel (g7_fixup); null: reduce launch
 };
 constexpr int G7_MAXP = 8;
 // A deferred LayerNorm backward's column-sum finalize (tt2_ln_args with defer_finalize) that
@@ -1247,54 +1199,6 @@ TT2_DEV void g7_epi_fast(const EpiParams& E, const f32x4 (&acc)[4][4], const f32
   }
 }
 
-// Split-K in-kernel reduce (P.fix): every wave of every split work group arrives here after
-// its slab stores.  The stores are released at agent scope (the tile's other splits run on
-// other XCDs, behind other L2s), one thread counts the arrival, and the work group that
-// completes the count acquires, sums the tile's [splits] slabs in split order and applies the
-// epilogue exactly as splitk_reduce_body's 8-wide path does (bitwise the same C), reduces the
-// tile rows' k-sum partials when this tile carries them, and resets the counter.  Nothing
-// waits on another work group, so the grid drains whatever the arrival order.
-TT2_DEV void g7_fixup(const G7Prob& P, int tile) {
-  __shared__ int last;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int* c = P.fix + tile;
-    const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == P.splits - 1;
-    if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const EpiParams& E = P.E;
-  const int M = P.M, N = P.N, m0 = (tile / P.ntn) * 256, n0 = (tile % P.ntn) * 128;
-  const int64_t total = (int64_t)M * N;
-  const uint32_t seed = E.drop.thr ? *E.drop.seed : 0u;
-  if (E.ksum && (tile % P.ntn) == 0) {
-    const float* kp = P.ws + P.splits * total;
-    for (int m = m0 + threadIdx.x; m < min(M, m0 + 256); m += G7_NT) {
-      float v = 0.f;
-      for (int z = 0; z < P.splits; ++z) v += kp[z * (int64_t)M + m];
-      E.ksum[m] = E.ksum_beta != 0.f ? E.ksum_beta * E.ksum[m] + v : v;
-    }
-  }
-  for (int id = threadIdx.x; id < 256 * 16; id += G7_NT) {
-    const int m = m0 + (id >> 4), n = n0 + 8 * (id & 15);
-    if (m >= M || n >= N) continue;
-    const int64_t i = ((int64_t)m * N + n) >> 3;
-    const f32x4* w0 = reinterpret_cast<const f32x4*>(P.ws) + 2 * i;
-    f32x4 lo = w0[0], hi = w0[1];
-    for (int z = 1; z < P.splits; ++z) {
-      const f32x4* wz = reinterpret_cast<const f32x4*>(P.ws + z * total) + 2 * i;
-      lo += wz[0];
-      hi += wz[1];
-    }
-    const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    epi_store8(E, seed, m, n, N, v);
-  }
-}
-
 template <bool AK, bool BKC>
 TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
   const OpDesc& A = P.A;
@@ -1349,10 +1253,7 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
-    if (!P.lds_epi) {
-      if (P.fix) g7_fixup(P, tile);   // the loader waves join the tile's reduce
-      return;
-    }
+    if (!P.lds_epi) return;
     __syncthreads();   // the MFMA waves' C image is in LDS
     g7_store_c(P, smem, m0, n0, nkt);
     return;
@@ -1548,7 +1449,6 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
       }
     }
   }
-  if (P.fix) g7_fixup(P, tile);
   G7_STAMP(nkt, 3)
 }
 
@@ -1612,7 +1512,7 @@ __global__ void gemm_splitk_reduce_g(G7Group G) {
     return;
   }
   const G7Prob& P = G.p[blockIdx.y];
-  if (P.splits > 1 && !P.fix) splitk_reduce_body(P.ws, P.splits, P.E, P.M, P.N, blockIdx.x, gridDim.x);
+  if (P.splits > 1) splitk_reduce_body(P.ws, P.splits, P.E, P.M, P.N, blockIdx.x, gridDim.x);
 }
 
 G7Prob g7_prob(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits,
@@ -1640,12 +1540,6 @@ int g7_fast_code(const G7Prob& P, bool fwd) {
   return (E.bias ? 1 : 0) | (E.act == ACT_RELU ? 2 : 0) | (E.drop.thr ? 4 : 0);
 }
 
-// the in-kernel split-K reduce covers splitk_reduce_body's 8-wide path: finished C wanted (no
-// raw slabs), N % 8 == 0 and vector epilogue access
-bool g7_fixup_ok(const G7Prob& P) {
-  return P.splits > 1 && !P.E.main_only && (P.N & 7) == 0 && P.E.vec;
-}
-
 template <bool AK, bool BKC>
 hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
                    hipStream_t s, bool lds_epi) {
@@ -1654,14 +1548,13 @@ hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   // the loader waves stage a bf16 residual / gate tile in LDS during the last K steps
   P.pre_x = !P.lds_epi ? 0 : (E.res && E.res_dt == TT2_BF16) ? 1 : (E.gate && E.gate_dt == TT2_BF16) ? 2 : 0;
   P.epi_fast = g7_fast_code(P, AK && BKC);
-  if (g7_fixup_ok(P)) P.fix = fix_counters(P.items / P.splits, s);
   ProbeScope ps(s, P.items);
   P.span = ps.span;
   if (ps.ext())
     hipExtLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, ps.e0, ps.e1, 0, P);
   else
     hipLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, P);
-  if (P.splits > 1 && !E.main_only && !P.fix)
+  if (P.splits > 1 && !E.main_only)
     hipLaunchKernelGGL(gemm_splitk_reduce, dim3(splitk_blocks(M, N, E)), dim3(256), 0, s, ws, P.splits, E, M, N);
   return hipGetLastError();
 }
@@ -2316,12 +2209,11 @@ extern "C" int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int n, const tt2
                        reinterpret_cast<float*>(a->workspace));
     P.item0 = G.items;
     G.items += P.items;
+    G.p[G.np++] = P;
     main_only &= a->main_only;
     if (P.splits > 1) {
-      if (g7_fixup_ok(P)) P.fix = fix_counters(P.items / P.splits, stream);
-      if (!P.fix) reduce_blocks = std::max(reduce_blocks, splitk_blocks(a->m, a->n, ep));
+      reduce_blocks = std::max(reduce_blocks, splitk_blocks(a->m, a->n, ep));
     }
-    G.p[G.np++] = P;
   }
   const int fin_blocks = G.fin.nb ? (3 * G.fin.C + G7_FIN_WAVES - 1) / G7_FIN_WAVES : 0;
   if (G.np == 0) {

@@ -16,8 +16,6 @@
 #include <math.h>
 #include <stdlib.h>
 
-#include <algorithm>
-
 #include "tt2_capi.h"
 #include "tt2_internal.h"
 #include "tt2_common.h"
@@ -500,120 +498,6 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
   }
 }
 
-// ---- Fused-statistics BatchNorm passes (training, no SyncBN): one launch instead of
-// stats + finalize.  Grid (column blocks of 64) x (row chunks of rp rows); 256 threads =
-// 8 column groups of 8 x 32 row lanes, each lane issuing 8 rows of loads before it sums.
-// A workgroup writes its chunk's per-column partials to part[chunk][2][C]; the last chunk of
-// a column block to finish (one counter per block, from the library's counter pool) combines
-// the block's chunks in chunk order, so the result does not depend on which one that is.
-constexpr int BN2_COLS = 64, BN2_RL = NT / (BN2_COLS / 8), BN2_U = 8;
-struct Bn2 {
-  int rp, rc, cb;   // rows per chunk, chunks, column blocks
-  int* cnt;         // [cb] arrival counters (zero between launches)
-};
-
-// Arrival of a chunk workgroup: 1 in the workgroup that completes its column block's count
-// (its counter reset), after an agent-scope acquire of every chunk's partials.
-TT2_DEV bool bn2_arrive(const Bn2& q, int* last) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int* c = q.cnt + blockIdx.x;
-    const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    *last = old == q.rc - 1;
-    if (*last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!*last) return false;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return true;
-}
-
-template <typename T>
-__global__ __launch_bounds__(NT) void bn_stats2_kernel(BnArgs a, Bn2 q) {
-  __shared__ float red[2][BN2_RL][BN2_COLS + 1];
-  __shared__ float shift[BN2_COLS];
-  __shared__ double dred[NT / BN2_COLS][BN2_COLS];
-  __shared__ int last;
-  const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
-  const int c0 = blockIdx.x * BN2_COLS + cg * 8;
-  const bool cok = c0 < a.C;
-  const int r0 = blockIdx.y * q.rp, r1 = min(a.M, r0 + q.rp);
-  const T* y = reinterpret_cast<const T*>(a.y);
-  float k[8], s1[8], s2[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) k[j] = s1[j] = s2[j] = 0.f;
-  if (cok) {
-    ld8(y + (int64_t)r0 * a.C + c0, k);
-    for (int rb = r0 + rl; rb < r1; rb += BN2_U * BN2_RL) {
-      float v[BN2_U][8];
-#pragma unroll
-      for (int u = 0; u < BN2_U; ++u) {
-        const int r = rb + u * BN2_RL;
-        if (r < r1) ld8(y + (int64_t)r * a.C + c0, v[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < BN2_U; ++u) {
-        if (rb + u * BN2_RL >= r1) break;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = v[u][j] - k[j];
-          s1[j] += d;
-          s2[j] += d * d;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { red[0][rl][cg * 8 + j] = s1[j]; red[1][rl][cg * 8 + j] = s2[j]; }
-  if (rl == 0) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) shift[cg * 8 + j] = k[j];
-  }
-  __syncthreads();
-  if (threadIdx.x < BN2_COLS) {
-    const int c = blockIdx.x * BN2_COLS + threadIdx.x;
-    if (c < a.C) {
-      float S1 = 0.f, S2 = 0.f;
-      for (int l = 0; l < BN2_RL; ++l) { S1 += red[0][l][threadIdx.x]; S2 += red[1][l][threadIdx.x]; }
-      const float n = (float)(r1 - r0);
-      a.part[((int64_t)blockIdx.y * 2 + 0) * a.C + c] = shift[threadIdx.x] + S1 / n;
-      a.part[((int64_t)blockIdx.y * 2 + 1) * a.C + c] = fmaxf(S2 - S1 * S1 / n, 0.f);
-    }
-  }
-  if (!bn2_arrive(q, &last)) return;
-  // the block's finalize: bn_finalize_kernel's exact two-pass combine, 4 chunk groups per column
-  const int cl = threadIdx.x % BN2_COLS, g = threadIdx.x / BN2_COLS;
-  const int c = blockIdx.x * BN2_COLS + cl;
-  const bool ok = c < a.C;
-  const int cc = ok ? c : 0;
-  auto nrows = [&](int r) { return (double)min(q.rp, a.M - r * q.rp); };
-  double acc = 0.0;
-  for (int r = g; r < q.rc; r += NT / BN2_COLS) acc += nrows(r) * a.part[((int64_t)r * 2 + 0) * a.C + cc];
-  dred[g][cl] = acc;
-  __syncthreads();
-  const double mu = (((dred[0][cl] + dred[1][cl]) + dred[2][cl]) + dred[3][cl]) / a.M;
-  __syncthreads();
-  acc = 0.0;
-  for (int r = g; r < q.rc; r += NT / BN2_COLS) {
-    const double d = a.part[((int64_t)r * 2 + 0) * a.C + cc] - mu;
-    acc += a.part[((int64_t)r * 2 + 1) * a.C + cc] + nrows(r) * d * d;
-  }
-  dred[g][cl] = acc;
-  __syncthreads();
-  if (g != 0 || !ok) return;
-  const double m2 = ((dred[0][cl] + dred[1][cl]) + dred[2][cl]) + dred[3][cl];
-  const double n = a.M;
-  const double var = m2 / n;
-  a.mean[c] = (float)mu;
-  a.rstd[c] = (float)(1.0 / sqrt(var + a.eps));
-  if (a.run_mean) {
-    const double unb = n > 1 ? m2 / (n - 1) : var;
-    a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mu);
-    a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
-  }
-}
-
 // SyncBatchNorm: combine the W exchanged rank moments (M rows each) in rank order, exactly
 // as bn_finalize_kernel combines chunks: mean = sum mean_r / W, M2 = sum M2_r + M (mean_r - mean)^2
 __global__ __launch_bounds__(NT) void bn_sync_finalize_kernel(BnArgs a) {
@@ -781,84 +665,6 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(BnArgs a) {
   }
 }
 
-// Backward statistics in one launch (bn_stats2_kernel's grid and arrival): chunk sums of
-// dpre and dpre * xhat, and the block's last chunk sums the chunks in chunk order into
-// dbeta / dgamma (this rank's parameter gradients).  4 rows of loads in flight per lane
-// (y and dout both).
-constexpr int BN2B_U = 4;
-template <typename T, typename TD>
-__global__ __launch_bounds__(NT) void bn_bwd_stats2_kernel(BnArgs a, Bn2 q) {
-  __shared__ float red[2][BN2_RL][BN2_COLS + 1];
-  __shared__ int last;
-  const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
-  const int c0 = blockIdx.x * BN2_COLS + cg * 8;
-  const bool cok = c0 < a.C;
-  const int r0 = blockIdx.y * q.rp, r1 = min(a.M, r0 + q.rp);
-  const T* y = reinterpret_cast<const T*>(a.y);
-  const TD* dout = reinterpret_cast<const TD*>(a.dout);
-  const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
-  float s1[8], s2[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
-  if (cok) {
-    float mu[8], rs[8], g[8], b[8];
-    col8(a.mean, c0, mu); col8(a.rstd, c0, rs); col8(a.gamma, c0, g); col8(a.beta, c0, b);
-    for (int rb = r0 + rl; rb < r1; rb += BN2B_U * BN2_RL) {
-      float v[BN2B_U][8], d[BN2B_U][8];
-#pragma unroll
-      for (int u = 0; u < BN2B_U; ++u) {
-        const int r = rb + u * BN2_RL;
-        if (r < r1) {
-          ld8(y + (int64_t)r * a.C + c0, v[u]);
-          ld8(dout + (int64_t)r * a.C + c0, d[u]);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < BN2B_U; ++u) {
-        const int r = rb + u * BN2_RL;
-        if (r >= r1) break;
-        float kp[8];
-        bn_keep8(a, seed, (int64_t)r * a.C + c0, kp);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float xh = (v[u][j] - mu[j]) * rs[j];
-          const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[u][j]);
-          s1[j] += dp;
-          s2[j] += dp * xh;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { red[0][rl][cg * 8 + j] = s1[j]; red[1][rl][cg * 8 + j] = s2[j]; }
-  __syncthreads();
-  if (threadIdx.x < BN2_COLS) {
-    const int c = blockIdx.x * BN2_COLS + threadIdx.x;
-    if (c < a.C) {
-      float S1 = 0.f, S2 = 0.f;
-      for (int l = 0; l < BN2_RL; ++l) { S1 += red[0][l][threadIdx.x]; S2 += red[1][l][threadIdx.x]; }
-      a.part[((int64_t)blockIdx.y * 2 + 0) * a.C + c] = S1;
-      a.part[((int64_t)blockIdx.y * 2 + 1) * a.C + c] = S2;
-    }
-  }
-  if (!bn2_arrive(q, &last)) return;
-  const int cl = threadIdx.x % BN2_COLS, gq = threadIdx.x / BN2_COLS;
-  const int c = blockIdx.x * BN2_COLS + cl;
-  const int cc = c < a.C ? c : 0;
-  float t1 = 0.f, t2 = 0.f;
-  for (int r = gq; r < q.rc; r += NT / BN2_COLS) {
-    t1 += a.part[((int64_t)r * 2 + 0) * a.C + cc];
-    t2 += a.part[((int64_t)r * 2 + 1) * a.C + cc];
-  }
-  __syncthreads();
-  red[0][gq][cl] = t1;
-  red[1][gq][cl] = t2;
-  __syncthreads();
-  if (gq != 0 || c >= a.C) return;
-  a.dbeta[c] = ((red[0][0][cl] + red[0][1][cl]) + red[0][2][cl]) + red[0][3][cl];
-  a.dgamma[c] = ((red[1][0][cl] + red[1][1][cl]) + red[1][2][cl]) + red[1][3][cl];
-}
-
 template <typename T, typename TD>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
   const int CG = a.C >> 3;
@@ -1015,28 +821,10 @@ static BnArgs bn_args(const tt2_bn_args* p) {
   return a;
 }
 
-// the fused-statistics grid: 256-row chunks, fewer rows while the grid has < 256 workgroups
-static Bn2 bn2_plan(int m, int c) {
-  Bn2 q{};
-  q.cb = (c + BN2_COLS - 1) / BN2_COLS;
-  q.rp = 256;
-  while (q.rp > 32 && (int64_t)((m + q.rp - 1) / q.rp) * q.cb < 256) q.rp >>= 1;
-  q.rc = (m + q.rp - 1) / q.rp;
-  return q;
-}
-
 extern "C" size_t tt2_batchnorm_workspace_size(const tt2_bn_args* p) {
   const int rp = bn_rows_per(p->m);
-  const size_t R = std::max<size_t>((p->m + rp - 1) / rp, (size_t)bn2_plan(p->m, p->c).rc);
+  const size_t R = (p->m + rp - 1) / rp;
   return R * 2 * p->c * sizeof(float);
-}
-
-// the fused-statistics plan with its counters, or cnt == null (then stats + finalize launches)
-static Bn2 bn2_take(const tt2_bn_args* p, hipStream_t s) {
-  Bn2 q = bn2_plan(p->m, p->c);
-  q.cnt = nullptr;
-  if (p->training && (size_t)q.rc * 2 * p->c * sizeof(float) <= p->ws_bytes) q.cnt = tt2_fix_counters(q.cb, s);
-  return q;
 }
 
 static int bn_check(const tt2_bn_args* p, const char* what) {
@@ -1057,17 +845,11 @@ extern "C" int tt2_batchnorm_fwd(const tt2_bn_args* p, hipStream_t s) {
     return TT2_E_INVALID;
   BnArgs a = bn_args(p);
   const bool bf = p->dtype == TT2_DT_BF16;
-  const Bn2 q = bn2_take(p, s);
-  if (q.cnt) {
-    if (bf) hipLaunchKernelGGL(bn_stats2_kernel<bf16>, dim3(q.cb, q.rc), dim3(NT), 0, s, a, q);
-    else hipLaunchKernelGGL(bn_stats2_kernel<float>, dim3(q.cb, q.rc), dim3(NT), 0, s, a, q);
-  } else {
-    if (p->training) {
-      if (bf) hipLaunchKernelGGL(bn_stats_kernel<bf16>, dim3(a.R), dim3(NT), 0, s, a);
-      else hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(a.R), dim3(NT), 0, s, a);
-    }
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
+  if (p->training) {
+    if (bf) hipLaunchKernelGGL(bn_stats_kernel<bf16>, dim3(a.R), dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(a.R), dim3(NT), 0, s, a);
   }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
   const int g = grid_for((int64_t)p->m * p->c / 8);
   if (bf) hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(g), dim3(NT), 0, s, a);
   else hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(g), dim3(NT), 0, s, a);
@@ -1087,16 +869,8 @@ extern "C" int tt2_batchnorm_bwd(const tt2_bn_args* p, hipStream_t s) {
   else if (bf) hipLaunchKernelGGL((KER<bf16, float>), grid, dim3(NT), 0, s, a);                 \
   else if (dbf) hipLaunchKernelGGL((KER<float, bf16>), grid, dim3(NT), 0, s, a);                \
   else hipLaunchKernelGGL((KER<float, float>), grid, dim3(NT), 0, s, a);
-  const Bn2 q = bn2_take(p, s);
-  if (q.cnt) {
-    if (bf && dbf) hipLaunchKernelGGL((bn_bwd_stats2_kernel<bf16, bf16>), dim3(q.cb, q.rc), dim3(NT), 0, s, a, q);
-    else if (bf) hipLaunchKernelGGL((bn_bwd_stats2_kernel<bf16, float>), dim3(q.cb, q.rc), dim3(NT), 0, s, a, q);
-    else if (dbf) hipLaunchKernelGGL((bn_bwd_stats2_kernel<float, bf16>), dim3(q.cb, q.rc), dim3(NT), 0, s, a, q);
-    else hipLaunchKernelGGL((bn_bwd_stats2_kernel<float, float>), dim3(q.cb, q.rc), dim3(NT), 0, s, a, q);
-  } else {
-    TT2_BN_DISPATCH(bn_bwd_stats_kernel, dim3(a.R))
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
-  }
+  TT2_BN_DISPATCH(bn_bwd_stats_kernel, dim3(a.R))
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
   const int ga = grid_for((int64_t)p->m * p->c / 8);
   TT2_BN_DISPATCH(bn_bwd_apply_kernel, dim3(ga))
 #undef TT2_BN_DISPATCH

@@ -8,7 +8,3 @@ int tt2_check_launch(hipError_t err, const char* what);
 }
 // compute units of the current device (cached per device; 256 on an MI355X)
 int tt2_cu_count();
-// gemm.hip -- n zeroed arrival counters from the device's counter pool for one launch whose
-// last-arriving workgroup resets each counter it completes; null when the pool cannot be
-// allocated here (first use inside a stream capture): the caller takes its multi-launch path
-int* tt2_fix_counters(int n, hipStream_t s);
