@@ -1,7 +1,7 @@
 #!/bin/bash
 # Full GPU pass: GPU test suite, smoke, default bench line, timed-step kernel profile.
 set -euo pipefail
-TAG=${1:-r03c}
+TAG=${1:-r03v}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
