@@ -207,18 +207,25 @@ def decode_bench(model, reps: int = 3):
             "config": {"workload": "AR decode: encoder + 800 forced hipGraph decode steps + post-net", "batch": DEC_B,
                        "text_len": TX, "frames": DEC_T, "dtype": "bf16"},
             "roofline": {"bound": "hbm", "achieved": round(DEC_BYTES / dt / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
-                         "frac": round(DEC_BYTES / dt / 8e12, 4), **decode_traffic(),
-                         "note": "whole-run algorithmic bytes / wall time (launch-bound: ~58 kernels per step)"}}
+                         "frac": round(DEC_BYTES / dt / 8e12, 4), **decode_traffic("decode"),
+                         "note": "whole-run algorithmic bytes / wall time (latency-bound: a chain of "
+                                 f"{DECODE_LAUNCHES} dependent kernels per step)"}}
 
 
-def decode_traffic():
-    """PMC HBM bytes of one cfg3 run (profiles/*_decode_traffic.json, tools/decode_traffic.py)."""
+DECODE_LAUNCHES = 46   # kernels per decode step (csrc/decoder.cpp tt2_decode_step; profiles/r04_decode_traffic.json counts them)
+
+
+def decode_traffic(kind: str):
+    """PMC HBM bytes of one decode run: kind "decode" (cfg3) or "longform" (cfg5), from the
+    latest profiles/*_<kind>_traffic.json (tools/decode_traffic.py + summarize_decode_traffic.py)."""
     prof = os.path.join(ROOT, "profiles")
-    files = sorted(f for f in os.listdir(prof) if f.endswith("_decode_traffic.json")) if os.path.isdir(prof) else []
+    suffix = f"_{kind}_traffic.json"
+    files = sorted(f for f in os.listdir(prof) if f.endswith(suffix)) if os.path.isdir(prof) else []
     if not files:
         return {"traffic": None}
     t = json.load(open(os.path.join(prof, files[-1])))
     return {"traffic": round(t["hbm_bytes_per_run"]), "traffic_unit": "B per run",
+            "traffic_over_algorithmic": round(t["traffic_over_algorithmic"], 3),
             "traffic_source": "profiles/" + files[-1]}
 
 
@@ -412,7 +419,7 @@ def longform_bench(model):
                        "text_len": TX, "t_max": LF_T, "lengths": "U[1000, 2000] seeded",
                        "dtype": "fp16 decode step (f16 weights, KV cache, cross K/V; bf16 encoder / post-net)"},
             "roofline": {"bound": "hbm", "achieved": round(algo / dt / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
-                         "frac": round(algo / dt / 8e12, 4), "traffic": None,
+                         "frac": round(algo / dt / 8e12, 4), **decode_traffic("longform"),
                          "algo_bytes": algo, "note": "weights per step + running utterances' KV bytes only"}}
 
 

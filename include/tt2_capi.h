@@ -406,12 +406,14 @@ typedef struct tt2_bn_args {
 size_t tt2_batchnorm_workspace_size(const tt2_bn_args* a);
 int tt2_batchnorm_fwd(const tt2_bn_args* a, hipStream_t stream);
 int tt2_batchnorm_bwd(const tt2_bn_args* a, hipStream_t stream);
-/* SyncBatchNorm over sync_world data-parallel ranks of m rows each (torch.nn.SyncBatchNorm's
- * semantics: training statistics and the backward's column sums over all W*m rows; the
- * dgamma / dbeta parameter gradients stay this rank's sums, for the gradient all-reduce).
+/* SyncBatchNorm over sync_world data-parallel ranks, rank r holding its own m_r rows (ranks
+ * may differ: torch.nn.SyncBatchNorm's semantics, training statistics and the backward's
+ * column sums over all sum_r m_r rows, each rank weighted by its row count; the dgamma / dbeta
+ * parameter gradients stay this rank's sums, for the gradient all-reduce).
  * Each pass is two phases around a caller-issued SUM all-reduce of the first
- * sync_world * 2 * c floats of sync_buf (this rank's slot holds its moments / sums, the
- * other slots zeros, so the reduced slots are exact and rank-ordered on every rank):
+ * sync_world * 3 * c floats of sync_buf ([W][3][c]: this rank's slot holds its moments / sums
+ * and its row count m, the other slots zeros, so the reduced slots are exact and rank-ordered
+ * on every rank):
  *   tt2_batchnorm_fwd_stats -> all-reduce -> tt2_batchnorm_fwd_apply   (training only)
  *   tt2_batchnorm_bwd_stats -> all-reduce -> tt2_batchnorm_bwd_apply
  * sync_world = 1 reproduces tt2_batchnorm_fwd / _bwd (no exchange needed).  The optional

@@ -218,7 +218,14 @@ class FFN(nn.Module):
 
 
 class ConvBN(nn.Module):
-    """Conv1d(k, pad (k-1)/2, bias) + BatchNorm1d on channels-last input."""
+    """Conv1d(k, pad (k-1)/2, bias) + BatchNorm1d on channels-last input.
+
+    ``ConvBN.stats_f64`` (class-wide, off by default) is a conditioning probe for the tests,
+    not a model option: the training-mode normalisation is then evaluated in float64 from
+    the f32 conv output and rounded back, i.e. the same model with the BatchNorm's
+    reductions rounded differently.  How far a gradient moves under it measures that
+    gradient's own sensitivity to BatchNorm rounding (tests/test_gpu_fullsize.py)."""
+    stats_f64 = False
 
     def __init__(self, cin: int, cout: int, k: int, momentum: float, eps: float):
         super().__init__()
@@ -226,7 +233,14 @@ class ConvBN(nn.Module):
         self.bn = nn.BatchNorm1d(cout, momentum=momentum, eps=eps)
 
     def forward(self, x):  # x [B, T, C]
-        return self.bn(self.conv(x.transpose(1, 2))).transpose(1, 2)
+        y = self.conv(x.transpose(1, 2))
+        if self.stats_f64 and self.training and y.dtype == torch.float32:
+            bn = self.bn
+            with torch.no_grad():
+                bn(y)                       # running statistics exactly as the plain path
+            z = F.batch_norm(y.double(), None, None, bn.weight.double(), bn.bias.double(), True, 0.0, bn.eps)
+            return z.float().transpose(1, 2)
+        return self.bn(y).transpose(1, 2)
 
 
 class EncoderPrenet(nn.Module):

@@ -99,27 +99,32 @@ def test_dp_gradient_is_mean_of_shards():
 
 def _bnsync_case(rank, world):
     """SyncBatchNorm's exchange protocol (tt2/dist.py BnSync, the tt2_batchnorm_*_stats slot
-    layout): each rank fills only its own [2][C] slot of the [world][2][C] buffer, the SUM
-    all-reduce gives every rank every slot, and combining them in rank order the way
-    bn_sync_finalize_kernel does (mean of means, M2 + M (mean_r - mean)^2) gives the
-    statistics of the concatenated rows."""
+    layout): each rank fills only its own [3][C] slot (mean, M2, row count) of the
+    [world][3][C] buffer, the SUM all-reduce gives every rank every slot, and combining them
+    in rank order the way bn_sync_finalize_kernel does (count-weighted mean, M2 + n_r
+    (mean_r - mean)^2) gives the statistics of the concatenated rows, with ranks holding
+    different row counts."""
     from tt2.dist import BnSync
-    M, C = 37, 16
-    ys = [torch.randn(M, C, generator=torch.Generator().manual_seed(50 + r), dtype=torch.float64) * (1 + r) + r
+    C = 16
+    Ms = [37 + 11 * r for r in range(world)]
+    ys = [torch.randn(Ms[r], C, generator=torch.Generator().manual_seed(50 + r), dtype=torch.float64) * (1 + r) + r
           for r in range(world)]
     s = BnSync(world, rank, device="cpu")
-    buf = s.buffer((world + 1) * 2 * C * 4)
-    slots = buf[:world * 2 * C].view(world, 2, C)
+    buf = s.buffer((3 * world + 2) * C * 4)
+    slots = buf[:world * 3 * C].view(world, 3, C)
     slots.zero_()
     y = ys[rank]
     slots[rank, 0] = y.mean(0).float()
     slots[rank, 1] = ((y - y.mean(0)) ** 2).sum(0).float()
-    s.exchange(buf[:world * 2 * C])
-    mu = slots[:, 0].double().mean(0)
-    m2 = (slots[:, 1].double() + M * (slots[:, 0].double() - mu) ** 2).sum(0)
+    slots[rank, 2] = float(Ms[rank])
+    s.exchange(buf[:world * 3 * C])
+    n = slots[:, 2].double()
+    N = n.sum(0)
+    mu = (n * slots[:, 0].double()).sum(0) / N
+    m2 = (slots[:, 1].double() + n * (slots[:, 0].double() - mu) ** 2).sum(0)
     full = torch.cat(ys)
     return max((mu - full.mean(0)).abs().max().item(),
-               (m2 / (world * M) - full.var(0, unbiased=False)).abs().max().item() / full.var(0).max().item())
+               (m2 / N - full.var(0, unbiased=False)).abs().max().item() / full.var(0).max().item())
 
 
 def test_syncbn_exchange_gloo():

@@ -13,7 +13,7 @@ import torch.distributed as dist
 pytestmark = pytest.mark.gpu
 
 from tt2.config import TTSConfig  # noqa: E402
-from tt2.dist import GradSync, RcclGradSync, attach  # noqa: E402
+from tt2.dist import GradSync, attach  # noqa: E402
 from tt2.model import TransformerTTS  # noqa: E402
 
 
@@ -105,16 +105,7 @@ class SnapshotSync(_Snap, GradSync):
         self._init_snap()
 
 
-class RcclSnapshotSync(_Snap, RcclGradSync):
-    """The same check for the in-graph path, eagerly (its launch points are the same hook
-    calls; inside a capture the comm stream is ordered by the same stream waits)."""
-
-    def __init__(self, *a, **kw):
-        RcclGradSync.__init__(self, *a, **kw)
-        self._init_snap()
-
-
-@pytest.mark.parametrize("bucket_mb,cls", [(4, SnapshotSync), (25, SnapshotSync), (25, RcclSnapshotSync)])
+@pytest.mark.parametrize("bucket_mb,cls", [(4, SnapshotSync), (25, SnapshotSync)])
 def test_buckets_final_when_launched_cfg2(nccl_group, bucket_mb, cls):
     """At the cfg2 shape (B = 16, 128 phonemes, 800 frames, dropout on): every gradient
     bucket is final when its all-reduce is launched, eagerly (hook during the backward)
@@ -135,9 +126,6 @@ def test_buckets_final_when_launched_cfg2(nccl_group, bucket_mb, cls):
         m.train_step(text, tl, mel, ml, sync_grads=sync.finish)
     torch.cuda.synchronize()
     assert sync.steps == 2 and sync.bad == [], f"eager: buckets written after launch {sync.bad}"
-    if cls is RcclSnapshotSync:
-        sync.close()
-        return
     run = m.capture_train_step(B, Tx, Ty, sync_grads=sync.finish)
     for _ in range(2):
         run(text, tl, mel, ml)
@@ -145,11 +133,116 @@ def test_buckets_final_when_launched_cfg2(nccl_group, bucket_mb, cls):
     assert sync.steps == 4 and sync.bad == [], f"captured: buckets written after launch {sync.bad}"
 
 
+class InGraphSnap:
+    """Bucket finality INSIDE the captured one-graph DP step (RcclGradSync, the path bench.py
+    runs at N > 1).  RcclGradSync.snap_hook copies each bucket on the comm stream right after
+    its all-reduce is issued, so the copies are captured with the step and replay in the
+    comm stream's order; after a replay every copy must equal the final gradients bit for
+    bit (one rank: the all-reduce is the identity).  A kernel of the compute stream that
+    writes into a bucket after the bucket was forked to RCCL changes the final gradients
+    but not the copy.  SyncBatchNorm exchanges (BnSync on the same comm stream) are checked
+    the same way: the slots as the stats kernel left them on the compute stream (copied
+    before the fork) against the slots after the comm stream's all-reduce."""
+
+    def __init__(self, sync, bn=None, n_bn=64):
+        self.sync = sync
+        self.buf = torch.zeros_like(sync.flat)
+        sync.snap_hook = self._bucket
+        self.bn = bn
+        if bn is not None:
+            self.pre = torch.zeros(n_bn, bn._buf.numel(), device=bn._buf.device)
+            self.post = torch.zeros_like(self.pre)
+            self.n = [0, 0]
+            bn.snap_hook = self._bn_post
+            ex = bn.exchange
+
+            def exchange(slots):
+                k = self.n[0] % n_bn
+                self.pre[k, :slots.numel()].copy_(slots)
+                self.n[0] += 1
+                ex(slots)
+            bn.exchange = exchange
+
+    def _bucket(self, lo, hi):
+        self.buf[lo:hi].copy_(self.sync.flat[lo:hi])
+
+    def _bn_post(self, slots):
+        k = self.n[1] % self.pre.shape[0]
+        self.post[k, :slots.numel()].copy_(slots)
+        self.n[1] += 1
+
+    def bad(self):
+        torch.cuda.synchronize()
+        out = [(lo, hi) for lo, hi in self.sync.buckets if not torch.equal(self.buf[lo:hi], self.sync.flat[lo:hi])]
+        if self.bn is not None:
+            n = min(self.n[1], self.pre.shape[0])
+            out += [("bn", k) for k in range(n) if not torch.equal(self.pre[k], self.post[k])]
+        return out
+
+
+def _cfg2_batch(seed=4):
+    g = torch.Generator().manual_seed(seed)
+    B, Tx, Ty = 16, 128, 800
+    text = torch.randint(1, 80, (B, Tx), generator=g).cuda()
+    tl = torch.full((B,), Tx, dtype=torch.int32).cuda()
+    mel = torch.randn(B, Ty, 80, generator=g).cuda()
+    ml = torch.full((B,), Ty, dtype=torch.int32).cuda()
+    return B, Tx, Ty, text, tl, mel, ml
+
+
+@pytest.mark.parametrize("sync_bn", [False, True])
+def test_buckets_final_in_captured_rccl_step_cfg2(nccl_group, sync_bn):
+    """cfg2 (B = 16, 128 phonemes, 800 frames, dropout on), the RCCL in-graph path that
+    bench.py runs at N = 8: inside the ONE captured step graph every bucket is final when the
+    comm stream's all-reduce runs, over two replays, with and without SyncBatchNorm (whose
+    16 exchanges per step share the comm stream)."""
+    B, Tx, Ty, text, tl, mel, ml = _cfg2_batch()
+    m = _model()
+    sync = attach(m, kind="rccl", sync_bn=sync_bn)
+    assert sync.in_graph and len(sync.buckets) >= 3
+    snap = InGraphSnap(sync, m.engine.bn_sync)
+    for _ in range(2):
+        m.train_step(text, tl, mel, ml, sync_grads=sync.finish)
+    assert snap.bad() == [], "eager"
+    run = m.capture_train_step(B, Tx, Ty, sync_grads=sync.finish)
+    segs, g2 = m._graphs[(B, Tx, Ty)]
+    assert g2 is None and len(segs) == 1
+    for _ in range(2):
+        snap.buf.fill_(float("nan"))      # a bucket the graph does not copy stays NaN: unequal
+        run(text, tl, mel, ml)
+        assert snap.bad() == [], "captured"
+    if sync_bn:
+        assert snap.n[0] == snap.n[1] and snap.n[0] >= 2 * 16
+    sync.close()
+    assert m.engine.bn_sync is None and m.engine.grad_ready_hook is None   # detached on close
+
+
+def test_misplaced_grad_ready_is_caught(nccl_group):
+    """Negative control for the check above: the engine's bucket hook shifted so every bucket
+    is handed to RCCL 2M elements (8 MB of gradients) before it is final.  The captured step
+    must then show buckets whose final gradients differ from what the comm stream copied."""
+    B, Tx, Ty, text, tl, mel, ml = _cfg2_batch()
+    m = _model()
+    sync = attach(m, kind="rccl")
+    snap = InGraphSnap(sync)
+    shift = 2 << 20
+    ready = sync.ready
+    sync.ready = lambda off: ready(max(0, off - shift))   # the captured step hooks sync.ready too
+    m.engine.grad_ready_hook = sync.ready
+    for _ in range(2):
+        m.train_step(text, tl, mel, ml, sync_grads=sync.finish)
+    run = m.capture_train_step(B, Tx, Ty, sync_grads=sync.finish)
+    run(text, tl, mel, ml)
+    assert len(snap.bad()) >= 1, "an early bucket hand-off went unnoticed"
+    sync.close()
+
+
 def test_syncbn_rccl_exchange_in_graph_one_rank(nccl_group):
     """SyncBatchNorm over libtt2's RCCL communicator (attach(sync_bn=True), nccl): the 16
     BatchNorm exchanges per step are captured in the one step graph with the bucket
-    all-reduces; with one rank the exchange is the identity, so the step follows the plain
-    one up to the slot's f32 rounding of M2 (no host sync anywhere: replays only)."""
+    all-reduces, on the comm stream; with one rank the exchange (which runs: BnSync does not
+    skip it at world 1 on RCCL) is the identity, so the step follows the plain one up to the
+    slot's f32 rounding of the mean and M2 (no host sync anywhere: replays only)."""
     g = torch.Generator().manual_seed(4)
     B, Tx, Ty = 2, 24, 48
     text = torch.randint(1, 80, (B, Tx), generator=g).cuda()

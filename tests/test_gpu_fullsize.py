@@ -33,7 +33,33 @@ def batch(B, tls, mls, seed=0, Tx=128, Ty=800):
     return text, tl, mel, ml
 
 
+def _oracle_grads(text, tl, mel, ml, dtype, bn_f64=False):
+    """Parameter gradients of the oracle at the test batch: f32, f64, or f32 with its
+    BatchNorm normalisation evaluated in float64 (ConvBN.stats_f64, a rounding probe)."""
+    from tt2_oracle import ConvBN
+    o = init_deterministic(TransformerTTSOracle(OracleConfig()), 21).train().to(dtype)
+    o.set_seed(99)
+    ConvBN.stats_f64 = bn_f64
+    try:
+        m = mel.to(dtype)
+        ob, oa, os_, _ = o(text, tl, m, ml)
+        lo, _ = o.loss((ob, oa, os_), m, ml)
+        lo.backward()
+    finally:
+        ConvBN.stats_f64 = False
+    return {k: (p.grad if p.grad is not None else torch.zeros_like(p)).detach().clone()
+            for k, p in o.named_parameters()}
+
+
 def test_full_length_fp32_parity():
+    """Exact-f32 engine vs the oracle at 128 / 800 (B = 2, ragged, dropout on).  Gradients are
+    anchored on a float64 oracle: each parameter's gradient must sit within
+    max(1e-3, 2 x noise) of float64, where noise is the larger distance from float64 of two
+    f32 evaluations of the same model (the plain f32 oracle, and the f32 oracle whose BatchNorm
+    reductions round differently), i.e. the gradient's own f32 conditioning; and where that
+    noise is below 3e-4 the plain engine-vs-f32-oracle 1e-3 bound holds as well.  (A scalar
+    such as decoder.pos.alpha, a cancelling sum over 1600 x 512 frame-channel terms, moves by
+    ~3e-3 under a different BatchNorm rounding while every matrix gradient moves < 1e-5.)"""
     torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
     oracle = init_deterministic(TransformerTTSOracle(OracleConfig()), 21).train()
     model = TransformerTTS(TTSConfig(), dtype=torch.float32).train()
@@ -50,14 +76,26 @@ def test_full_length_fp32_parity():
     lo.backward()
     model.backward()
     gm = model.grads_state_dict()
-    gnorm = torch.sqrt(sum((p.grad.double() ** 2).sum() for p in oracle.parameters() if p.grad is not None))
-    bad = []
-    for k, p in oracle.named_parameters():
-        ref = p.grad if p.grad is not None else torch.zeros_like(p)
+    g32 = {k: (p.grad if p.grad is not None else torch.zeros_like(p)) for k, p in oracle.named_parameters()}
+    g64 = _oracle_grads(text, tl, mel, ml, torch.float64)
+    gbn = _oracle_grads(text, tl, mel, ml, torch.float32, bn_f64=True)
+    gnorm = torch.sqrt(sum((g.double() ** 2).sum() for g in g64.values()))
+    bad, report = [], []
+    for k, ref in g64.items():
         if ref.double().norm() < 1e-6 * gnorm:
-            continue      # conv biases in front of training-mode BatchNorm: analytically zero
-        if rel(gm[k], ref) >= 1e-3:
-            bad.append((k, rel(gm[k], ref)))
+            # conv biases in front of training-mode BatchNorm: analytically zero
+            assert gm[k].double().norm() < 1e-5 * gnorm, (k, gm[k].norm())
+            continue
+        e64 = rel(gm[k], ref)
+        noise = max(rel(g32[k], ref), rel(gbn[k], ref))
+        tol = max(1e-3, 2 * noise)
+        report.append((e64, noise, k))
+        if e64 > tol:
+            bad.append((k, e64, tol))
+        if noise < 3e-4 and rel(gm[k], g32[k]) >= 1e-3:
+            bad.append((k, "vs f32 oracle", rel(gm[k], g32[k])))
+    report.sort(reverse=True)
+    print("worst engine-vs-f64 / f32 noise:", [(f"{a:.2e}", f"{b:.2e}", k) for a, b, k in report[:4]])
     assert not bad, bad
 
 

@@ -111,10 +111,13 @@ def test_layernorm_bwd_chained_finalize(m1, m2):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("m,c,act,res", [(1000, 512, 1, False), (333, 80, 0, True), (64, 512, 2, False)])
+@pytest.mark.parametrize("m,c,act,res", [(1000, 512, 1, False), (333, 80, 0, True), (64, 512, 2, False),
+                                         (12800, 80, 2, True), (12800, 512, 1, False), (12800, 512, 2, False)])
 def test_batchnorm_train_fwd_bwd(dtype, m, c, act, res):
     """Training-mode BatchNorm1d over rows + act + dropout (+ residual): forward, running
-    statistics and backward vs float64 torch."""
+    statistics and backward vs float64 torch, up to cfg2's 12800 post-net rows (B = 16 x 800
+    frames; C = 80 is the last post-net layer with the residual, C = 512 the tanh layers);
+    repeated calls give bitwise the same statistics and gradients."""
     g = torch.Generator().manual_seed(m + c + act)
     y = (torch.randn(m, c, generator=g) * 3 + 1.5)
     gamma = 1 + 0.1 * torch.randn(c, generator=g)
@@ -152,6 +155,15 @@ def test_batchnorm_train_fwd_bwd(dtype, m, c, act, res):
     assert rel(dy, yr.grad) < tol_b
     assert rel(dg, gr.grad) < tol_b
     assert rel(db, br.grad) < tol_b
+    for _ in range(2):   # fixed reduction order: repeated calls are bitwise identical
+        m2, r2, o2 = torch.empty_like(mean), torch.empty_like(rstd), torch.empty_like(out)
+        ops.batchnorm_fwd(yd, gamma.cuda(), beta.cuda(), m2, r2, torch.zeros(c, device="cuda"),
+                          torch.ones(c, device="cuda"), o2, m, c, act, True, drop=drop,
+                          res=r.cuda() if res else None, res_ld=96)
+        dy2, dg2, db2 = torch.empty_like(dy), torch.empty_like(dg), torch.empty_like(db)
+        ops.batchnorm_bwd(yd, dd, gamma.cuda(), beta.cuda(), m2, r2, dy2, dg2, db2, m, c, act, drop=drop)
+        assert torch.equal(m2, mean) and torch.equal(r2, rstd) and torch.equal(o2, out)
+        assert torch.equal(dy2, dy) and torch.equal(dg2, dg) and torch.equal(db2, db)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

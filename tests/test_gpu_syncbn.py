@@ -34,7 +34,7 @@ class SimSync:
 
     def __init__(self, world, rank, others=()):
         self.world, self.rank, self.others = world, rank, list(others)
-        self.buf = torch.zeros((world + 1) * 2 * 2048, device="cuda")
+        self.buf = torch.zeros((3 * world + 2) * 2048, device="cuda")
         self.sent = None
 
     def buffer(self, nbytes):
@@ -60,28 +60,31 @@ def _bn_bwd(y, dout, gamma, beta, mean, rstd, m, c, act, sync=None):
     return dy, dg, db
 
 
-@pytest.mark.parametrize("c,act", [(512, 1), (80, 0), (512, 2)])
-def test_syncbn_kernels_match_full_batch(c, act):
-    torch.manual_seed(c + act)
-    M, W = 640, 2
-    y = [(torch.randn(M, c, device="cuda") * 1.7 + 0.3 * r + 2.0) for r in range(W)]
-    dout = [torch.randn(M, c, device="cuda") for _ in range(W)]
+@pytest.mark.parametrize("c,act,Ms", [(512, 1, (640, 640)), (80, 0, (640, 640)), (512, 2, (640, 640)),
+                                      (512, 2, (640, 213)), (80, 1, (96, 1201))])
+def test_syncbn_kernels_match_full_batch(c, act, Ms):
+    """Ms: each rank's row count (ranks padded to different lengths hold different counts;
+    the exchange carries them and weights each rank by its rows)."""
+    torch.manual_seed(c + act + Ms[1])
+    W = 2
+    y = [(torch.randn(Ms[r], c, device="cuda") * 1.7 + 0.3 * r + 2.0) for r in range(W)]
+    dout = [torch.randn(Ms[r], c, device="cuda") for r in range(W)]
     gamma, beta = torch.rand(c, device="cuda") + 0.5, torch.randn(c, device="cuda") * 0.1
     rm0, rv0 = torch.randn(c, device="cuda") * 0.1, torch.rand(c, device="cuda") + 0.5
     # the full batch, plain BatchNorm
     rmf, rvf = rm0.clone(), rv0.clone()
     yf, df = torch.cat(y), torch.cat(dout)
-    of, mf, sf = _bn_fwd(yf, gamma, beta, W * M, c, act, rmf, rvf)
-    dyf, dgf, dbf = _bn_bwd(yf, df, gamma, beta, mf, sf, W * M, c, act)
+    of, mf, sf = _bn_fwd(yf, gamma, beta, sum(Ms), c, act, rmf, rvf)
+    dyf, dgf, dbf = _bn_bwd(yf, df, gamma, beta, mf, sf, sum(Ms), c, act)
     # rank 1's slots first (its own outputs are not used), then each rank with the other's
     pre = SimSync(W, 1)
-    _bn_fwd(y[1], gamma, beta, M, c, act, rm0.clone(), rv0.clone(), pre)
+    _bn_fwd(y[1], gamma, beta, Ms[1], c, act, rm0.clone(), rv0.clone(), pre)
     s0 = SimSync(W, 0, [pre.sent])
     rm_0, rv_0 = rm0.clone(), rv0.clone()
-    o0, m0, r0 = _bn_fwd(y[0], gamma, beta, M, c, act, rm_0, rv_0, s0)
+    o0, m0, r0 = _bn_fwd(y[0], gamma, beta, Ms[0], c, act, rm_0, rv_0, s0)
     s1 = SimSync(W, 1, [s0.sent])
     rm_1, rv_1 = rm0.clone(), rv0.clone()
-    o1, m1, r1 = _bn_fwd(y[1], gamma, beta, M, c, act, rm_1, rv_1, s1)
+    o1, m1, r1 = _bn_fwd(y[1], gamma, beta, Ms[1], c, act, rm_1, rv_1, s1)
     assert torch.equal(m0, m1) and torch.equal(r0, r1)          # same slots, same order: same statistics
     assert torch.equal(rm_0, rm_1) and torch.equal(rv_0, rv_1)
     assert rel(m0, mf) < 1e-6 and rel(r0, sf) < 1e-6
@@ -89,18 +92,18 @@ def test_syncbn_kernels_match_full_batch(c, act):
     assert rel(torch.cat([o0, o1]), of) < 1e-6
     # backward
     preb = SimSync(W, 1)
-    _bn_bwd(y[1], dout[1], gamma, beta, m1, r1, M, c, act, preb)
+    _bn_bwd(y[1], dout[1], gamma, beta, m1, r1, Ms[1], c, act, preb)
     b0 = SimSync(W, 0, [preb.sent])
-    dy0, dg0, db0 = _bn_bwd(y[0], dout[0], gamma, beta, m0, r0, M, c, act, b0)
+    dy0, dg0, db0 = _bn_bwd(y[0], dout[0], gamma, beta, m0, r0, Ms[0], c, act, b0)
     b1 = SimSync(W, 1, [b0.sent])
-    dy1, dg1, db1 = _bn_bwd(y[1], dout[1], gamma, beta, m1, r1, M, c, act, b1)
+    dy1, dg1, db1 = _bn_bwd(y[1], dout[1], gamma, beta, m1, r1, Ms[1], c, act, b1)
     assert rel(torch.cat([dy0, dy1]), dyf) < 1e-5
     assert rel(dg0 + dg1, dgf) < 1e-5 and rel(db0 + db1, dbf) < 1e-5
     # dgamma / dbeta are each rank's own sums (the gradient all-reduce adds them)
-    _, dg0s, db0s = _bn_bwd(y[0], dout[0], gamma, beta, m0, r0, M, c, act)
+    _, dg0s, db0s = _bn_bwd(y[0], dout[0], gamma, beta, m0, r0, Ms[0], c, act)
     assert torch.equal(dg0, dg0s) and torch.equal(db0, db0s)
     # per-replica statistics differ from the full batch's (the shards were shifted apart)
-    _, ml, _ = _bn_fwd(y[0], gamma, beta, M, c, act, rm0.clone(), rv0.clone())
+    _, ml, _ = _bn_fwd(y[0], gamma, beta, Ms[0], c, act, rm0.clone(), rv0.clone())
     assert rel(ml, mf) > 1e-2
 
 
@@ -145,16 +148,16 @@ def _free_port():
 def _shard(r, B=3, Tx=24, Ty=56):
     g = torch.Generator().manual_seed(31 + r)
     text = torch.randint(1, 80, (B, Tx), generator=g)
-    tl = torch.tensor([Tx, Tx - 5 - r, Tx - 9])
+    tl = torch.tensor([Tx, Tx - 5 - r, Tx - 9][:B])
     mel = torch.randn(B, Ty, 80, generator=g) * (1.0 + r) + 0.5 * r   # shards with different statistics
-    ml = torch.tensor([Ty, Ty - 13, Ty - 20])                          # equal valid frames per rank
+    ml = torch.tensor([Ty, Ty - 13, Ty - 20][:B])                      # equal valid frames per rank
     for b in range(B):
         text[b, tl[b]:] = 0
         mel[b, ml[b]:] = 0
     return [t.cuda() for t in (text, tl, mel, ml)]
 
 
-def _rank(rank, world, port, q):
+def _rank(rank, world, port, q, Bs=(3, 3)):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), TT2_DIST_BACKEND="gloo")
     sys.path.insert(0, os.path.join(ROOT, "transformer-tacotron2_amd"))
@@ -174,7 +177,7 @@ def _rank(rank, world, port, q):
                 if len(shape) >= 2:
                     e.P(name).copy_(torch.randn(shape, generator=g, device="cuda") / (n // shape[0]) ** 0.5)
             e.sync_shadow()
-        shards = [_shard(r) for r in range(world)]
+        shards = [_shard(r, B=Bs[r]) for r in range(world)]
         full = [torch.cat([s[i] for s in shards]) for i in range(4)]
         S0 = e.stats.clone()
 
@@ -212,12 +215,17 @@ def _rank(rank, world, port, q):
         raise
 
 
-def test_two_rank_syncbn_equals_full_batch():
+@pytest.mark.parametrize("Bs", [(3, 3), (3, 1)])
+def test_two_rank_syncbn_equals_full_batch(Bs):
+    """Bs: utterances per rank.  (3, 1): the ranks' BatchNorms hold 3x56 and 1x56 decoder rows
+    (3x24 / 1x24 encoder rows); the exchanged row counts weight them, so the running statistics
+    are the concatenated batch's.  The DP gradient is a mean over ranks of per-rank losses and
+    equals the concatenated batch's only when the ranks hold equal batches (3, 3)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     world = 2
-    ps = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_rank, args=(r, world, port, q, Bs)) for r in range(world)]
     for p in ps:
         p.start()
     try:
@@ -232,7 +240,8 @@ def test_two_rank_syncbn_equals_full_batch():
     for p in ps:
         assert p.exitcode == 0
     for r, v in out.items():
-        assert v["sync"] < 1e-4, (r, v)           # SyncBN DP gradient = the concatenated batch's
-        assert v["replica"] > 20 * v["sync"], (r, v)   # per-replica statistics are not
+        if Bs[0] == Bs[1]:
+            assert v["sync"] < 1e-4, (r, v)           # SyncBN DP gradient = the concatenated batch's
+            assert v["replica"] > 20 * v["sync"], (r, v)   # per-replica statistics are not
         assert v["stats"] < 1e-5, (r, v)          # running statistics of the whole batch
         assert v["refused"], (r, v)

@@ -39,9 +39,19 @@ for s in $STEPS; do
       ;;
     dpmc)  # the same for one cfg3 decode run
       timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/dtr/fetch" -o run --output-format csv -- \
-        python3 tools/decode_traffic.py > "$OUT/dtr_fetch.log" 2>&1
+        python3 tools/decode_traffic.py --out="$OUT/dtr" > "$OUT/dtr_fetch.log" 2>&1
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/dtr/write" -o run --output-format csv -- \
-        python3 tools/decode_traffic.py > "$OUT/dtr_write.log" 2>&1
+        python3 tools/decode_traffic.py --out="$OUT/dtr" > "$OUT/dtr_write.log" 2>&1
+      ;;
+    lpmc)  # and for one cfg5 long-form run
+      timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE -d "$OUT/ltr/fetch" -o run --output-format csv -- \
+        python3 tools/decode_traffic.py --longform --out="$OUT/ltr" > "$OUT/ltr_fetch.log" 2>&1
+      timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE -d "$OUT/ltr/write" -o run --output-format csv -- \
+        python3 tools/decode_traffic.py --longform --out="$OUT/ltr" > "$OUT/ltr_write.log" 2>&1
+      ;;
+    dpt)   # the DP / SyncBN / norm / full-length parity tests of round 4
+      timeout -k 10 900 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_syncbn.py tests/test_gpu_norm.py \
+        tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread > "$OUT/dpt_tests.log" 2>&1
       ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -347,11 +347,12 @@ struct BnArgs {
   int M, C, R, rows_per, act, out_dt, res_dt, training;
   float eps, momentum;
   DropDesc drop;
-  // SyncBatchNorm exchange (tt2_batchnorm_{fwd,bwd}_{stats,apply}): [W][2][C] rank slots
-  // (this rank's moments or sums, zeros in the others; all-reduced by the caller) + [2][C]
+  // SyncBatchNorm exchange (tt2_batchnorm_{fwd,bwd}_{stats,apply}): [W][3][C] rank slots
+  // (this rank's moments or sums and its row count, zeros in the others; all-reduced by the
+  // caller) + [2][C]
   float* sync;
   int W, rank;
-  int64_t Mtot;   // rows behind the statistics: M, or W * M once exchanged
+  int64_t Mtot;   // rows behind the statistics: M (1 in the SyncBN apply: sums arrive divided)
 };
 
 // tanh through one v_exp_f32 and one v_rcp_f32 (ocml's tanhf is a long branchy sequence and
@@ -480,10 +481,11 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
   if (g != 0 || !ok) return;
   double m2 = 0.0;
   for (int k = 0; k < BNF_GROUPS; ++k) m2 += red[k][cl];
-  if (a.sync) {   // this rank's (mean, M2) into its slot; the other ranks' slots zero
+  if (a.sync) {   // this rank's (mean, M2, rows) into its slot; the other ranks' slots zero
     for (int r2 = 0; r2 < a.W; ++r2) {
-      a.sync[((int64_t)r2 * 2 + 0) * a.C + c] = r2 == a.rank ? (float)mu : 0.f;
-      a.sync[((int64_t)r2 * 2 + 1) * a.C + c] = r2 == a.rank ? (float)m2 : 0.f;
+      a.sync[((int64_t)r2 * 3 + 0) * a.C + c] = r2 == a.rank ? (float)mu : 0.f;
+      a.sync[((int64_t)r2 * 3 + 1) * a.C + c] = r2 == a.rank ? (float)m2 : 0.f;
+      a.sync[((int64_t)r2 * 3 + 2) * a.C + c] = r2 == a.rank ? (float)a.M : 0.f;
     }
     return;
   }
@@ -498,20 +500,25 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
   }
 }
 
-// SyncBatchNorm: combine the W exchanged rank moments (M rows each) in rank order, exactly
-// as bn_finalize_kernel combines chunks: mean = sum mean_r / W, M2 = sum M2_r + M (mean_r - mean)^2
+// SyncBatchNorm: combine the W exchanged rank moments in rank order, exactly as
+// bn_finalize_kernel combines chunks, weighted by each rank's row count n_r (ranks may hold
+// different numbers of rows): N = sum n_r, mean = sum n_r mean_r / N,
+// M2 = sum M2_r + n_r (mean_r - mean)^2.  Slots are [W][3][C]: (mean, M2, n) per rank.
 __global__ __launch_bounds__(NT) void bn_sync_finalize_kernel(BnArgs a) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= a.C) return;
-  double mu = 0.0;
-  for (int r = 0; r < a.W; ++r) mu += (double)a.sync[((int64_t)r * 2 + 0) * a.C + c];
-  mu /= a.W;
+  double n = 0.0, mu = 0.0;
+  for (int r = 0; r < a.W; ++r) {
+    const double nr = (double)a.sync[((int64_t)r * 3 + 2) * a.C + c];
+    n += nr;
+    mu += nr * (double)a.sync[((int64_t)r * 3 + 0) * a.C + c];
+  }
+  mu /= n;
   double m2 = 0.0;
   for (int r = 0; r < a.W; ++r) {
-    const double d = (double)a.sync[((int64_t)r * 2 + 0) * a.C + c] - mu;
-    m2 += (double)a.sync[((int64_t)r * 2 + 1) * a.C + c] + (double)a.M * d * d;
+    const double d = (double)a.sync[((int64_t)r * 3 + 0) * a.C + c] - mu;
+    m2 += (double)a.sync[((int64_t)r * 3 + 1) * a.C + c] + (double)a.sync[((int64_t)r * 3 + 2) * a.C + c] * d * d;
   }
-  const double n = (double)a.Mtot;
   const double var = m2 / n;
   a.mean[c] = (float)mu;
   a.rstd[c] = (float)(1.0 / sqrt(var + a.eps));
@@ -523,17 +530,21 @@ __global__ __launch_bounds__(NT) void bn_sync_finalize_kernel(BnArgs a) {
 }
 
 // SyncBatchNorm backward: the global column sums (sum dpre, sum dpre * xhat) from the W
-// exchanged rank slots, in rank order, into the [2][C] region after the slots
+// exchanged rank slots, in rank order, each already scaled by 1 / N (N = sum of the ranks'
+// row counts, the same f32 product bn_bwd_apply_kernel forms with invM), into the [2][C]
+// region after the slots; the apply then runs with Mtot = 1
 __global__ __launch_bounds__(NT) void bn_bwd_sync_kernel(BnArgs a) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= a.C) return;
-  float s1 = 0.f, s2 = 0.f;
+  float s1 = 0.f, s2 = 0.f, n = 0.f;
   for (int r = 0; r < a.W; ++r) {
-    s1 += a.sync[((int64_t)r * 2 + 0) * a.C + c];
-    s2 += a.sync[((int64_t)r * 2 + 1) * a.C + c];
+    s1 += a.sync[((int64_t)r * 3 + 0) * a.C + c];
+    s2 += a.sync[((int64_t)r * 3 + 1) * a.C + c];
+    n += a.sync[((int64_t)r * 3 + 2) * a.C + c];
   }
-  a.sync[((int64_t)a.W * 2 + 0) * a.C + c] = s1;
-  a.sync[((int64_t)a.W * 2 + 1) * a.C + c] = s2;
+  const float invM = 1.f / n;
+  a.sync[((int64_t)a.W * 3 + 0) * a.C + c] = s1 * invM;
+  a.sync[((int64_t)a.W * 3 + 1) * a.C + c] = s2 * invM;
 }
 
 // per-column constants of 8 consecutive columns
@@ -659,8 +670,9 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(BnArgs a) {
   a.dgamma[c] = t2;
   if (a.sync) {
     for (int r2 = 0; r2 < a.W; ++r2) {
-      a.sync[((int64_t)r2 * 2 + 0) * a.C + c] = r2 == a.rank ? t1 : 0.f;
-      a.sync[((int64_t)r2 * 2 + 1) * a.C + c] = r2 == a.rank ? t2 : 0.f;
+      a.sync[((int64_t)r2 * 3 + 0) * a.C + c] = r2 == a.rank ? t1 : 0.f;
+      a.sync[((int64_t)r2 * 3 + 1) * a.C + c] = r2 == a.rank ? t2 : 0.f;
+      a.sync[((int64_t)r2 * 3 + 2) * a.C + c] = r2 == a.rank ? (float)a.M : 0.f;
     }
   }
 }
@@ -878,12 +890,12 @@ extern "C" int tt2_batchnorm_bwd(const tt2_bn_args* p, hipStream_t s) {
 }
 
 // ------------------------------------------------------------ SyncBatchNorm phases
-// The caller SUM-all-reduces the first W * 2 * C floats of sync_buf between the phases
+// The caller SUM-all-reduces the first W * 3 * C floats of sync_buf between the phases
 // (tt2/dist.py BnSync: RCCL in the captured step, or torch.distributed).  Every rank then
 // holds the same slots and computes the same global statistics in the same order.
 extern "C" size_t tt2_batchnorm_sync_size(const tt2_bn_args* p) {
   const int w = p->sync_world > 0 ? p->sync_world : 1;
-  return (size_t)(w + 1) * 2 * p->c * sizeof(float);
+  return (size_t)(3 * w + 2) * p->c * sizeof(float);
 }
 
 static int bn_sync_check(const tt2_bn_args* p, const char* what) {
@@ -900,7 +912,7 @@ static BnArgs bn_sync_args(const tt2_bn_args* p) {
   a.sync = p->sync_buf;
   a.W = p->sync_world;
   a.rank = p->sync_rank;
-  a.Mtot = (int64_t)p->sync_world * p->m;
+  a.Mtot = 1;   // the exchanged statistics carry each rank's row count (bn_*sync*_kernel)
   return a;
 }
 
@@ -951,7 +963,7 @@ extern "C" int tt2_batchnorm_bwd_apply(const tt2_bn_args* p, hipStream_t s) {
     return TT2_E_INVALID;
   BnArgs a = bn_sync_args(p);
   hipLaunchKernelGGL(bn_bwd_sync_kernel, dim3((p->c + NT - 1) / NT), dim3(NT), 0, s, a);
-  a.dbeta = a.sync + (int64_t)a.W * 2 * a.C;   // the apply reads the global sums
+  a.dbeta = a.sync + (int64_t)a.W * 3 * a.C;   // the apply reads the global sums / N
   a.dgamma = a.dbeta + a.C;
   const bool bf = p->dtype == TT2_DT_BF16, dbf = p->dout_dtype == TT2_DT_BF16;
   const int ga = grid_for((int64_t)p->m * p->c / 8);

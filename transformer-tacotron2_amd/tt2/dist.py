@@ -158,14 +158,22 @@ class RcclGradSync(GradSync):
         _lib.check(L.tt2_comm_init(C.byref(self.comm), self.world, uid, rank), "tt2_comm_init")
         self.stream = torch.cuda.Stream()
         self.pending = False
+        # test hook: snap_hook(lo, hi) runs with the comm stream current right after each
+        # bucket's all-reduce is issued (captured with it), e.g. to copy what RCCL produced
+        self.snap_hook = None
 
     def _launch(self, lo, hi):
+        if not (self.comm and self.comm.value):
+            raise RuntimeError("RcclGradSync: the communicator was closed")
         cur = torch.cuda.current_stream()
         self.stream.wait_stream(cur)          # the bucket's gradients are final on `cur`
         L = self._lib.lib()
         base = self.flat.data_ptr() + lo * self.flat.element_size()
         self._lib.check(L.tt2_allreduce_bucket(C.c_void_p(base), hi - lo, self._lib.dt(self.flat), self.comm,
                                                C.c_void_p(self.stream.cuda_stream)), "tt2_allreduce_bucket")
+        if self.snap_hook is not None:
+            with torch.cuda.stream(self.stream):
+                self.snap_hook(lo, hi)
         self.pending = True
 
     def finish(self):
@@ -181,6 +189,13 @@ class RcclGradSync(GradSync):
         self.pending = False
 
     def close(self):
+        """Destroy the communicator.  A BnSync sharing it (attach(sync_bn=True)) is detached
+        from the engine first, so no later step can issue a collective on a freed handle."""
+        eng = getattr(self, "engine", None)
+        if eng is not None and getattr(eng, "bn_sync", None) is not None and eng.bn_sync.grad_sync is self:
+            eng.bn_sync = None
+        if eng is not None and getattr(eng, "grad_ready_hook", None) == self.ready:
+            eng.grad_ready_hook = None
         if getattr(self, "comm", None) and self.comm.value:
             torch.cuda.synchronize()
             self._lib.check(self._lib.lib().tt2_comm_destroy(self.comm), "tt2_comm_destroy")
@@ -190,18 +205,32 @@ class RcclGradSync(GradSync):
 class BnSync:
     """SyncBatchNorm exchange (SURVEY.md:219, optional; per-replica statistics stay the
     default).  Each BatchNorm's forward moments and backward column sums leave the kernels as
-    [world][2][C] rank slots (this rank's values, zeros elsewhere: exact and rank-ordered once
-    summed), and ``exchange`` SUM-all-reduces them between the two kernel phases
-    (ops.batchnorm_fwd / _bwd with ``sync=``).  With libtt2's RCCL communicator the all-reduce
-    is issued on the current stream, so it is captured with the step (``in_graph``); with gloo
-    it is a blocking torch.distributed all-reduce, for eager steps only."""
+    [world][3][C] rank slots (this rank's values and its row count, zeros elsewhere: exact and
+    rank-ordered once summed, and ranks may hold different row counts), and ``exchange``
+    SUM-all-reduces them between the two kernel phases (ops.batchnorm_fwd / _bwd with
+    ``sync=``).
+
+    With libtt2's RCCL communicator (``grad_sync``: the RcclGradSync that owns it) the
+    all-reduce runs on the SAME comm stream as the gradient buckets, forked from and joined
+    back to the compute stream by stream waits: every collective on the communicator is then
+    issued from one stream in one program order on every rank (two streams sharing one
+    communicator may interleave differently per rank and deadlock), and it is captured with
+    the step (``in_graph``).  The exchange runs at world size 1 too (the identity), so a
+    one-GPU test executes the captured path itself.  With gloo it is a blocking
+    torch.distributed all-reduce, for eager steps only."""
     C_MAX = 2048   # tt2_batchnorm's channel limit
 
-    def __init__(self, world: int, rank: int, group=None, comm=None, device="cuda"):
-        self.world, self.rank, self.group, self.comm = world, rank, group, comm
-        self.in_graph = comm is not None
+    def __init__(self, world: int, rank: int, group=None, grad_sync=None, device="cuda"):
+        self.world, self.rank, self.group, self.grad_sync = world, rank, group, grad_sync
+        self.in_graph = grad_sync is not None
+        self.snap_hook = None   # test hook: called with the slots after each in-graph exchange
         # one buffer serves every BatchNorm: stats -> exchange -> apply run in stream order
-        self._buf = torch.zeros((world + 1) * 2 * self.C_MAX, dtype=torch.float32, device=device)
+        self._buf = torch.zeros((3 * world + 2) * self.C_MAX, dtype=torch.float32, device=device)
+
+    @property
+    def comm(self):
+        gs = self.grad_sync
+        return gs.comm if gs is not None and gs.comm.value else None
 
     def buffer(self, nbytes: int) -> torch.Tensor:
         n = (nbytes + 3) // 4
@@ -210,15 +239,21 @@ class BnSync:
         return self._buf[:n]
 
     def exchange(self, slots: torch.Tensor):
-        if self.world == 1:
-            return
-        if self.comm is not None:
+        if self.grad_sync is not None:
+            comm = self.comm
+            if comm is None:
+                raise RuntimeError("BnSync: the RCCL communicator was closed (RcclGradSync.close())")
             from . import _lib
             L = _lib.lib()
-            _lib.check(L.tt2_allreduce_bucket(C.c_void_p(slots.data_ptr()), slots.numel(), _lib.dt(slots), self.comm,
-                                              C.c_void_p(torch.cuda.current_stream().cuda_stream)),
-                       "tt2_allreduce_bucket")
-        else:
+            cur, cs = torch.cuda.current_stream(), self.grad_sync.stream
+            cs.wait_stream(cur)              # the stats kernel's slots are written on `cur`
+            _lib.check(L.tt2_allreduce_bucket(C.c_void_p(slots.data_ptr()), slots.numel(), _lib.dt(slots), comm,
+                                              C.c_void_p(cs.cuda_stream)), "tt2_allreduce_bucket")
+            if self.snap_hook is not None:
+                with torch.cuda.stream(cs):
+                    self.snap_hook(slots)
+            cur.wait_stream(cs)              # the apply kernel reads the reduced slots
+        elif self.world > 1:
             dist.all_reduce(slots, op=dist.ReduceOp.SUM, group=self.group)
 
 
@@ -265,9 +300,10 @@ def attach(model, group=None, bucket_bytes: int = 25 << 20, kind: str | None = N
     sync = cls(eng.grads, bucket_bytes, group)
     eng.grad_scale = 1.0 / sync.world
     eng.grad_ready_hook = sync.ready
+    sync.engine = eng
     if sync_bn:
         rank = dist.get_rank(group) if dist.is_initialized() else 0
-        eng.bn_sync = BnSync(sync.world, rank, group, comm=sync.comm if kind == "rccl" else None, device=eng.dev)
+        eng.bn_sync = BnSync(sync.world, rank, group, grad_sync=sync if kind == "rccl" else None, device=eng.dev)
     return sync
 
 

@@ -379,7 +379,7 @@ def _bn_sync_into(L, a, sync):
     a.sync_world, a.sync_rank = sync.world, sync.rank
     buf = sync.buffer(L.tt2_batchnorm_sync_size(C.byref(a)))
     a.sync_buf = buf.data_ptr()
-    return buf[:sync.world * 2 * a.c]
+    return buf[:sync.world * 3 * a.c]
 
 
 def batchnorm_fwd(y, gamma, beta, mean, rstd, run_mean, run_var, out, m, c, act, training, drop: Drop = NO_DROP,
