@@ -167,6 +167,11 @@ class RcclGradSync(GradSync):
             raise RuntimeError("RcclGradSync: the communicator was closed")
         cur = torch.cuda.current_stream()
         self.stream.wait_stream(cur)          # the bucket's gradients are final on `cur`
+        if self._span is None and not torch.cuda.is_current_stream_capturing():
+            # eager step: the exchange's span on the comm stream, from the first bucket's start
+            # to finish() (StepMetrics' allreduce_ms; a captured step records no events)
+            self._span = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+            self._span[0].record(self.stream)
         L = self._lib.lib()
         base = self.flat.data_ptr() + lo * self.flat.element_size()
         self._lib.check(L.tt2_allreduce_bucket(C.c_void_p(base), hi - lo, self._lib.dt(self.flat), self.comm,
@@ -180,6 +185,9 @@ class RcclGradSync(GradSync):
         while self.next < len(self.buckets):
             self._launch(*self.buckets[self.next])
             self.next += 1
+        if self._span is not None and len(self._span) == 2:
+            self._span[1].record(self.stream)
+            self._done_span, self._span = tuple(self._span), None
         if self.pending:
             torch.cuda.current_stream().wait_stream(self.stream)
         self.reset()
@@ -187,6 +195,13 @@ class RcclGradSync(GradSync):
     def reset(self):
         super().reset()
         self.pending = False
+        if not hasattr(self, "_span"):
+            self._span, self._done_span = None, None
+
+    def pop_span(self):
+        """(start, end) events of the last eager step's all-reduces on the comm stream."""
+        s, self._done_span = self._done_span, None
+        return s
 
     def close(self):
         """Destroy the communicator.  A BnSync sharing it (attach(sync_bn=True)) is detached

@@ -28,6 +28,7 @@ shadow the kernels read is refreshed at the next forward (version-counter check)
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -95,6 +96,9 @@ class TransformerTTS(nn.Module):
         self._graphs: dict = {}
         self._loss_bufs: dict = {}
         self._slot_names = list(e.lay.slots)
+        self.metrics = None   # StepMetrics (enable_metrics / TT2_METRICS): one JSONL line per step
+        if os.environ.get("TT2_METRICS"):
+            self.enable_metrics(os.environ["TT2_METRICS"])
         # parameters alias the flat master buffer (in-place optimizer updates land in it)
         self.slots = nn.ParameterDict({n.replace(".", "__"): nn.Parameter(e.P(n)) for n in self._slot_names})
         # the autograd Function's inputs and returned gradients follow the ParameterDict's order
@@ -346,15 +350,35 @@ class TransformerTTS(nn.Module):
             sync_grads()
         e.optimizer_step()
 
+    def enable_metrics(self, path: str | None, world: int | None = None):
+        """Per-step JSONL metrics (tt2/metrics.py) appended to `path`; None turns them off.
+        world: ranks whose frames count in frames/s (default: torch.distributed's world)."""
+        from .metrics import StepMetrics
+        if self.metrics is not None:
+            self.metrics.close()
+            self.metrics = None
+        if path:
+            if world is None:
+                import torch.distributed as dist
+                world = dist.get_world_size() if dist.is_initialized() else 1
+            self.metrics = StepMetrics(path, self.cfg, world)
+
+    def _metrics_end(self, A: Arena, sync_grads):
+        self.metrics.end(A["loss"], A.B, A.Tx, A.Ty, sync=getattr(sync_grads, "__self__", None))
+
     def train_step(self, text, text_len, mel, mel_len, sync_grads=None):
         """One optimisation step, eagerly.  Returns the device loss vector
         [total, mse_before, mse_after, bce_stop] (no host sync)."""
         if self.engine.exp_avg is None:
             self.engine.init_optimizer()
+        if self.metrics is not None:
+            self.metrics.begin()
         self._sync_shadow()
         A = self._stage(text, text_len, mel, mel_len)
         self._step_body(A, sync_grads)
         self._last = A
+        if self.metrics is not None:
+            self._metrics_end(A, sync_grads)
         return A["loss"]
 
     def capture_train_step(self, B: int, Tx: int, Ty: int, sync_grads=None):
@@ -420,6 +444,8 @@ class TransformerTTS(nn.Module):
         self._graphs[(B, Tx, Ty)] = (segs, g2)
 
         def run(text, text_len, mel, mel_len):
+            if self.metrics is not None:
+                self.metrics.begin()
             e.stage_inputs(A, text, text_len.to(torch.int32), mel, mel_len.to(torch.int32))
             for g, idx in segs:
                 g.replay()
@@ -431,6 +457,8 @@ class TransformerTTS(nn.Module):
             for k in e.nbt:
                 e.nbt[k] += 1
             self._last = A
+            if self.metrics is not None:
+                self._metrics_end(A, sync_grads)
             return A["loss"]
 
         return run
@@ -461,11 +489,15 @@ class TransformerTTS(nn.Module):
         self._graphs[(A.B, A.Tx, A.Ty)] = ([(g, [])], None)
 
         def run(text, text_len, mel, mel_len):
+            if self.metrics is not None:
+                self.metrics.begin()
             e.stage_inputs(A, text, text_len.to(torch.int32), mel, mel_len.to(torch.int32))
             g.replay()
             for k in e.nbt:
                 e.nbt[k] += 1
             self._last = A
+            if self.metrics is not None:
+                self.metrics.end(A["loss"], A.B, A.Tx, A.Ty)   # the all-reduce span is inside the graph
             return A["loss"]
 
         return run
