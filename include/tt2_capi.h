@@ -158,6 +158,10 @@ float tt2_probe_span_ms(int slot);
  * number of work groups, -groups - 1 if cap is too small, -1 if the slot has no record.  Read
  * it before tt2_probe_span_ms, which clears the record. */
 int tt2_probe_span_records(int slot, unsigned long long* out, int cap);
+/* u64 slots per work group in tt2_probe_span_records' output: 2 ({start, end}); 32 in the
+ * in-step GEMM phase build (-DTT2_PHASE=1, tools/g7_phases.py: s_memtime stamps of the K
+ * steps and the epilogue after the pair). */
+int tt2_probe_span_width(void);
 void tt2_probe_reset(void);
 
 /* ---------------------------------------------------------------- attention

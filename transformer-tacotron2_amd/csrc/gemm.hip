@@ -47,7 +47,16 @@ thread_local int g_probe_armed = -1;
 // added to the stream, so the span of a launch inside a replayed step graph is its in-step
 // duration, with no event node (and its dispatch gap) around it.  Records come from one
 // pool per thread, allocated (zeroed) by the first tt2_probe_arm, outside any capture.
+// Record width per work group: {start, end}; the in-step phase build (TT2_PHASE) adds
+// s_memtime stamps (slot 2: entry; 3 + 2t / 4 + 2t: K step t's start / after its MFMAs,
+// t < 12; 27..30: the epilogue's points, G7_STAMP; 31: the last wave's stores drained).
+#ifdef TT2_PHASE
+#define TT2_SPAN_W 32
+constexpr int64_t PROBE_SPAN_PAIRS = 1 << 17;
+#else
+#define TT2_SPAN_W 2
 constexpr int64_t PROBE_SPAN_PAIRS = 1 << 20;
+#endif
 thread_local unsigned long long* g_span = nullptr;
 thread_local int64_t g_span_used = 0;
 thread_local std::vector<std::pair<int64_t, int>> g_span_rec;   // per slot: pool offset, work groups
@@ -61,7 +70,7 @@ int probe_take(hipEvent_t& e0, hipEvent_t& e1, unsigned long long*& span, int gr
   e1 = p.stop;
   p.used = true;
   if (g_span && groups > 0 && g_span_used + groups <= PROBE_SPAN_PAIRS) {
-    span = g_span + 2 * g_span_used;
+    span = g_span + TT2_SPAN_W * g_span_used;
     g_span_rec[slot] = {g_span_used, groups};
     g_span_used += groups;
   }
@@ -73,7 +82,10 @@ TT2_DEV void span_begin(unsigned long long* span, int* done) {
   if (span && threadIdx.x == 0) {
     *done = 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // visible before the first barrier
-    span[2 * blockIdx.x] = wall_clock64();
+    span[TT2_SPAN_W * blockIdx.x] = wall_clock64();
+#ifdef TT2_PHASE
+    span[TT2_SPAN_W * blockIdx.x + 2] = __builtin_amdgcn_s_memtime();
+#endif
   }
 }
 // every wave once its own stores have completed (stores count in vmcnt on gfx9); the last
@@ -81,7 +93,12 @@ TT2_DEV void span_begin(unsigned long long* span, int* done) {
 TT2_DEV void span_end(unsigned long long* span, int* done, int waves) {
   if (span) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if ((threadIdx.x & 63) == 0 && atomicAdd(done, 1) == waves - 1) span[2 * blockIdx.x + 1] = wall_clock64();
+    if ((threadIdx.x & 63) == 0 && atomicAdd(done, 1) == waves - 1) {
+#ifdef TT2_PHASE
+      span[TT2_SPAN_W * blockIdx.x + 31] = __builtin_amdgcn_s_memtime();
+#endif
+      span[TT2_SPAN_W * blockIdx.x + 1] = wall_clock64();
+    }
   }
 }
 
@@ -946,7 +963,17 @@ TT2_DEV void g7_frag(Frag8<bf16>& f, const char* img, int r0, int kk, int lane) 
 }
 
 // Measurement hook: tools/gemm_stamps.hip defines these (and the buffer they write)
-// before including this file; the library build compiles them away.
+// before including this file; the library build compiles them away.  The in-step phase
+// build (-DTT2_PHASE=1, tools/g7_phases.py) writes them into the launch probe's per-work-group
+// record (TT2_SPAN_W slots, layout at span_begin): s_memtime of MFMA wave 0 at the start of
+// K steps 0..11 and after their MFMAs, and at the epilogue's four points.
+#if defined(TT2_PHASE) && !defined(G7_STAMP)
+#define G7_STAMP(t, slot)                                                                  \
+  if (srec && threadIdx.x == 0) {                                                          \
+    const int si_ = (t) == nkt ? 27 + (slot) : (t) < 12 ? 3 + 2 * (t) + (slot) : -1;        \
+    if (si_ >= 0) srec[si_] = __builtin_amdgcn_s_memtime();                                \
+  }
+#endif
 #ifndef G7_STAMP
 #define G7_STAMP(t, slot)
 #endif
@@ -1200,7 +1227,12 @@ TT2_DEV void g7_epi_fast(const EpiParams& E, const f32x4 (&acc)[4][4], const f32
 }
 
 template <bool AK, bool BKC>
-TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem) {
+TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem, unsigned long long* span) {
+#ifdef TT2_PHASE
+  unsigned long long* srec = span ? span + TT2_SPAN_W * blockIdx.x : nullptr;
+#else
+  (void)span;
+#endif
   const OpDesc& A = P.A;
   const OpDesc& B = P.B;
   const EpiParams& E = P.E;
@@ -1465,7 +1497,7 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(G7Prob P) {
   G7_RT(0)
   span_begin(P.span, &span_done);
   const int u = xcd_item(blockIdx.x, P.items);
-  g7_item<AK, BKC>(P, u % (P.items / P.splits), u / (P.items / P.splits), smem);
+  g7_item<AK, BKC>(P, u % (P.items / P.splits), u / (P.items / P.splits), smem, P.span);
   span_end(P.span, &span_done, G7_NT / 64);
   G7_RT(1)
 }
@@ -1484,7 +1516,7 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7g_kernel(G7Group G) {
     if (i < G.np && u >= G.p[i].item0) p = i;
   const G7Prob& P = G.p[p];
   const int local = u - P.item0, nt = P.items / P.splits;
-  g7_item<AK, BKC>(P, local % nt, local / nt, smem);
+  g7_item<AK, BKC>(P, local % nt, local / nt, smem, G.p[0].span);
   span_end(G.p[0].span, &span_done, G7_NT / 64);
 }
 
@@ -1783,7 +1815,11 @@ __global__ __launch_bounds__(G10_NT, 1) void gemm10_kernel(OpDesc A, OpDesc B, E
   constexpr bool BIAS = CODE & 1, RELU = CODE & 2, DROP = CODE & 4;
   __shared__ __attribute__((aligned(1024))) char smem[G10_SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (span && tid == 0) span[2 * blockIdx.x] = wall_clock64();
+  if (span && tid == 0) span[TT2_SPAN_W * blockIdx.x] = wall_clock64();
+#ifdef TT2_PHASE
+  unsigned long long* srec = span ? span + TT2_SPAN_W * blockIdx.x : nullptr;
+  if (srec && tid == 0) srec[2] = __builtin_amdgcn_s_memtime();
+#endif
   const int tile = xcd_item(blockIdx.x, items);
   const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
   const int nkt = K / 64, nit = 2 * nkt;   // ring items: A_t = 2 t, B_t = 2 t + 1
@@ -1824,6 +1860,7 @@ __global__ __launch_bounds__(G10_NT, 1) void gemm10_kernel(OpDesc A, OpDesc B, E
     uint64_t dbits[2] = {0, 0};
     __builtin_amdgcn_s_barrier();
     for (int t = 0; t < nkt; ++t) {
+      G7_STAMP(t, 0)
       const char* sa = smem + ((2 * t) % G10_SLOTS) * G10_SLOT;
       const char* sb = smem + ((2 * t + 1) % G10_SLOTS) * G10_SLOT;
 #pragma unroll
@@ -1848,9 +1885,11 @@ __global__ __launch_bounds__(G10_NT, 1) void gemm10_kernel(OpDesc A, OpDesc B, E
           dbits[gi >> 3] |= kb << (8 * (gi & 7));
         }
       }
+      G7_STAMP(t, 1)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this step's reads retired (WAR vs its slots)
       __builtin_amdgcn_s_barrier();
     }
+    G7_STAMP(nkt, 0)
     // epilogue: alpha, bias, ReLU, dropout (v7's order) into the C image (the ring is free)
     f32x4 pbias[2][2];
 #pragma unroll
@@ -1897,8 +1936,10 @@ __global__ __launch_bounds__(G10_NT, 1) void gemm10_kernel(OpDesc A, OpDesc B, E
         *reinterpret_cast<bf16x8*>(smem + g10_img(r, cl)) = x;
       }
     }
+    G7_STAMP(nkt, 1)
   }
   __syncthreads();   // the C image is complete: all 12 waves store whole 256-B row segments
+  if (wave == 0) { G7_STAMP(nkt, 2) }
   bf16* C = reinterpret_cast<bf16*>(E.c);
   for (int id = tid; id < 256 * 32; id += G10_NT) {
     const int half = id >> 12, r = (id >> 4) & 255, c = id & 15;
@@ -1907,10 +1948,14 @@ __global__ __launch_bounds__(G10_NT, 1) void gemm10_kernel(OpDesc A, OpDesc B, E
       __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(smem + half * 65536 + r * 256 + ((c ^ (r & 15)) << 4)),
                                   reinterpret_cast<u32x4*>(C + (int64_t)mm * E.ldc + nn));
   }
+  if (wave == 0) { G7_STAMP(nkt, 3) }
   if (span) {   // every wave's stores completed, then one end stamp
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) span[2 * blockIdx.x + 1] = wall_clock64();
+#ifdef TT2_PHASE
+    if (tid == 0) span[TT2_SPAN_W * blockIdx.x + 31] = __builtin_amdgcn_s_memtime();
+#endif
+    if (tid == 0) span[TT2_SPAN_W * blockIdx.x + 1] = wall_clock64();
   }
 }
 
@@ -2254,8 +2299,8 @@ extern "C" int tt2_probe_arm(void) {
   ProbeSlot p{nullptr, nullptr, false};
   hipError_t e = hipSuccess;
   if (!g_span) {
-    e = hipMalloc(&g_span, 2 * sizeof(unsigned long long) * PROBE_SPAN_PAIRS);
-    if (e == hipSuccess) e = hipMemset(g_span, 0, 2 * sizeof(unsigned long long) * PROBE_SPAN_PAIRS);
+    e = hipMalloc(&g_span, TT2_SPAN_W * sizeof(unsigned long long) * PROBE_SPAN_PAIRS);
+    if (e == hipSuccess) e = hipMemset(g_span, 0, TT2_SPAN_W * sizeof(unsigned long long) * PROBE_SPAN_PAIRS);
     if (e != hipSuccess) {
       if (g_span) (void)hipFree(g_span);
       g_span = nullptr;
@@ -2283,16 +2328,17 @@ extern "C" float tt2_probe_span_ms(int slot) {
   if (slot < 0 || slot >= (int)g_probe.size() || !g_probe[slot].used || g_span_rec[slot].first < 0) return -1.f;
   const int64_t off = g_span_rec[slot].first;
   const int groups = g_span_rec[slot].second;
-  std::vector<unsigned long long> h(2 * (size_t)groups);
+  std::vector<unsigned long long> h(TT2_SPAN_W * (size_t)groups);
   if (hipDeviceSynchronize() != hipSuccess) return -1.f;
-  if (hipMemcpy(h.data(), g_span + 2 * off, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1.f;
+  if (hipMemcpy(h.data(), g_span + TT2_SPAN_W * off, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1.f;
   // zeroed again, so the next replay of a graph must record every pair afresh
-  if (hipMemset(g_span + 2 * off, 0, h.size() * 8) != hipSuccess) return -1.f;
+  if (hipMemset(g_span + TT2_SPAN_W * off, 0, h.size() * 8) != hipSuccess) return -1.f;
   unsigned long long t0 = ~0ull, t1 = 0;
   for (int i = 0; i < groups; ++i) {
-    if (h[2 * i] == 0 || h[2 * i + 1] < h[2 * i]) return -1.f;   // a work group left no record
-    t0 = std::min(t0, h[2 * i]);
-    t1 = std::max(t1, h[2 * i + 1]);
+    const unsigned long long s0 = h[TT2_SPAN_W * i], s1 = h[TT2_SPAN_W * i + 1];
+    if (s0 == 0 || s1 < s0) return -1.f;   // a work group left no record
+    t0 = std::min(t0, s0);
+    t1 = std::max(t1, s1);
   }
   static int khz = 0;
   if (!khz) {
@@ -2313,13 +2359,18 @@ extern "C" int tt2_probe_span_records(int slot, unsigned long long* out, int cap
   const int groups = g_span_rec[slot].second;
   if (cap < groups) return -groups - 1;
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpy(out, g_span + 2 * off, (size_t)groups * 16, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hipMemcpy(out, g_span + TT2_SPAN_W * off, (size_t)groups * TT2_SPAN_W * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
   return groups;
 }
 
+// u64 slots per work group in tt2_probe_span_records' output: 2 ({start, end} on the wall
+// clock), 32 in the in-step phase build (TT2_PHASE, see TT2_SPAN_W)
+extern "C" int tt2_probe_span_width(void) { return TT2_SPAN_W; }
+
 extern "C" void tt2_probe_reset(void) {
   // records of slots never read are zeroed so the pool can be handed out again
-  if (g_span && g_span_used) (void)hipMemset(g_span, 0, 2 * sizeof(unsigned long long) * g_span_used);
+  if (g_span && g_span_used) (void)hipMemset(g_span, 0, TT2_SPAN_W * sizeof(unsigned long long) * g_span_used);
   g_span_used = 0;
   g_span_rec.clear();
   for (ProbeSlot& p : g_probe) {

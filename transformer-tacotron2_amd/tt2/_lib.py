@@ -69,6 +69,7 @@ SIGNATURES: dict[str, tuple[list, object]] = {
     "tt2_probe_ms": ([C.c_int], C.c_float),
     "tt2_probe_span_ms": ([C.c_int], C.c_float),
     "tt2_probe_span_records": ([C.c_int, C.POINTER(C.c_uint64), C.c_int], C.c_int),
+    "tt2_probe_span_width": ([], C.c_int),
     "tt2_probe_reset": ([], None),
 }
 
