@@ -34,7 +34,7 @@ class SimSync:
 
     def __init__(self, world, rank, others=()):
         self.world, self.rank, self.others = world, rank, list(others)
-        self.buf = torch.zeros((3 * world + 2) * 2048, device="cuda")
+        self.buf = torch.zeros((3 * world + 2) * 2048 + 4, device="cuda")
         self.sent = None
 
     def buffer(self, nbytes):

@@ -352,7 +352,8 @@ struct BnArgs {
   // caller) + [2][C]
   float* sync;
   int W, rank;
-  int64_t Mtot;   // rows behind the statistics: M (1 in the SyncBN apply: sums arrive divided)
+  int64_t Mtot;   // rows behind the statistics: M (SyncBN: the exchanged counts, see inv_m)
+  const float* inv_m;   // SyncBN backward apply: 1 / (sum of the ranks' rows), written by bn_bwd_sync_kernel
 };
 
 // tanh through one v_exp_f32 and one v_rcp_f32 (ocml's tanhf is a long branchy sequence and
@@ -530,9 +531,9 @@ __global__ __launch_bounds__(NT) void bn_sync_finalize_kernel(BnArgs a) {
 }
 
 // SyncBatchNorm backward: the global column sums (sum dpre, sum dpre * xhat) from the W
-// exchanged rank slots, in rank order, each already scaled by 1 / N (N = sum of the ranks'
-// row counts, the same f32 product bn_bwd_apply_kernel forms with invM), into the [2][C]
-// region after the slots; the apply then runs with Mtot = 1
+// exchanged rank slots, in rank order, into the [2][C] region after the slots, and
+// 1 / N (N = sum of the ranks' row counts, as f32: the value bn_bwd_apply_kernel forms from
+// Mtot on one rank, so one SyncBN rank reproduces plain BatchNorm bit for bit) after them
 __global__ __launch_bounds__(NT) void bn_bwd_sync_kernel(BnArgs a) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= a.C) return;
@@ -542,9 +543,9 @@ __global__ __launch_bounds__(NT) void bn_bwd_sync_kernel(BnArgs a) {
     s2 += a.sync[((int64_t)r * 3 + 1) * a.C + c];
     n += a.sync[((int64_t)r * 3 + 2) * a.C + c];
   }
-  const float invM = 1.f / n;
-  a.sync[((int64_t)a.W * 3 + 0) * a.C + c] = s1 * invM;
-  a.sync[((int64_t)a.W * 3 + 1) * a.C + c] = s2 * invM;
+  a.sync[((int64_t)a.W * 3 + 0) * a.C + c] = s1;
+  a.sync[((int64_t)a.W * 3 + 1) * a.C + c] = s2;
+  if (c == 0) a.sync[((int64_t)a.W * 3 + 2) * a.C] = 1.f / n;
 }
 
 // per-column constants of 8 consecutive columns
@@ -684,7 +685,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
   const T* y = reinterpret_cast<const T*>(a.y);
   const TD* dout = reinterpret_cast<const TD*>(a.dout);
   const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
-  const float invM = 1.f / (float)a.Mtot;
+  const float invM = a.inv_m ? *a.inv_m : 1.f / (float)a.Mtot;
   for (int q = blockIdx.x * NT + threadIdx.x; q < nq; q += gridDim.x * NT) {
     const int m = q / CG, c0 = (q - m * CG) * 8;
     const int64_t i0 = (int64_t)m * a.C + c0;
@@ -895,7 +896,7 @@ extern "C" int tt2_batchnorm_bwd(const tt2_bn_args* p, hipStream_t s) {
 // holds the same slots and computes the same global statistics in the same order.
 extern "C" size_t tt2_batchnorm_sync_size(const tt2_bn_args* p) {
   const int w = p->sync_world > 0 ? p->sync_world : 1;
-  return (size_t)(3 * w + 2) * p->c * sizeof(float);
+  return ((size_t)(3 * w + 2) * p->c + 4) * sizeof(float);   // + 1 / N (padded to 16 B)
 }
 
 static int bn_sync_check(const tt2_bn_args* p, const char* what) {
@@ -912,7 +913,7 @@ static BnArgs bn_sync_args(const tt2_bn_args* p) {
   a.sync = p->sync_buf;
   a.W = p->sync_world;
   a.rank = p->sync_rank;
-  a.Mtot = 1;   // the exchanged statistics carry each rank's row count (bn_*sync*_kernel)
+  a.Mtot = 1;   // unused: the exchanged statistics carry each rank's row count (bn_*sync*_kernel, inv_m)
   return a;
 }
 
@@ -963,8 +964,9 @@ extern "C" int tt2_batchnorm_bwd_apply(const tt2_bn_args* p, hipStream_t s) {
     return TT2_E_INVALID;
   BnArgs a = bn_sync_args(p);
   hipLaunchKernelGGL(bn_bwd_sync_kernel, dim3((p->c + NT - 1) / NT), dim3(NT), 0, s, a);
-  a.dbeta = a.sync + (int64_t)a.W * 3 * a.C;   // the apply reads the global sums / N
+  a.dbeta = a.sync + (int64_t)a.W * 3 * a.C;   // the apply reads the global sums and 1 / N
   a.dgamma = a.dbeta + a.C;
+  a.inv_m = a.dgamma + a.C;
   const bool bf = p->dtype == TT2_DT_BF16, dbf = p->dout_dtype == TT2_DT_BF16;
   const int ga = grid_for((int64_t)p->m * p->c / 8);
   TT2_BN_DISPATCH2(bn_bwd_apply_kernel, dim3(ga), a)

@@ -240,7 +240,7 @@ class BnSync:
         self.in_graph = grad_sync is not None
         self.snap_hook = None   # test hook: called with the slots after each in-graph exchange
         # one buffer serves every BatchNorm: stats -> exchange -> apply run in stream order
-        self._buf = torch.zeros((3 * world + 2) * self.C_MAX, dtype=torch.float32, device=device)
+        self._buf = torch.zeros((3 * world + 2) * self.C_MAX + 4, dtype=torch.float32, device=device)
 
     @property
     def comm(self):
