@@ -170,18 +170,22 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
   const int k0 = w * per, k1 = min(nk, k0 + per);
   const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)b * a.k_bstride + h * D + dc * 8;
   const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)b * a.v_bstride + h * D + dc * 8;
-  float kv[U][8], vv[U][8];
-  // every load of an iteration first (clamped to the last valid key: branch-free)
-  auto load_keys = [&](int kb) {
+  // two register buffers of raw K / V rows: the loads of iteration i + 1 are issued before
+  // iteration i's arithmetic, so a wave's key range costs one memory round trip plus its
+  // arithmetic instead of one round trip per iteration
+  typedef T t8 __attribute__((ext_vector_type(8)));
+  t8 kr[2][U], vr[2][U];
+  // every load of an iteration at once (clamped to the last valid key: branch-free)
+  auto load_keys = [&](int kb, int buf) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int key = min(kb + 8 * u + kg, k1 - 1);
-      load8f(K + (int64_t)key * a.k_ld, kv[u]);
-      load8f(V + (int64_t)key * a.v_ld, vv[u]);
+      kr[buf][u] = *reinterpret_cast<const t8*>(K + (int64_t)key * a.k_ld);
+      vr[buf][u] = *reinterpret_cast<const t8*>(V + (int64_t)key * a.v_ld);
     }
   };
   // the first iteration's keys do not depend on the query: in flight during its projection
-  if (k0 < k1) load_keys(k0);
+  if (k0 < k1) load_keys(k0, 0);
   float qv[8];
   if (a.wq) {
     float wv[8][8];
@@ -198,8 +202,18 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
     load8f(reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld + h * D + dc * 8, qv);
   }
   float m = -INFINITY, l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int kb = k0; kb < k1; kb += 8 * U) {
-    if (kb != k0) load_keys(kb);
+  // one iteration on register buffer BUF (compile-time, so the buffers stay in registers)
+  auto iter = [&](auto BUFC, int kb) {
+    constexpr int BUF = decltype(BUFC)::value;
+    if (kb + 8 * U < k1) load_keys(kb + 8 * U, BUF ^ 1);
+    float kv[U][8], vv[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        kv[u][j] = (float)kr[BUF][u][j];
+        vv[u][j] = (float)vr[BUF][u][j];
+      }
     float s[U];
     float mx = -INFINITY;
 #pragma unroll
@@ -229,6 +243,10 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
       for (int j = 0; j < 8; ++j) o[j] += p * vv[u][j];
     }
     m = mn;
+  };
+  for (int kb = k0; kb < k1; kb += 16 * U) {
+    iter(std::integral_constant<int, 0>{}, kb);
+    if (kb + 8 * U < k1) iter(std::integral_constant<int, 1>{}, kb + 8 * U);
   }
   // combine the 8 key slots (same m across the wave)
 #pragma unroll

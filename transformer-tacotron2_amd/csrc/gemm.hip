@@ -1509,14 +1509,19 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7g_kernel(G7Group G) {
   __shared__ __attribute__((aligned(1024))) char smem[G7_SMEM];
   __shared__ int span_done;
   span_begin(G.p[0].span, &span_done);
-  const int u = xcd_item(blockIdx.x, G.items);
-  int p = 0;
+  // a capped grid (tt2_gemm_grouped_ex, gridDim.x a multiple of 8 below G.items) walks the
+  // items: block b takes b, b + gridDim.x, ... (same XCD); uncapped, one item per block
+  for (int bi = blockIdx.x; bi < G.items; bi += gridDim.x) {
+    const int u = xcd_item(bi, G.items);
+    int p = 0;
 #pragma unroll
-  for (int i = 1; i < G7_MAXP; ++i)
-    if (i < G.np && u >= G.p[i].item0) p = i;
-  const G7Prob& P = G.p[p];
-  const int local = u - P.item0, nt = P.items / P.splits;
-  g7_item<AK, BKC>(P, local % nt, local / nt, smem, G.p[0].span);
+    for (int i = 1; i < G7_MAXP; ++i)
+      if (i < G.np && u >= G.p[i].item0) p = i;
+    const G7Prob& P = G.p[p];
+    const int local = u - P.item0, nt = P.items / P.splits;
+    g7_item<AK, BKC>(P, local % nt, local / nt, smem, G.p[0].span);
+    if (bi + (int)gridDim.x < G.items) __syncthreads();   // the epilogue's LDS image is read out
+  }
   span_end(G.p[0].span, &span_done, G7_NT / 64);
 }
 
@@ -2224,6 +2229,11 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
 
 extern "C" int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int n, const tt2_ln_args* fin,
                                     hipStream_t stream) {
+  return tt2_gemm_grouped_ex(probs, n, fin, 0, stream);
+}
+
+extern "C" int tt2_gemm_grouped_ex(const tt2_gemm_args* probs, int n, const tt2_ln_args* fin, int max_groups,
+                                   hipStream_t stream) {
   ProbeDisarm disarm;
   if (n <= 0 && !fin) return TT2_OK;
   if ((n > 0 && !probs) || n > G7_MAXP) return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: 1..8 problems");
@@ -2266,19 +2276,22 @@ extern "C" int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int n, const tt2
     if (fin_blocks) hipLaunchKernelGGL(gemm_splitk_reduce_g, dim3(fin_blocks, 1), dim3(256), 0, stream, G);
     return tt2_check_launch(hipGetLastError(), "tt2_gemm_grouped");
   }
-  ProbeScope ps(stream, G.items);
+  // max_groups > 0: at most that many work groups (rounded down to a multiple of 8, >= 8), each
+  // walking several items, so a launch beside other work leaves the rest of the CUs free
+  const int grid = max_groups > 0 ? std::min(G.items, std::max(8, max_groups / 8 * 8)) : G.items;
+  ProbeScope ps(stream, grid);
   G.p[0].span = ps.span;
   if (ps.ext()) {
-#define TT2_G7G(A_, B_) hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_>), dim3(G.items), dim3(G7_NT), 0, stream, ps.e0, ps.e1, 0, G)
+#define TT2_G7G(A_, B_) hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_>), dim3(grid), dim3(G7_NT), 0, stream, ps.e0, ps.e1, 0, G)
     if (!ta && !tb) TT2_G7G(true, true);
     else if (!ta && tb) TT2_G7G(true, false);
     else if (ta && !tb) TT2_G7G(false, true);
     else TT2_G7G(false, false);
 #undef TT2_G7G
-  } else if (!ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<true, true>), dim3(G.items), dim3(G7_NT), 0, stream, G);
-  else if (!ta && tb) hipLaunchKernelGGL((gemm7g_kernel<true, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
-  else if (ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<false, true>), dim3(G.items), dim3(G7_NT), 0, stream, G);
-  else hipLaunchKernelGGL((gemm7g_kernel<false, false>), dim3(G.items), dim3(G7_NT), 0, stream, G);
+  } else if (!ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<true, true>), dim3(grid), dim3(G7_NT), 0, stream, G);
+  else if (!ta && tb) hipLaunchKernelGGL((gemm7g_kernel<true, false>), dim3(grid), dim3(G7_NT), 0, stream, G);
+  else if (ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<false, true>), dim3(grid), dim3(G7_NT), 0, stream, G);
+  else hipLaunchKernelGGL((gemm7g_kernel<false, false>), dim3(grid), dim3(G7_NT), 0, stream, G);
   if (main_only) reduce_blocks = 0;
   G.fin_only = reduce_blocks == 0 && fin_blocks > 0;
   if (G.fin_only)

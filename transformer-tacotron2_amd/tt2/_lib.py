@@ -65,6 +65,7 @@ SIGNATURES: dict[str, tuple[list, object]] = {
     "tt2_gemm_plan": ([C.POINTER(GemmArgs)], C.c_int),
     "tt2_gemm_grouped": ([C.POINTER(GemmArgs), C.c_int32, vp], C.c_int),
     "tt2_gemm_grouped_fin": ([C.POINTER(GemmArgs), C.c_int32, vp, vp], C.c_int),
+    "tt2_gemm_grouped_ex": ([C.POINTER(GemmArgs), C.c_int32, vp, C.c_int32, vp], C.c_int),
     "tt2_probe_arm": ([], C.c_int),
     "tt2_probe_ms": ([C.c_int], C.c_float),
     "tt2_probe_span_ms": ([C.c_int], C.c_float),

@@ -187,6 +187,16 @@ class Arena:
             self[k]
         return self
 
+    def layer_buf(self, name: str, key, shape=None) -> torch.Tensor:
+        """A per-layer copy `name@key` of gradient scratch buffer `name` (optionally of another
+        shape): the overlapped backward (TTSEngine.wgrad_overlap) keeps each layer's weight-
+        gradient dY alive until the side stream has used it."""
+        full = f"{name}@{key}"
+        if full not in self.spec:
+            shp, dt, zero = self.spec[name]
+            self.spec[full] = (tuple(shape) if shape is not None else shp, dt, zero)
+        return self[full]
+
 
 class TTSEngine:
     def __init__(self, cfg: TTSConfig | None = None, dtype: torch.dtype = torch.bfloat16, device="cuda",
@@ -203,6 +213,20 @@ class TTSEngine:
         self.ln_fin_in_reduce = os.environ.get("TT2_LN_FIN_REDUCE", "1") != "0"
         self._wq = None   # weight-gradient requests queued for one grouped launch (see _defer_wgrads)
         self.wflip_batch = os.environ.get("TT2_WFLIP_BATCH", "1") != "0"
+        # bf16 backward: every weight-gradient GEMM (and the DP hook of its bucket) runs on a side
+        # stream that starts with the encoder backward, whose small latency-bound launches leave
+        # most of the chip idle; the decoder / post-net dgrad chain no longer waits for them
+        # (see backward).  Off: each layer's weight gradients run in place, as before.
+        self.wgrad_overlap = os.environ.get("TT2_WGRAD_OVERLAP", "1") != "0"
+        self._jobs = None    # overlapped backward: queued weight-gradient jobs (see _push_job)
+        self._side = None
+        self._side_ws = None
+        self._side_live = False
+        self._ln_parts_l = {}   # per-layer partials of the deferred last LayerNorm of a layer
+        # side-stream weight-gradient launches: split-K factor multiplier (shorter work items)
+        # and work-group cap (0: none), dev knobs for the overlap's A/B
+        self.side_split = int(os.environ.get("TT2_SIDE_SPLIT", "1"))
+        self.side_groups = int(os.environ.get("TT2_SIDE_WG", "0"))
         self.cd = dtype
         self.dev = torch.device(device)
         self.lay = Layout(build_slots(c))
@@ -294,12 +318,16 @@ class TTSEngine:
         ops.gemm(dy, wflip, out, m, cin, K * cout, cout, K * cout, ldo or cin, a_conv=(T, cout, (K - 1) // 2),
                  beta=beta, ws=self.ws, splits=act_splits(m, cin, K * cout))
 
-    def _wgrad(self, dy, x, gw, n_out, n_in, m, ldy=None, ldx=None, b_conv=None, gb=None):
+    def _wgrad(self, dy, x, gw, n_out, n_in, m, ldy=None, ldx=None, b_conv=None, gb=None, now=False):
         """gw[n_out, n_in] (f32) = dy[m, n_out]^T @ x[m, n_in]; gb (optional) = the
         bias gradient sum_m dy[m, :], fused into the GEMM's A-tile pass for bf16.
         Inside a _defer_wgrads() scope, v7-eligible requests are queued and launched
-        together by _flush_wgrads (their inputs must stay live until then)."""
-        if self._wq is not None and _wide(dy.dtype, b_conv, n_out, n_out, n_in):
+        together by _flush_wgrads (their inputs must stay live until then); in an overlapped
+        backward every v7-eligible request is queued for the side stream (now=True: not)."""
+        if (self._wq is not None or (self._jobs is not None and not now)) and _wide(dy.dtype, b_conv, n_out, n_out,
+                                                                                     n_in):
+            if self._wq is None:
+                self._wq = []
             self._wq.append(dict(a=dy, b=x, c=gw, m=n_out, n=n_in, k=m, lda=ldy or n_out, ldb=ldx or n_in, ldc=n_in,
                                  trans_a=True, trans_b=True, b_conv=b_conv, a_ksum=gb))
             return
@@ -328,11 +356,25 @@ class TTSEngine:
         `slot` (free: its previous user was completed by `prev`'s launch) and returned for
         _flush_wgrads to finalize inside the layer's grouped weight-gradient launch, which
         precedes the layer's DP bucket (_ready) and the next use of the slot."""
-        extra = self._ln_defer(slot, 0, prev) if self.ln_chain and self.ln_fin_in_reduce else {"prev": prev}
+        if self._jobs is not None:
+            # overlapped: finalized later by the layer's weight-gradient job on the side stream,
+            # so the partials get a buffer of their own (the chain slots are reused meanwhile)
+            key = kw.pop("key")
+            buf = self._ln_parts_l.get(key)
+            if buf is None:
+                buf = torch.empty(ops.layernorm_bwd_workspace_size(1 << 30, self.cfg.d_model), dtype=torch.uint8,
+                                  device=self.dev)
+                self._ln_parts_l[key] = buf
+            extra = {"part": buf, "defer": True, "prev": prev}
+        else:
+            kw.pop("key", None)
+            extra = self._ln_defer(slot, 0, prev) if self.ln_chain and self.ln_fin_in_reduce else {"prev": prev}
         a = ops.layernorm_bwd(*args, ws=self.ws, **kw, **extra)
         return a if extra.get("defer") else None
 
     def _defer_wgrads(self):
+        if self._wq and self._jobs is not None:   # overlapped: earlier queued requests keep their order
+            self._push_job(self._wq)
         self._wq = []
 
     def _flush_wgrads(self, fin=None):
@@ -340,7 +382,13 @@ class TTSEngine:
         split-K factor per group: about 256 work items, >= 512 tokens per split.  fin: the
         layer's last (deferred) LayerNorm backward, finalized in the first group's reduce
         launch instead of a launch of its own."""
-        q, self._wq = self._wq, None
+        q, self._wq = self._wq or [], None
+        if self._jobs is not None:
+            self._push_job(q, fin)
+            return
+        self._launch_wgrads(q, fin, self.ws)
+
+    def _launch_wgrads(self, q, fin, ws, side=False):
         if not q and fin is not None:
             ops.layernorm_bwd_finalize(fin)
         for i in range(0, len(q), 8):
@@ -348,7 +396,60 @@ class TTSEngine:
             tiles = sum(((p["m"] + 255) // 256) * ((p["n"] + 127) // 128) for p in grp)
             kmin = min(p["k"] for p in grp)
             sp = max(1, min(16, 256 // tiles, kmin // 512))
-            ops.gemm_grouped([dict(p, splits=sp) for p in grp], ws=self.ws, fin=fin if i == 0 else None)
+            if side:   # beside the encoder backward: shorter items, a capped grid
+                sp = max(1, min(16 * self.side_split, sp * self.side_split, kmin // 256))
+            ops.gemm_grouped([dict(p, splits=sp) for p in grp], ws=ws, fin=fin if i == 0 else None,
+                             max_groups=self.side_groups if side else 0)
+
+    # ------------------------------------------------------------ overlapped weight gradients
+    # A job = queued weight-gradient requests (+ a deferred LayerNorm finalize, + the DP hooks
+    # of the buckets they complete), ordered after the main-stream work that produced its
+    # inputs by an event.  Jobs run in order on the side stream, which first waits for the
+    # start of the encoder backward (_start_side); the main stream joins it at the end of the
+    # backward.  Every DP hook therefore fires from the side stream, in bucket order.
+    def _ov_begin(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream()
+            self._side_ws = ops.Workspace()
+        self._side.wait_stream(torch.cuda.current_stream())
+        self._jobs = []
+        self._side_live = False
+
+    def _push_job(self, q, fin=None, ready=()):
+        ev = torch.cuda.Event()
+        ev.record()
+        job = {"q": q, "fin": fin, "ready": list(ready), "ev": ev, "done": False}
+        self._jobs.append(job)
+        if self._side_live:
+            self._run_job(job)
+        return job
+
+    def _run_job(self, job):
+        self._side.wait_event(job["ev"])
+        with torch.cuda.stream(self._side):
+            self._launch_wgrads(job["q"], job["fin"], self._side_ws, side=True)
+            for name in job["ready"]:
+                self.grad_ready_hook(self.lay.offset(name))
+        job["done"] = True
+
+    def _start_side(self):
+        gate = torch.cuda.Event()
+        gate.record()
+        self._side.wait_event(gate)
+        self._side_live = True
+        for job in self._jobs:
+            if not job["done"]:
+                self._run_job(job)
+
+    def _ov_end(self):
+        if self._wq:
+            self._push_job(self._wq)
+            self._wq = None
+        if not self._side_live:
+            self._start_side()
+        torch.cuda.current_stream().wait_stream(self._side)
+        self._jobs = None
+        self._side_live = False
 
     def _bias(self, dy, ld, m, n, gb):
         ops.colsum(dy, ld, m, n, gb, ws=self.ws)
@@ -498,6 +599,12 @@ class TTSEngine:
 
     # ------------------------------------------------------------ backward
     def _ready(self, name):
+        if self._jobs is not None:
+            # the bucket is final once the queued weight gradients have run: its hook goes
+            # with them, in a job ordered after everything the main stream has issued so far
+            q, self._wq = self._wq or [], None
+            self._push_job(q, ready=[name] if self.grad_ready_hook is not None else [])
+            return
         if self.grad_ready_hook is not None:
             self.grad_ready_hook(self.lay.offset(name))
 
@@ -509,6 +616,12 @@ class TTSEngine:
         pad = (K - 1) // 2
         scale = 1.0 / math.sqrt(c.head_dim)
         gs = lambda p: 1.0 / (1.0 - p) if (self.training and self.dropout_enabled and p > 0) else 1.0  # noqa: E731
+        ov = self.wgrad_overlap and cd == torch.bfloat16
+        if ov:
+            self._ov_begin()
+        # a weight-gradient dY buffer: per layer (`key`) when the side stream reads it later
+        gbuf = (lambda name, key, shape=None: A.layer_buf(name, key, shape)) if ov else \
+            (lambda name, key, shape=None: A[name] if shape is None else A[name].view(-1)[:math.prod(shape)].view(shape))
         self._flip_conv_weights()
         # ---------------- post-net
         chans = postnet_channels(c)
@@ -519,7 +632,7 @@ class TTSEngine:
             cin, cout = chans[i], chans[i + 1]
             last = i == nl - 1
             # BN backward may run in place (g is dead afterwards)
-            dyv = scratch[i % 2].view(-1)[:Md * cout].view(Md, cout)
+            dyv = gbuf("g_pa", f"p{i}", (Md, cout)) if ov else scratch[i % 2].view(-1)[:Md * cout].view(Md, cout)
             ops.batchnorm_bwd(A[f"pcv_y{i}"], g, self.P(f"post.bn{i}.g"), self.P(f"post.bn{i}.b"),
                               A[f"pcv_mean{i}"], A[f"pcv_rstd{i}"], dyv, self.G(f"post.bn{i}.g"),
                               self.G(f"post.bn{i}.b"), Md, cout, ACT_NONE if last else ACT_TANH,
@@ -550,7 +663,7 @@ class TTSEngine:
                                    torch.zeros(nhp, dtype=torch.float32, device=self.dev),
                                    torch.zeros(nhp, d, dtype=cd, device=self.dev))
             gw_p, gb_p, w_p = self._heads_pad
-            self._wgrad(A["gh_cd"], x_top, gw_p, nhp, d, Md, ldy=A.heads_ld, gb=gb_p)
+            self._wgrad(A["gh_cd"], x_top, gw_p, nhp, d, Md, ldy=A.heads_ld, gb=gb_p, now=True)
             ops.cast2d(gw_p, d, self.G("heads.w"), d, nh, d)
             ops.cast2d(gb_p, nhp, self.G("heads.b"), nh, 1, nh)
             ops.cast2d(self.W("heads.w"), d, w_p, d, nh, d)
@@ -569,25 +682,27 @@ class TTSEngine:
             h1, h2 = A[f"dh1{l}"], A[f"dh2{l}"]
             self._defer_wgrads()
             # LN3 + FFN
+            g_br3, g_f1 = gbuf("g_br3", l), gbuf("g_f1", l)
             ln3 = ops.layernorm_bwd(gx, h2, A[f"df2{l}"], self.P(p + "ln3.g"), A[f"dln3m{l}"], A[f"dln3r{l}"],
-                                    A["g_res"], A["g_br3"], self.G(p + "ln3.g"), self.G(p + "ln3.b"), Md,
+                                    A["g_res"], g_br3, self.G(p + "ln3.g"), self.G(p + "ln3.b"), Md,
                                     drop=self.drop(base + 3, c.dropout), ws=self.ws, dbias=self.G(p + "ffn2.b"),
                                     **self._ln_defer(0, Md))
-            self._wgrad(A["g_br3"], A[f"df1{l}"], self.G(p + "ffn2.w"), d, F, Md)
-            self._dgrad(A["g_br3"], self.W(p + "ffn2.w"), A["g_f1"], Md, F, d, gate=A[f"df1{l}"],
+            self._wgrad(g_br3, A[f"df1{l}"], self.G(p + "ffn2.w"), d, F, Md)
+            self._dgrad(g_br3, self.W(p + "ffn2.w"), g_f1, Md, F, d, gate=A[f"df1{l}"],
                         gate_scale=gs(c.dropout))
-            self._wgrad(A["g_f1"], h2, self.G(p + "ffn1.w"), F, d, Md, gb=self.G(p + "ffn1.b"))
-            self._dgrad(A["g_f1"], self.W(p + "ffn1.w"), gx2, Md, d, F, res=A["g_res"])
+            self._wgrad(g_f1, h2, self.G(p + "ffn1.w"), F, d, Md, gb=self.G(p + "ffn1.b"))
+            self._dgrad(g_f1, self.W(p + "ffn1.w"), gx2, Md, d, F, res=A["g_res"])
             gx, gx2 = gx2, gx
             # LN2 + cross attention
+            g_br2 = gbuf("g_br2", l)
             ln2 = ops.layernorm_bwd(gx, h1, A[f"dco{l}"], self.P(p + "ln2.g"), A[f"dln2m{l}"], A[f"dln2r{l}"],
-                                    A["g_res"], A["g_br2"], self.G(p + "ln2.g"), self.G(p + "ln2.b"), Md,
+                                    A["g_res"], g_br2, self.G(p + "ln2.g"), self.G(p + "ln2.b"), Md,
                                     drop=self.drop(base + 1, c.dropout), ws=self.ws, dbias=self.G(p + "co.b"),
                                     **self._ln_defer(1, Md, ln3))
-            self._wgrad(A["g_br2"], A[f"dcatt{l}"], self.G(p + "co.w"), d, d, Md)
-            self._dgrad(A["g_br2"], self.W(p + "co.w"), A["g_att"], Md, d, d)
+            self._wgrad(g_br2, A[f"dcatt{l}"], self.G(p + "co.w"), d, d, Md)
+            self._dgrad(g_br2, self.W(p + "co.w"), A["g_att"], Md, d, d)
             ko = 2 * d * l
-            g_cq = A["g_cq"]
+            g_cq = gbuf("g_cq", l)
             ops.attn_bwd(A[f"dcq{l}"], mkv[:, ko:], mkv[:, ko + d:], A[f"dcatt{l}"], A["g_att"], A[f"dclse{l}"],
                          A["delta"], g_cq, g_mkv[:, ko:], g_mkv[:, ko + d:], d, kvld, kvld, d, d, d, kvld, kvld,
                          B, H, Ty, Tx, A["text_len"], False, scale)
@@ -595,12 +710,14 @@ class TTSEngine:
             self._dgrad(g_cq, self.W(p + "cq.w"), gx2, Md, d, d, res=A["g_res"])
             gx, gx2 = gx2, gx
             # LN1 + self attention
+            g_br = gbuf("g_br", l)
             ln1 = self._ln_last(gx, x_in, A[f"do{l}"], self.P(p + "ln1.g"), A[f"dln1m{l}"], A[f"dln1r{l}"],
-                                A["g_res"], A["g_br"], self.G(p + "ln1.g"), self.G(p + "ln1.b"), Md,
-                                drop=self.drop(base, c.dropout), dbias=self.G(p + "o.b"), prev=ln2, slot=0)
-            self._wgrad(A["g_br"], A[f"datt{l}"], self.G(p + "o.w"), d, d, Md)
-            self._dgrad(A["g_br"], self.W(p + "o.w"), A["g_att"], Md, d, d)
-            qkv, gq = A[f"dqkv{l}"], A["g_qkv"]
+                                A["g_res"], g_br, self.G(p + "ln1.g"), self.G(p + "ln1.b"), Md,
+                                drop=self.drop(base, c.dropout), dbias=self.G(p + "o.b"), prev=ln2, slot=0,
+                                key=("dec", l))
+            self._wgrad(g_br, A[f"datt{l}"], self.G(p + "o.w"), d, d, Md)
+            self._dgrad(g_br, self.W(p + "o.w"), A["g_att"], Md, d, d)
+            qkv, gq = A[f"dqkv{l}"], gbuf("g_qkv", l)
             ops.attn_bwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"datt{l}"], A["g_att"], A[f"dlse{l}"], A["delta"],
                          gq, gq[:, d:], gq[:, 2 * d:], 3 * d, 3 * d, 3 * d, d, d, 3 * d, 3 * d, 3 * d,
                          B, H, Ty, Ty, A["mel_len"], True, scale)
@@ -610,7 +727,7 @@ class TTSEngine:
             self._flush_wgrads(fin=ln1)
             self._ready(p + "qkv.w")
         # ---------------- decoder pre-net
-        g_proj = A["g_br"]
+        g_proj = gbuf("g_br", "pre")
         ops.posenc_bwd(gx, self.pe, g_proj, self.G("dec.alpha"), Md, Ty, drop=self.drop(SITE_DEC_PE, c.dropout),
                        ws=self.ws)
         self._wgrad(g_proj, A["dp2"], self.G("dec.proj.w"), d, c.dec_prenet, Md, gb=self.G("dec.proj.b"))
@@ -635,11 +752,16 @@ class TTSEngine:
         gatt = A["g_att"].view(-1)[:Me * d].view(Me, d)
         gq = A["g_qkv"].view(-1)[:Me * 3 * d].view(Me, 3 * d)
         self._dgrad(g_mkv, self.W("dec.kv.w"), gxe, Me, d, kvld)
+        if ov:   # the weight gradients queued so far run beside the encoder backward
+            self._start_side()
         # ---------------- encoder layers
         for l in reversed(range(c.n_enc)):
             p, base = f"enc{l}.", SITE_ENC_LAYER + 4 * l
             x_in, h1 = A[f"ex{l}"], A[f"eh1{l}"]
             self._defer_wgrads()
+            if ov:
+                gbr, gbr2 = gbuf("g_br", f"e{l}", (Me, d)), gbuf("g_br2", f"e{l}", (Me, d))
+                gf1, gq = gbuf("g_f1", f"e{l}", (Me, F)), gbuf("g_qkv", f"e{l}", (Me, 3 * d))
             ln2 = ops.layernorm_bwd(gxe, h1, A[f"ef2{l}"], self.P(p + "ln2.g"), A[f"eln2m{l}"], A[f"eln2r{l}"],
                                     gres, gbr2, self.G(p + "ln2.g"), self.G(p + "ln2.b"), Me,
                                     drop=self.drop(base + 2, c.dropout), ws=self.ws, dbias=self.G(p + "ffn2.b"),
@@ -651,7 +773,7 @@ class TTSEngine:
             gxe, gxe2 = gxe2, gxe
             ln1 = self._ln_last(gxe, x_in, A[f"eo{l}"], self.P(p + "ln1.g"), A[f"eln1m{l}"], A[f"eln1r{l}"], gres,
                                 gbr, self.G(p + "ln1.g"), self.G(p + "ln1.b"), Me, drop=self.drop(base, c.dropout),
-                                dbias=self.G(p + "o.b"), prev=ln2, slot=1)
+                                dbias=self.G(p + "o.b"), prev=ln2, slot=1, key=("enc", l))
             self._wgrad(gbr, A[f"eatt{l}"], self.G(p + "o.w"), d, d, Me)
             self._dgrad(gbr, self.W(p + "o.w"), gatt, Me, d, d)
             qkv = A[f"eqkv{l}"]
@@ -664,6 +786,8 @@ class TTSEngine:
             self._flush_wgrads(fin=ln1)
             self._ready(p + "qkv.w")
         # ---------------- encoder pre-net
+        if ov:
+            gbr = gbuf("g_br", "eproj", (Me, d))
         ops.posenc_bwd(gxe, self.pe, gbr, self.G("enc.alpha"), Me, Tx, drop=self.drop(SITE_ENC_PE, c.dropout),
                        ws=self.ws)
         self._wgrad(gbr, A[f"ecv_o{c.enc_conv_layers - 1}"], self.G("enc.proj.w"), d, d, Me,
@@ -672,6 +796,8 @@ class TTSEngine:
         self._dgrad(gbr, self.W("enc.proj.w"), gc, Me, d, d)
         gdy = gres
         for i in reversed(range(c.enc_conv_layers)):
+            if ov:
+                gdy = gbuf("g_res", f"c{i}", (Me, d))
             ops.batchnorm_bwd(A[f"ecv_y{i}"], gc, self.P(f"enc.bn{i}.g"), self.P(f"enc.bn{i}.b"), A[f"ecv_mean{i}"],
                               A[f"ecv_rstd{i}"], gdy, self.G(f"enc.bn{i}.g"), self.G(f"enc.bn{i}.b"), Me, d,
                               ACT_RELU, drop=self.drop(SITE_ENC_CONV + i, c.prenet_dropout), ws=self.ws,
@@ -683,6 +809,8 @@ class TTSEngine:
             self._conv_dgrad(gdy, wflip, gc, Me, d, d, K, Tx)
         ops.embedding_bwd(A["text"], gc, self.G("enc.embed"), Me, c.vocab, pad_idx=0)
         self._ready("enc.embed")
+        if ov:
+            self._ov_end()
 
     def _wflip_buf(self, name, cout, cin, K):
         key = ("wflip", name)

@@ -393,7 +393,10 @@ class TransformerTTS(nn.Module):
         if e.exp_avg is None:
             e.init_optimizer()
         A = e.arena(B, Tx, Ty)
-        # the caller's warm-up eager steps size every workspace; capture must not allocate
+        # the caller's warm-up eager steps size every workspace; capture must not allocate.
+        # Every arena buffer exists before capture (the warm-ups may have run the overlapped
+        # backward, which uses per-layer copies in place of some shared scratch buffers)
+        A.materialize()
         nbt_saved = dict(e.nbt)
         hook, e.grad_ready_hook = e.grad_ready_hook, None
         sync = getattr(sync_grads, "__self__", None)   # a GradSync's bound finish(): overlap buckets
@@ -402,6 +405,11 @@ class TransformerTTS(nn.Module):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g2 = torch.cuda.CUDAGraph() if sync_grads is not None else None
+        # the segmented capture ends graphs inside the backward, where the overlapped weight
+        # gradients' side stream (engine.wgrad_overlap) would still be forked: off for it
+        ov_saved = e.wgrad_overlap
+        if sync is not None and hasattr(sync, "take_ready"):
+            e.wgrad_overlap = False
         segs = []   # [(graph, bucket indices launched right after its replay)]
         # captures are thread-local: RCCL's watchdog thread polls its work events during
         # capture, which a global-mode capture treats as a prohibited call (capture invalidated)
@@ -440,6 +448,7 @@ class TransformerTTS(nn.Module):
                     e.optimizer_step()
         torch.cuda.current_stream().wait_stream(s)
         e.grad_ready_hook = hook
+        e.wgrad_overlap = ov_saved
         e.nbt = nbt_saved  # capture records kernels only; each replay counts one batch
         self._graphs[(B, Tx, Ty)] = (segs, g2)
 

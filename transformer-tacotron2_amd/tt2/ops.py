@@ -139,11 +139,12 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, **kw):
     return c
 
 
-def gemm_grouped(problems, ws: Workspace | None = None, fin=None):
+def gemm_grouped(problems, ws: Workspace | None = None, fin=None, max_groups: int = 0):
     """One tt2_gemm_grouped launch (v7) over up to 8 requests, each a dict of gemm()
     arguments (a, b, c, m, n, k, lda, ldb, ldc + keywords); their split-K slabs get
     disjoint slices of one workspace.  fin: a deferred layernorm_bwd's returned LnArgs,
-    completed in the group's reduce launch (tt2_gemm_grouped_fin)."""
+    completed in the group's reduce launch (tt2_gemm_grouped_fin).  max_groups > 0: at most
+    that many work groups walk the items (tt2_gemm_grouped_ex)."""
     L = lib()
     finp = C.addressof(fin) if fin is not None else None
     arr = (GemmArgs * len(problems))()
@@ -162,10 +163,10 @@ def gemm_grouped(problems, ws: Workspace | None = None, fin=None):
         flops = sum(2.0 * g.m * g.n * g.k for g in arr)
         ab = sum(2 * (g.m * g.k + g.n * g.k) + (2 if g.dtype_out == _lib.DT_BF16 else 4) * g.m * g.n for g in arr)
         PROBE.begin()
-        check(L.tt2_gemm_grouped_fin(arr, len(problems), finp, stream_ptr()), "tt2_gemm_grouped")
+        check(L.tt2_gemm_grouped_ex(arr, len(problems), finp, max_groups, stream_ptr()), "tt2_gemm_grouped")
         PROBE.end(key, flops, ab, list(arr))
         return
-    check(L.tt2_gemm_grouped_fin(arr, len(problems), finp, stream_ptr()), "tt2_gemm_grouped")
+    check(L.tt2_gemm_grouped_ex(arr, len(problems), finp, max_groups, stream_ptr()), "tt2_gemm_grouped")
 
 
 class LaunchProbe:
