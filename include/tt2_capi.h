@@ -505,9 +505,16 @@ typedef struct tt2_adam_args {
   int64_t n;
   float lr, beta1, beta2, eps, weight_decay, clip_norm, warmup;
   int32_t noam, d_model;
+  /* clip: norm_parts != NULL gives the squared gradient norm as the sum of norm_nparts partial
+   * sums the caller computed beforehand (tt2_sumsq_parts over ranges that cover grads[0, n)),
+   * in place of the step's own pass over the gradients */
+  const float* norm_parts;
+  int32_t norm_nparts;
 } tt2_adam_args;
 size_t tt2_adam_workspace_size(void);
 int tt2_adam_step(const tt2_adam_args* a, hipStream_t stream);
+/* parts[0 .. nparts) = partial sums of g[i]^2 over g[0, n) (fixed split: reproducible) */
+int tt2_sumsq_parts(const float* g, int64_t n, float* parts, int32_t nparts, hipStream_t stream);
 /* step += 1; seed += 1 (seed may be NULL) */
 int tt2_step_bump(int32_t* step, uint32_t* seed, hipStream_t stream);
 

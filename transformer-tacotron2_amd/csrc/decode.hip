@@ -105,14 +105,34 @@ TT2_DEV void qproj(const DecArgs& a, int b, int h, float* sq, const float* sx, c
 // instruction reads 8 whole rows; every lane issues its 8 row loads before the first FMA;
 // the 8 chunk partials of a row meet by xor shuffles and leave through LDS as one
 // coalesced row of the slab.  o: this lane's 8 elements of the head output (chunk lane & 7).
+// pre: this wave's first 8 rows, loaded by oproj_prefetch at the start of the kernel (behind the
+// first keys, so no earlier wait drains them): the projection then costs no memory round trip
+// of its own when H * 64 == NW * 64 (one row block per wave)
+template <typename T>
+using T8 = T __attribute__((ext_vector_type(8)));
 template <typename T, int NW>
-TT2_DEV void oproj_slab(const DecArgs& a, int b, int h, const float (&o)[8], float* sres) {
+TT2_DEV void oproj_prefetch(const DecArgs& a, int h, T8<T> (&pre)[8]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 7, g = lane >> 3;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    pre[i] = *reinterpret_cast<const T8<T>*>(reinterpret_cast<const T*>(a.wo) + (int64_t)(w * 64 + 8 * i + g) * a.wo_ld +
+                                              h * D + 8 * c);
+}
+template <typename T, int NW>
+TT2_DEV void oproj_slab(const DecArgs& a, int b, int h, const float (&o)[8], float* sres, const T8<T> (&pre)[8]) {
   const int N = a.H * D, lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 7, g = lane >> 3;
   for (int r0 = w * 64; r0 < N; r0 += NW * 64) {
     float wv[8][8];
+    if (sizeof(T) == 2 && r0 == w * 64) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      load8f(reinterpret_cast<const T*>(a.wo) + (int64_t)(r0 + 8 * i + g) * a.wo_ld + h * D + 8 * c, wv[i]);
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wv[i][j] = (float)pre[i][j];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        load8f(reinterpret_cast<const T*>(a.wo) + (int64_t)(r0 + 8 * i + g) * a.wo_ld + h * D + 8 * c, wv[i]);
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float p = 0.f;
@@ -186,6 +206,10 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
   };
   // the first iteration's keys do not depend on the query: in flight during its projection
   if (k0 < k1) load_keys(k0, 0);
+  T8<T> wpre[8];   // 16-bit types only: the f32 (parity-mode) kernel has no registers to spare
+  if constexpr (sizeof(T) == 2) {
+    if (a.wo) oproj_prefetch<T, NW>(a, h, wpre);
+  }
   float qv[8];
   if (a.wq) {
     float wv[8][8];
@@ -281,7 +305,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
     float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = sfin[8 * (lane & 7) + j];
-    oproj_slab<T, NW>(a, b, h, o, sres);
+    oproj_slab<T, NW>(a, b, h, o, sres, wpre);
   }
 }
 

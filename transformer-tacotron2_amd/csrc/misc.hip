@@ -751,15 +751,24 @@ extern "C" int tt2_adam_step(const tt2_adam_args* p, hipStream_t s) {
   if (p->clip_norm > 0.f) {
     if (!p->workspace || p->ws_bytes < tt2_adam_workspace_size())
       return tt2_set_error(TT2_E_INVALID, "tt2_adam_step: workspace");
+    if (p->norm_parts && p->norm_nparts <= 0) return tt2_set_error(TT2_E_INVALID, "tt2_adam_step: norm_nparts");
     float* part = reinterpret_cast<float*>(p->workspace);
     float* total = part + TT2_ADAM_NORM_BLOCKS;
-    hipLaunchKernelGGL(sumsq_kernel, dim3(TT2_ADAM_NORM_BLOCKS), dim3(NT), 0, s, p->grads, p->n, part);
-    hipLaunchKernelGGL(reduce_rows_kernel, dim3(1), dim3(NT), 0, s, part, TT2_ADAM_NORM_BLOCKS, 1, (int64_t)1, total,
-                       0.f, 1);
+    if (!p->norm_parts)
+      hipLaunchKernelGGL(sumsq_kernel, dim3(TT2_ADAM_NORM_BLOCKS), dim3(NT), 0, s, p->grads, p->n, part);
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3(1), dim3(NT), 0, s, p->norm_parts ? p->norm_parts : part,
+                       p->norm_parts ? p->norm_nparts : TT2_ADAM_NORM_BLOCKS, 1, (int64_t)1, total, 0.f, 1);
     a.sumsq = total;
   }
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(p->n / 4)), dim3(NT), 0, s, a);
   return tt2_check_launch(hipGetLastError(), "tt2_adam_step");
+}
+
+extern "C" int tt2_sumsq_parts(const float* g, int64_t n, float* parts, int32_t nparts, hipStream_t s) {
+  if (!g || !parts || nparts <= 0 || n < 0 || (reinterpret_cast<uintptr_t>(g) % 16))
+    return tt2_set_error(TT2_E_INVALID, "tt2_sumsq_parts: g 16-B aligned, parts, nparts > 0");
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(NT), 0, s, g, n, parts);
+  return tt2_check_launch(hipGetLastError(), "tt2_sumsq_parts");
 }
 
 extern "C" int tt2_step_bump(int32_t* step, uint32_t* seed, hipStream_t s) {

@@ -208,13 +208,14 @@ class AdamArgs(C.Structure):
         ("params", vp), ("grads", vp), ("exp_avg", vp), ("exp_avg_sq", vp), ("shadow_bf16", vp), ("step", vp),
         ("workspace", vp), ("ws_bytes", sz), ("n", i64),
         ("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32), ("weight_decay", f32), ("clip_norm", f32),
-        ("warmup", f32), ("noam", i32), ("d_model", i32),
+        ("warmup", f32), ("noam", i32), ("d_model", i32), ("norm_parts", vp), ("norm_nparts", i32),
     ]
 
 
 P_ = C.POINTER
 SIGNATURES.update({
     "tt2_reduce_rows": ([P_(ReduceArgs), vp], C.c_int),
+    "tt2_sumsq_parts": ([vp, i64, vp, C.c_int32, vp], C.c_int),
     "tt2_colsum_workspace_size": ([C.c_int, C.c_int], sz),
     "tt2_colsum": ([vp, C.c_int, i64, C.c_int, C.c_int, vp, f32, vp, sz, vp], C.c_int),
     "tt2_layernorm_fwd": ([P_(LnArgs), vp], C.c_int),

@@ -199,6 +199,8 @@ class Arena:
 
 
 class TTSEngine:
+    NORM_RANGES, NORM_PARTS = 64, 32   # overlapped backward: gradient ranges x sumsq partials each
+
     def __init__(self, cfg: TTSConfig | None = None, dtype: torch.dtype = torch.bfloat16, device="cuda",
                  seed: int = 0):
         self.cfg = c = cfg or TTSConfig()
@@ -225,6 +227,8 @@ class TTSEngine:
         self._ln_parts_l = {}   # per-layer partials of the deferred last LayerNorm of a layer
         # side-stream weight-gradient launches: split-K factor multiplier (shorter work items)
         # and work-group cap (0: none), dev knobs for the overlap's A/B
+        self._norm_buf = None
+        self._norm_pending = None   # (ranges, computed on the side stream) of the last overlapped backward
         self.side_split = int(os.environ.get("TT2_SIDE_SPLIT", "1"))
         self.side_groups = int(os.environ.get("TT2_SIDE_WG", "0"))
         self.cd = dtype
@@ -414,6 +418,12 @@ class TTSEngine:
         self._side.wait_stream(torch.cuda.current_stream())
         self._jobs = []
         self._side_live = False
+        # the clip norm's squared sum, one range of the flat gradients per DP bucket boundary
+        # (each range final when its job has run): on the side stream without a DP hook, else
+        # by optimizer_step once the exchange has finished (same ranges: same result)
+        if self._norm_buf is None:
+            self._norm_buf = torch.empty(self.NORM_RANGES * self.NORM_PARTS, dtype=torch.float32, device=self.dev)
+        self._norm_ranges, self._norm_hi, self._norm_side = [], self.lay.numel, self.grad_ready_hook is None
 
     def _push_job(self, q, fin=None, ready=()):
         ev = torch.cuda.Event()
@@ -429,8 +439,24 @@ class TTSEngine:
         with torch.cuda.stream(self._side):
             self._launch_wgrads(job["q"], job["fin"], self._side_ws, side=True)
             for name in job["ready"]:
-                self.grad_ready_hook(self.lay.offset(name))
+                off = self.lay.offset(name)
+                if self.grad_ready_hook is not None:
+                    self.grad_ready_hook(off)
+                self._norm_range(off)
         job["done"] = True
+
+    def _norm_range(self, lo):
+        """Gradients [lo, hi) are final (hi: the previous boundary): their squared-norm partials."""
+        hi = self._norm_hi
+        if lo >= hi:
+            return
+        k = len(self._norm_ranges)
+        if k >= self.NORM_RANGES:
+            raise RuntimeError("overlapped backward: more gradient ranges than NORM_RANGES")
+        self._norm_ranges.append((lo, hi))
+        self._norm_hi = lo
+        if self._norm_side:
+            ops.sumsq_parts(self.grads[lo:hi], self._norm_buf[k * self.NORM_PARTS:], self.NORM_PARTS)
 
     def _start_side(self):
         gate = torch.cuda.Event()
@@ -447,9 +473,12 @@ class TTSEngine:
             self._wq = None
         if not self._side_live:
             self._start_side()
+        with torch.cuda.stream(self._side):
+            self._norm_range(0)
         torch.cuda.current_stream().wait_stream(self._side)
         self._jobs = None
         self._side_live = False
+        self._norm_pending = (list(self._norm_ranges), self._norm_side)
 
     def _bias(self, dy, ld, m, n, gb):
         ops.colsum(dy, ld, m, n, gb, ws=self.ws)
@@ -603,7 +632,7 @@ class TTSEngine:
             # the bucket is final once the queued weight gradients have run: its hook goes
             # with them, in a job ordered after everything the main stream has issued so far
             q, self._wq = self._wq or [], None
-            self._push_job(q, ready=[name] if self.grad_ready_hook is not None else [])
+            self._push_job(q, ready=[name])
             return
         if self.grad_ready_hook is not None:
             self.grad_ready_hook(self.lay.offset(name))
@@ -617,6 +646,7 @@ class TTSEngine:
         scale = 1.0 / math.sqrt(c.head_dim)
         gs = lambda p: 1.0 / (1.0 - p) if (self.training and self.dropout_enabled and p > 0) else 1.0  # noqa: E731
         ov = self.wgrad_overlap and cd == torch.bfloat16
+        self._norm_pending = None
         if ov:
             self._ov_begin()
         # a weight-gradient dY buffer: per layer (`key`) when the side stream reads it later
@@ -848,7 +878,15 @@ class TTSEngine:
     @ranged("tt2.optimizer")
     def optimizer_step(self):
         o = self.opt
+        parts = None
+        if self._norm_pending is not None:
+            ranges, done = self._norm_pending
+            self._norm_pending = None
+            if not done:   # DP: the gradients are final (all-reduced) only now
+                for k, (lo, hi) in enumerate(ranges):
+                    ops.sumsq_parts(self.grads[lo:hi], self._norm_buf[k * self.NORM_PARTS:], self.NORM_PARTS)
+            parts = self._norm_buf[:len(ranges) * self.NORM_PARTS]
         ops.adam_step(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.shadow, self.step_t,
                       self.lay.numel, o["lr"], o["beta1"], o["beta2"], o["eps"], o["weight_decay"], o["clip_norm"],
-                      o["warmup"], o["noam"], self.cfg.d_model, ws=self.ws)
+                      o["warmup"], o["noam"], self.cfg.d_model, ws=self.ws, norm_parts=parts)
         ops.step_bump(self.step_t, self.seed)

@@ -493,10 +493,20 @@ def conv_weight_flip(w, wd, cout, cin, k):
           "tt2_conv_weight_flip")
 
 
+def sumsq_parts(g: torch.Tensor, parts: torch.Tensor, nparts: int):
+    """parts[:nparts] = partial sums of g**2 (f32, fixed split), for adam_step(norm_parts=)."""
+    check(lib().tt2_sumsq_parts(g.data_ptr(), g.numel(), parts.data_ptr(), nparts, stream_ptr()), "tt2_sumsq_parts")
+
+
 def adam_step(params, grads, m, v, shadow, step, n, lr, beta1=0.9, beta2=0.98, eps=1e-9, weight_decay=0.0,
-              clip_norm=1.0, warmup=4000.0, noam=True, d_model=512, ws: Workspace | None = None):
+              clip_norm=1.0, warmup=4000.0, noam=True, d_model=512, ws: Workspace | None = None,
+              norm_parts: torch.Tensor | None = None):
+    """norm_parts: the squared-norm partial sums of every gradient (sumsq_parts over ranges
+    covering grads), so the clip needs no pass of its own over the gradients."""
     L = lib()
     a = _lib.AdamArgs()
+    if norm_parts is not None:
+        a.norm_parts, a.norm_nparts = norm_parts.data_ptr(), norm_parts.numel()
     a.params, a.grads, a.exp_avg, a.exp_avg_sq = params.data_ptr(), grads.data_ptr(), m.data_ptr(), v.data_ptr()
     a.shadow_bf16, a.step, a.n = ptr(shadow), step.data_ptr(), n
     a.lr, a.beta1, a.beta2, a.eps, a.weight_decay = lr, beta1, beta2, eps, weight_decay
