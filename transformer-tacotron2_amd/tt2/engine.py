@@ -231,6 +231,7 @@ class TTSEngine:
         self._norm_pending = None   # (ranges, computed on the side stream) of the last overlapped backward
         self.side_split = int(os.environ.get("TT2_SIDE_SPLIT", "1"))
         self.side_groups = int(os.environ.get("TT2_SIDE_WG", "0"))
+        self.side_start = int(os.environ.get("TT2_SIDE_START", "-1"))   # decoder layer whose backward starts it
         self.cd = dtype
         self.dev = torch.device(device)
         self.lay = Layout(build_slots(c))
@@ -708,6 +709,8 @@ class TTSEngine:
         g_mkv = A["g_mkv"]
         for l in reversed(range(c.n_dec)):
             p, base = f"dec{l}.", SITE_DEC_LAYER + 4 * l
+            if ov and l == self.side_start and not self._side_live:
+                self._start_side()   # (dev knob) the side stream starts inside the decoder backward
             x_in = A[f"dx{l}"]
             h1, h2 = A[f"dh1{l}"], A[f"dh2{l}"]
             self._defer_wgrads()
@@ -782,7 +785,7 @@ class TTSEngine:
         gatt = A["g_att"].view(-1)[:Me * d].view(Me, d)
         gq = A["g_qkv"].view(-1)[:Me * 3 * d].view(Me, 3 * d)
         self._dgrad(g_mkv, self.W("dec.kv.w"), gxe, Me, d, kvld)
-        if ov:   # the weight gradients queued so far run beside the encoder backward
+        if ov and not self._side_live:   # the weight gradients queued so far run beside the encoder backward
             self._start_side()
         # ---------------- encoder layers
         for l in reversed(range(c.n_enc)):
