@@ -648,6 +648,7 @@ class TTSEngine:
         gs = lambda p: 1.0 / (1.0 - p) if (self.training and self.dropout_enabled and p > 0) else 1.0  # noqa: E731
         ov = self.wgrad_overlap and cd == torch.bfloat16
         self._norm_pending = None
+        self._jobs = self._wq = None   # (a backward that raised leaves no queue behind)
         if ov:
             self._ov_begin()
         # a weight-gradient dY buffer: per layer (`key`) when the side stream reads it later
