@@ -1,0 +1,148 @@
+"""The overlapped bf16 backward (engine.wgrad_overlap: every weight-gradient GEMM queued as a job
+on a side stream that runs beside the encoder backward, per-layer dY buffers, the layer's last
+LayerNorm finalize deferred into its job, clip-norm partials per finished gradient range) against
+the in-place schedule it replaces, and its two kernel-level pieces: the grid-capped grouped GEMM
+(tt2_gemm_grouped_ex) and the range-partitioned clip norm (tt2_sumsq_parts + adam norm_parts)."""
+import ctypes as C
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from tt2 import ops  # noqa: E402
+from tt2._lib import lib  # noqa: E402
+from tt2.config import TTSConfig  # noqa: E402
+from tt2.model import TransformerTTS  # noqa: E402
+
+
+def _model(overlap, **knobs):
+    torch.manual_seed(0)
+    m = TransformerTTS(TTSConfig(), dtype=torch.bfloat16, seed=5)
+    with torch.no_grad():
+        for name, (off, shape, n) in m.engine.lay.slots.items():
+            if len(shape) >= 2:
+                m.engine.P(name).normal_(0, 0.02)
+        m.engine.sync_shadow()
+    m.configure_optimizer(lr=1e-3, warmup=10.0, clip_norm=1.0)
+    m.engine.wgrad_overlap = overlap
+    for k, v in knobs.items():
+        setattr(m.engine, k, v)
+    return m.train()
+
+
+def _batch(B=3, Tx=40, Ty=96, seed=2):
+    g = torch.Generator().manual_seed(seed)
+    text = torch.randint(1, 80, (B, Tx), generator=g).cuda()
+    tl = torch.tensor([Tx, Tx - 7, Tx - 19][:B]).cuda()
+    mel = torch.randn(B, Ty, 80, generator=g).cuda()
+    ml = torch.tensor([Ty, Ty - 30, Ty - 51][:B]).cuda()
+    return text, tl, mel, ml
+
+
+def _grads(m, b):
+    e = m.engine
+    m._sync_shadow()
+    A = m._stage(*b)
+    e.forward(A)
+    e.loss(A)
+    e.backward(A)
+    torch.cuda.synchronize()
+    return e.grads.clone()
+
+
+@pytest.mark.parametrize("knobs", [{}, {"side_groups": 64, "side_split": 2}, {"side_start": 2}])
+def test_overlapped_backward_gradients_bitwise(knobs):
+    """Same kernels, same split factors (side_split 1), same order per stream: the gradients of
+    the overlapped backward equal the in-place backward's bit for bit; with a capped grid
+    (the items walk the same tiles) too; with side_split 2 the weight gradients take twice the
+    split-K slabs, so those are compared at f32 rounding."""
+    b = _batch()
+    ref = _grads(_model(False), b)
+    got = _grads(_model(True, **knobs), b)
+    if knobs.get("side_split", 1) == 1:
+        assert torch.equal(ref, got)
+    else:
+        assert ((got - ref).norm() / ref.norm()).item() < 1e-5
+
+
+def test_overlapped_step_clip_norm_and_graph():
+    """A train step with the overlap: the clip norm comes from range partials (a different
+    summation order than the one-pass norm), so parameters match the in-place step to f32
+    rounding; the captured overlapped step equals its own eager step bit for bit."""
+    b = _batch()
+    a, o = _model(False), _model(True)
+    for _ in range(2):
+        a.train_step(*b)
+        o.train_step(*b)
+    torch.cuda.synchronize()
+    d = (o.engine.params - a.engine.params).abs().max().item()
+    assert d <= 1e-6, d
+    # eager vs captured, both overlapped, from the same state
+    e1, e2 = _model(True), _model(True)
+    for m in (e1, e2):
+        m.train_step(*b)
+    run = e2.capture_train_step(b[0].shape[0], b[0].shape[1], b[2].shape[1])
+    for _ in range(2):
+        l1 = e1.train_step(*b).clone()
+        l2 = run(*b).clone()
+        assert torch.equal(l1, l2)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.engine.params, e2.engine.params)
+
+
+@pytest.mark.parametrize("cap", [8, 64, 200])
+def test_grouped_gemm_grid_cap_bitwise(cap):
+    """tt2_gemm_grouped_ex on `cap` work groups (each walking several 256 x 128 items, some
+    split-K) writes the same bits as one work group per item."""
+    torch.manual_seed(1)
+    K = 3000
+    probs = []
+    for mo, no in ((512, 2048), (1536, 512), (88, 512)):
+        dy = torch.randn(K, mo, device="cuda").bfloat16()
+        x = torch.randn(K, no, device="cuda").bfloat16()
+        probs.append((dy, x, mo, no))
+
+    def run(max_groups):
+        outs, reqs = [], []
+        for dy, x, mo, no in probs:
+            c = torch.empty(mo, no, device="cuda")
+            ks = torch.empty(mo, device="cuda")
+            outs.append((c, ks))
+            reqs.append(dict(a=dy, b=x, c=c, m=mo, n=no, k=K, lda=mo, ldb=no, ldc=no, trans_a=True, trans_b=True,
+                             a_ksum=ks, splits=3))
+        ops.gemm_grouped(reqs, max_groups=max_groups)
+        torch.cuda.synchronize()
+        return outs
+
+    ref, got = run(0), run(cap)
+    for (c0, k0), (c1, k1) in zip(ref, got):
+        assert torch.equal(c0, c1) and torch.equal(k0, k1)
+    dy, x, mo, no = probs[0]
+    want = dy.float().t() @ x.float()
+    assert ((ref[0][0] - want).norm() / want.norm()).item() < 1e-5
+
+
+def test_sumsq_parts_and_adam_norm_parts():
+    torch.manual_seed(2)
+    n = 1 << 20
+    g = torch.randn(n, device="cuda") * 0.01
+    cuts = [0, 4096, 70000, 500000, n]
+    parts = torch.zeros(32 * (len(cuts) - 1), device="cuda")
+    for k in range(len(cuts) - 1):
+        ops.sumsq_parts(g[cuts[k]:cuts[k + 1]], parts[32 * k:], 32)
+    torch.cuda.synchronize()
+    ref = (g.double() ** 2).sum().item()
+    assert abs(parts.double().sum().item() - ref) / ref < 1e-5
+    # adam with precomputed partials == adam with its own norm pass (to f32 summation order)
+    outs = []
+    for use in (False, True):
+        p = torch.ones(n, device="cuda")
+        m, v = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+        step = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ops.adam_step(p, g, m, v, None, step, n, 1e-3, clip_norm=0.5, noam=False,
+                      norm_parts=parts if use else None)
+        outs.append(p)
+    torch.cuda.synchronize()
+    assert (outs[0] - outs[1]).abs().max().item() <= 1e-6
+    assert lib().tt2_sumsq_parts(C.c_void_p(g.data_ptr()), n, C.c_void_p(parts.data_ptr()), 0, None) != 0

@@ -51,7 +51,7 @@ for s in $STEPS; do
       ;;
     dpt)   # the DP / SyncBN / norm / full-length parity tests of round 4
       timeout -k 10 900 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_syncbn.py tests/test_gpu_norm.py \
-        tests/test_gpu_fullsize.py tests/test_gpu_metrics.py -x -v --timeout 300 --timeout-method thread > "$OUT/dpt_tests.log" 2>&1
+        tests/test_gpu_overlap.py tests/test_gpu_decode.py tests/test_gpu_fullsize.py tests/test_gpu_metrics.py -x -v --timeout 300 --timeout-method thread > "$OUT/dpt_tests.log" 2>&1
       ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
