@@ -217,24 +217,57 @@ def test_buckets_final_in_captured_rccl_step_cfg2(nccl_group, sync_bn):
     assert m.engine.bn_sync is None and m.engine.grad_ready_hook is None   # detached on close
 
 
-def test_misplaced_grad_ready_is_caught(nccl_group):
-    """Negative control for the check above: the engine's bucket hook shifted so every bucket
+class IssueSnap:
+    """Each bucket copied on the stream that issues its all-reduce, at the moment of issue: in
+    that stream's order, before any later kernel of it (the compute stream, or the overlapped
+    backward's side stream, which issues every bucket hook).  Unlike the comm-stream copy,
+    whose moment races with the issuing stream's next kernels, this sees a bucket handed over
+    before it is final deterministically, so it serves the negative control."""
+
+    def __init__(self, sync):
+        self.sync = sync
+        self.buf = torch.zeros_like(sync.flat)
+        ready = sync.ready
+
+        def hooked(off):
+            for i in range(sync.next, len(sync.buckets)):
+                lo, hi = sync.buckets[i]
+                if lo >= off:
+                    self.buf[lo:hi].copy_(sync.flat[lo:hi])
+            ready(off)
+        sync.ready = hooked
+
+    def bad(self):
+        torch.cuda.synchronize()
+        return [(lo, hi) for lo, hi in self.sync.buckets if not torch.equal(self.buf[lo:hi], self.sync.flat[lo:hi])]
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_misplaced_grad_ready_is_caught(nccl_group, overlap):
+    """Negative control for the checks above: the engine's bucket hook shifted so every bucket
     is handed to RCCL 2M elements (8 MB of gradients) before it is final.  The captured step
-    must then show buckets whose final gradients differ from what the comm stream copied."""
+    must then show buckets whose final gradients differ from what the issuing stream copied at
+    the hand-off, with the in-place and with the overlapped (side-stream) weight gradients;
+    the correctly placed hook shows none (IssueSnap agrees with InGraphSnap's positive check)."""
     B, Tx, Ty, text, tl, mel, ml = _cfg2_batch()
-    m = _model()
-    sync = attach(m, kind="rccl")
-    snap = InGraphSnap(sync)
-    shift = 2 << 20
-    ready = sync.ready
-    sync.ready = lambda off: ready(max(0, off - shift))   # the captured step hooks sync.ready too
-    m.engine.grad_ready_hook = sync.ready
-    for _ in range(2):
-        m.train_step(text, tl, mel, ml, sync_grads=sync.finish)
-    run = m.capture_train_step(B, Tx, Ty, sync_grads=sync.finish)
-    run(text, tl, mel, ml)
-    assert len(snap.bad()) >= 1, "an early bucket hand-off went unnoticed"
-    sync.close()
+    for shift, want_bad in ((2 << 20, True), (0, False)):
+        m = _model()
+        m.engine.wgrad_overlap = overlap
+        sync = attach(m, kind="rccl")
+        ready = sync.ready
+        sync.ready = lambda off, r=ready, s=shift: r(max(0, off - s))   # the captured step hooks it too
+        snap = IssueSnap(sync)
+        m.engine.grad_ready_hook = sync.ready
+        for _ in range(2):
+            m.train_step(text, tl, mel, ml, sync_grads=sync.finish)
+        run = m.capture_train_step(B, Tx, Ty, sync_grads=sync.finish)
+        run(text, tl, mel, ml)
+        bad = snap.bad()
+        if want_bad:
+            assert len(bad) >= 1, "an early bucket hand-off went unnoticed"
+        else:
+            assert bad == [], bad
+        sync.close()
 
 
 def test_syncbn_rccl_exchange_in_graph_one_rank(nccl_group):
