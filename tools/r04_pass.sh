@@ -1,0 +1,69 @@
+#!/bin/bash
+# One round-4 GPU pass in priority order, inside one gpurun call (run from the repo root):
+#   tools/r04_pass.sh <tag> [budget_s] [steps...]
+# steps (default: dpt bench ab prof phases decab tests): each GPU step runs under its own
+# timeout; a step starts only while the call's time budget allows it; a timeout, abort or
+# segfault (124/137/134/139) ends the pass, a failing test run (rc 1) does not.
+TAG=${1:-r04x}; BUDGET=${2:-1100}; shift 2 || true
+STEPS=${*:-dpt bench ab prof phases decab tests}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+T0=$(date +%s)
+left() { echo $(( BUDGET - ($(date +%s) - T0) )); }
+run() {   # run <name> <need_s> <timeout_s> <cmd...>
+  local name=$1 need=$2 to=$3; shift 3
+  if [ "$(left)" -lt "$need" ]; then echo "skip $name (budget)" >> "$OUT/pass.txt"; return 0; fi
+  local t=$(date +%s)
+  timeout -k 10 "$to" "$@"
+  local rc=$?
+  echo "$name rc=$rc $(( $(date +%s) - t ))s" >> "$OUT/pass.txt"
+  echo "$name rc=$rc" >&2
+  case $rc in 124|137|134|139) echo "stop after $name" >&2; cat "$OUT/pass.txt" >&2; exit $rc ;; esac
+  return 0
+}
+lastms() { python -c "import json,sys;print(json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])['ms_per_step'])" "$1" 2>&1 | tail -1; }
+for s in $STEPS; do
+  case $s in
+    dpt) run dpt 200 600 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_syncbn.py tests/test_gpu_norm.py \
+           tests/test_gpu_overlap.py tests/test_gpu_decode.py tests/test_gpu_fullsize.py tests/test_gpu_metrics.py \
+           -x -v --timeout 300 --timeout-method thread > "$OUT/dpt_tests.log" 2>&1 ;;
+    bench) run bench 150 420 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    ab) for i in 1 2; do
+          for e in TT2_WGRAD_OVERLAP=0 TT2_WGRAD_OVERLAP=1; do
+            run "ab $e" 90 200 env $e python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-decode \
+              > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
+            echo "$e $(lastms "$OUT/ab_run.json")" >> "$OUT/ab.txt"
+          done
+        done ;;
+    knobs) for e in TT2_SIDE_WG=128 TT2_SIDE_SPLIT=2 TT2_SIDE_START=1 TT2_SIDE_START=3 TT2_WGRAD_OVERLAP=1; do
+             run "knob $e" 90 200 env $e python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-decode \
+               > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
+             echo "$e $(lastms "$OUT/ab_run.json")" >> "$OUT/knobs.txt"
+           done ;;
+    prof) run prof 150 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
+            python3 bench.py --profile-run --steps 10 --warmup 2 > "$OUT/bench_step.json" 2> "$OUT/bench_step.err" ;;
+    phases) run phases 120 300 env TT2_LIB=abl/phase.so python -u tools/g7_phases.py --json "$OUT/phases.json" \
+              > "$OUT/phases.txt" 2>&1 ;;
+    decab) for i in 1 2; do
+             for lib in abl/dec0.so transformer-tacotron2_amd/tt2/libtt2.so; do
+               run "decab $lib" 90 200 env TT2_LIB=$lib python3 -u tools/decode_bench_only.py --no-longform \
+                 > "$OUT/dec_run.json" 2> "$OUT/dec_run.err"
+               echo "$lib $(python -c "import json,sys;print(json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])['decode']['value'])" "$OUT/dec_run.json" 2>&1 | tail -1)" >> "$OUT/decab.txt"
+             done
+           done ;;
+    dpmc) run dpmc_f 120 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/dtr/fetch" -o run --output-format csv -- \
+            python3 tools/decode_traffic.py --out="$OUT/dtr" > "$OUT/dtr_fetch.log" 2>&1
+          run dpmc_w 120 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/dtr/write" -o run --output-format csv -- \
+            python3 tools/decode_traffic.py --out="$OUT/dtr" > "$OUT/dtr_write.log" 2>&1 ;;
+    lpmc) run lpmc_f 150 400 rocprofv3 --pmc FETCH_SIZE -d "$OUT/ltr/fetch" -o run --output-format csv -- \
+            python3 tools/decode_traffic.py --longform --out="$OUT/ltr" > "$OUT/ltr_fetch.log" 2>&1
+          run lpmc_w 150 400 rocprofv3 --pmc WRITE_SIZE -d "$OUT/ltr/write" -o run --output-format csv -- \
+            python3 tools/decode_traffic.py --longform --out="$OUT/ltr" > "$OUT/ltr_write.log" 2>&1 ;;
+    tests) run tests 300 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+             > "$OUT/gpu_tests.log" 2>&1
+           run smoke 60 120 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+cat "$OUT/pass.txt"
