@@ -1503,15 +1503,16 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(G7Prob P) {
 }
 
 // Grouped launch: up to G7_MAXP independent problems of one layout (e.g. all weight
-// gradients of a layer, which share K = tokens), one workgroup per work item.
-template <bool AK, bool BKC>
+// gradients of a layer, which share K = tokens), one workgroup per work item.  CAP: a capped
+// grid (tt2_gemm_grouped_ex, gridDim.x a multiple of 8 below G.items) whose block b walks items
+// b, b + gridDim.x, ... (same XCD); a separate instance, because the item loop costs the
+// one-item kernel ~40 VGPR spills.
+template <bool AK, bool BKC, bool CAP>
 __global__ __launch_bounds__(G7_NT, 1) void gemm7g_kernel(G7Group G) {
   __shared__ __attribute__((aligned(1024))) char smem[G7_SMEM];
   __shared__ int span_done;
   span_begin(G.p[0].span, &span_done);
-  // a capped grid (tt2_gemm_grouped_ex, gridDim.x a multiple of 8 below G.items) walks the
-  // items: block b takes b, b + gridDim.x, ... (same XCD); uncapped, one item per block
-  for (int bi = blockIdx.x; bi < G.items; bi += gridDim.x) {
+  for (int bi = blockIdx.x; bi < G.items; bi += CAP ? (int)gridDim.x : G.items) {
     const int u = xcd_item(bi, G.items);
     int p = 0;
 #pragma unroll
@@ -1520,6 +1521,7 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7g_kernel(G7Group G) {
     const G7Prob& P = G.p[p];
     const int local = u - P.item0, nt = P.items / P.splits;
     g7_item<AK, BKC>(P, local % nt, local / nt, smem, G.p[0].span);
+    if (!CAP) break;
     if (bi + (int)gridDim.x < G.items) __syncthreads();   // the epilogue's LDS image is read out
   }
   span_end(G.p[0].span, &span_done, G7_NT / 64);
@@ -2281,17 +2283,24 @@ extern "C" int tt2_gemm_grouped_ex(const tt2_gemm_args* probs, int n, const tt2_
   const int grid = max_groups > 0 ? std::min(G.items, std::max(8, max_groups / 8 * 8)) : G.items;
   ProbeScope ps(stream, grid);
   G.p[0].span = ps.span;
-  if (ps.ext()) {
-#define TT2_G7G(A_, B_) hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_>), dim3(grid), dim3(G7_NT), 0, stream, ps.e0, ps.e1, 0, G)
-    if (!ta && !tb) TT2_G7G(true, true);
-    else if (!ta && tb) TT2_G7G(true, false);
-    else if (ta && !tb) TT2_G7G(false, true);
-    else TT2_G7G(false, false);
+  const bool cap = grid < G.items;
+#define TT2_G7G_ONE(A_, B_, C_)                                                                                  \
+  if (ps.ext())                                                                                                \
+    hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_, C_>), dim3(grid), dim3(G7_NT), 0, stream, ps.e0, ps.e1, 0, G); \
+  else                                                                                                         \
+    hipLaunchKernelGGL((gemm7g_kernel<A_, B_, C_>), dim3(grid), dim3(G7_NT), 0, stream, G);
+#define TT2_G7G(A_, B_)          \
+  if (cap) {                     \
+    TT2_G7G_ONE(A_, B_, true)    \
+  } else {                       \
+    TT2_G7G_ONE(A_, B_, false)   \
+  }
+  if (!ta && !tb) { TT2_G7G(true, true) }
+  else if (!ta && tb) { TT2_G7G(true, false) }
+  else if (ta && !tb) { TT2_G7G(false, true) }
+  else { TT2_G7G(false, false) }
 #undef TT2_G7G
-  } else if (!ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<true, true>), dim3(grid), dim3(G7_NT), 0, stream, G);
-  else if (!ta && tb) hipLaunchKernelGGL((gemm7g_kernel<true, false>), dim3(grid), dim3(G7_NT), 0, stream, G);
-  else if (ta && !tb) hipLaunchKernelGGL((gemm7g_kernel<false, true>), dim3(grid), dim3(G7_NT), 0, stream, G);
-  else hipLaunchKernelGGL((gemm7g_kernel<false, false>), dim3(grid), dim3(G7_NT), 0, stream, G);
+#undef TT2_G7G_ONE
   if (main_only) reduce_blocks = 0;
   G.fin_only = reduce_blocks == 0 && fin_blocks > 0;
   if (G.fin_only)

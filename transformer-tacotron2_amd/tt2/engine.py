@@ -199,7 +199,9 @@ class Arena:
 
 
 class TTSEngine:
-    NORM_RANGES, NORM_PARTS = 64, 32   # overlapped backward: gradient ranges x sumsq partials each
+    # overlapped backward's clip-norm partials: at most NORM_RANGES gradient ranges, each summed by
+    # one work group per NORM_CHUNK gradients (NORM_PARTS_MAX at most; bandwidth-bound either way)
+    NORM_RANGES, NORM_CHUNK, NORM_PARTS_MAX = 64, 1 << 16, 512
 
     def __init__(self, cfg: TTSConfig | None = None, dtype: torch.dtype = torch.bfloat16, device="cuda",
                  seed: int = 0):
@@ -423,8 +425,9 @@ class TTSEngine:
         # (each range final when its job has run): on the side stream without a DP hook, else
         # by optimizer_step once the exchange has finished (same ranges: same result)
         if self._norm_buf is None:
-            self._norm_buf = torch.empty(self.NORM_RANGES * self.NORM_PARTS, dtype=torch.float32, device=self.dev)
+            self._norm_buf = torch.empty(self.NORM_RANGES * self.NORM_PARTS_MAX, dtype=torch.float32, device=self.dev)
         self._norm_ranges, self._norm_hi, self._norm_side = [], self.lay.numel, self.grad_ready_hook is None
+        self._norm_used = 0
 
     def _push_job(self, q, fin=None, ready=()):
         ev = torch.cuda.Event()
@@ -451,13 +454,14 @@ class TTSEngine:
         hi = self._norm_hi
         if lo >= hi:
             return
-        k = len(self._norm_ranges)
-        if k >= self.NORM_RANGES:
+        if len(self._norm_ranges) >= self.NORM_RANGES:
             raise RuntimeError("overlapped backward: more gradient ranges than NORM_RANGES")
-        self._norm_ranges.append((lo, hi))
+        nb = max(1, min(self.NORM_PARTS_MAX, (hi - lo + self.NORM_CHUNK - 1) // self.NORM_CHUNK))
+        self._norm_ranges.append((lo, hi, self._norm_used, nb))
+        self._norm_used += nb
         self._norm_hi = lo
         if self._norm_side:
-            ops.sumsq_parts(self.grads[lo:hi], self._norm_buf[k * self.NORM_PARTS:], self.NORM_PARTS)
+            ops.sumsq_parts(self.grads[lo:hi], self._norm_buf[self._norm_ranges[-1][2]:], nb)
 
     def _start_side(self):
         gate = torch.cuda.Event()
@@ -479,7 +483,7 @@ class TTSEngine:
         torch.cuda.current_stream().wait_stream(self._side)
         self._jobs = None
         self._side_live = False
-        self._norm_pending = (list(self._norm_ranges), self._norm_side)
+        self._norm_pending = (list(self._norm_ranges), self._norm_side, self._norm_used)
 
     def _bias(self, dy, ld, m, n, gb):
         ops.colsum(dy, ld, m, n, gb, ws=self.ws)
@@ -884,12 +888,12 @@ class TTSEngine:
         o = self.opt
         parts = None
         if self._norm_pending is not None:
-            ranges, done = self._norm_pending
+            ranges, done, used = self._norm_pending
             self._norm_pending = None
             if not done:   # DP: the gradients are final (all-reduced) only now
-                for k, (lo, hi) in enumerate(ranges):
-                    ops.sumsq_parts(self.grads[lo:hi], self._norm_buf[k * self.NORM_PARTS:], self.NORM_PARTS)
-            parts = self._norm_buf[:len(ranges) * self.NORM_PARTS]
+                for lo, hi, at, nb in ranges:
+                    ops.sumsq_parts(self.grads[lo:hi], self._norm_buf[at:], nb)
+            parts = self._norm_buf[:used]
         ops.adam_step(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.shadow, self.step_t,
                       self.lay.numel, o["lr"], o["beta1"], o["beta2"], o["eps"], o["weight_decay"], o["clip_norm"],
                       o["warmup"], o["noam"], self.cfg.d_model, ws=self.ws, norm_parts=parts)
