@@ -371,9 +371,9 @@ size_t tt2_layernorm_bwd_workspace_size(const tt2_ln_args* a);
  * = 1, partials still in its workspace), inside the group's split-K reduce launch: a layer's
  * last LayerNorm gradients need no launch of their own.  fin may be NULL; n may be 0. */
 int tt2_gemm_grouped_fin(const tt2_gemm_args* probs, int32_t n, const tt2_ln_args* fin, hipStream_t stream);
-/* tt2_gemm_grouped_fin on at most max_groups work groups (rounded down to a multiple of 8; 0: one
- * work group per 256 x 128 item), each walking several items in XCD order: a launch that runs
- * beside other work on a second stream then leaves the remaining CUs to that work. */
+/* tt2_gemm_grouped_fin with at most max_groups work groups at a time (rounded down to a multiple
+ * of 8; 0: every 256 x 128 item at once): the items go out as consecutive launches of that many,
+ * so a launch beside other work on a second stream leaves the remaining CUs to that work. */
 int tt2_gemm_grouped_ex(const tt2_gemm_args* probs, int32_t n, const tt2_ln_args* fin, int32_t max_groups,
                         hipStream_t stream);
 int tt2_layernorm_bwd(const tt2_ln_args* a, hipStream_t stream);

@@ -93,8 +93,8 @@ def test_overlapped_step_clip_norm_and_graph():
 
 @pytest.mark.parametrize("cap", [8, 64, 200])
 def test_grouped_gemm_grid_cap_bitwise(cap):
-    """tt2_gemm_grouped_ex on `cap` work groups (each walking several 256 x 128 items, some
-    split-K) writes the same bits as one work group per item."""
+    """tt2_gemm_grouped_ex with at most `cap` work groups at a time (consecutive launches of
+    256 x 128 items, some split-K) writes the same bits as one launch of every item."""
     torch.manual_seed(1)
     K = 3000
     probs = []

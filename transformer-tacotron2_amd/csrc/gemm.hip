@@ -1128,6 +1128,7 @@ struct G7Fin {
 struct G7Group {
   G7Prob p[G7_MAXP];
   int np, items;
+  int ibase;   // first item of this launch (a capped grid: several launches)
   G7Fin fin;   // nb == 0: none
   int fin_only;   // the reduce launch holds only the finalize plane (no split problem to reduce)
 };
@@ -1503,27 +1504,22 @@ __global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(G7Prob P) {
 }
 
 // Grouped launch: up to G7_MAXP independent problems of one layout (e.g. all weight
-// gradients of a layer, which share K = tokens), one workgroup per work item.  CAP: a capped
-// grid (tt2_gemm_grouped_ex, gridDim.x a multiple of 8 below G.items) whose block b walks items
-// b, b + gridDim.x, ... (same XCD); a separate instance, because the item loop costs the
-// one-item kernel ~40 VGPR spills.
-template <bool AK, bool BKC, bool CAP>
+// gradients of a layer, which share K = tokens), one workgroup per work item; items
+// G.ibase + blockIdx.x (tt2_gemm_grouped_ex launches a capped grid as several launches of
+// consecutive items, G.ibase a multiple of 8, so block b still runs on XCD b % 8).
+template <bool AK, bool BKC>
 __global__ __launch_bounds__(G7_NT, 1) void gemm7g_kernel(G7Group G) {
   __shared__ __attribute__((aligned(1024))) char smem[G7_SMEM];
   __shared__ int span_done;
   span_begin(G.p[0].span, &span_done);
-  for (int bi = blockIdx.x; bi < G.items; bi += CAP ? (int)gridDim.x : G.items) {
-    const int u = xcd_item(bi, G.items);
-    int p = 0;
+  const int u = xcd_item(G.ibase + blockIdx.x, G.items);
+  int p = 0;
 #pragma unroll
-    for (int i = 1; i < G7_MAXP; ++i)
-      if (i < G.np && u >= G.p[i].item0) p = i;
-    const G7Prob& P = G.p[p];
-    const int local = u - P.item0, nt = P.items / P.splits;
-    g7_item<AK, BKC>(P, local % nt, local / nt, smem, G.p[0].span);
-    if (!CAP) break;
-    if (bi + (int)gridDim.x < G.items) __syncthreads();   // the epilogue's LDS image is read out
-  }
+  for (int i = 1; i < G7_MAXP; ++i)
+    if (i < G.np && u >= G.p[i].item0) p = i;
+  const G7Prob& P = G.p[p];
+  const int local = u - P.item0, nt = P.items / P.splits;
+  g7_item<AK, BKC>(P, local % nt, local / nt, smem, G.p[0].span);
   span_end(G.p[0].span, &span_done, G7_NT / 64);
 }
 
@@ -2278,29 +2274,26 @@ extern "C" int tt2_gemm_grouped_ex(const tt2_gemm_args* probs, int n, const tt2_
     if (fin_blocks) hipLaunchKernelGGL(gemm_splitk_reduce_g, dim3(fin_blocks, 1), dim3(256), 0, stream, G);
     return tt2_check_launch(hipGetLastError(), "tt2_gemm_grouped");
   }
-  // max_groups > 0: at most that many work groups (rounded down to a multiple of 8, >= 8), each
-  // walking several items, so a launch beside other work leaves the rest of the CUs free
+  // max_groups > 0: at most that many work groups at a time (rounded down to a multiple of 8,
+  // >= 8): the items go out as consecutive launches of that many, so a launch beside other
+  // work leaves the rest of the CUs free (no probe span: a capped launch is not one kernel)
   const int grid = max_groups > 0 ? std::min(G.items, std::max(8, max_groups / 8 * 8)) : G.items;
-  ProbeScope ps(stream, grid);
+  ProbeScope ps(stream, grid < G.items ? 0 : grid);
   G.p[0].span = ps.span;
-  const bool cap = grid < G.items;
-#define TT2_G7G_ONE(A_, B_, C_)                                                                                  \
-  if (ps.ext())                                                                                                \
-    hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_, C_>), dim3(grid), dim3(G7_NT), 0, stream, ps.e0, ps.e1, 0, G); \
-  else                                                                                                         \
-    hipLaunchKernelGGL((gemm7g_kernel<A_, B_, C_>), dim3(grid), dim3(G7_NT), 0, stream, G);
-#define TT2_G7G(A_, B_)          \
-  if (cap) {                     \
-    TT2_G7G_ONE(A_, B_, true)    \
-  } else {                       \
-    TT2_G7G_ONE(A_, B_, false)   \
-  }
-  if (!ta && !tb) { TT2_G7G(true, true) }
-  else if (!ta && tb) { TT2_G7G(true, false) }
-  else if (ta && !tb) { TT2_G7G(false, true) }
-  else { TT2_G7G(false, false) }
+  for (G.ibase = 0; G.ibase < G.items; G.ibase += grid) {
+    const dim3 g(std::min(grid, G.items - G.ibase));
+#define TT2_G7G(A_, B_)                                                                                    \
+  if (ps.ext() && grid >= G.items)                                                                       \
+    hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_>), g, dim3(G7_NT), 0, stream, ps.e0, ps.e1, 0, G);        \
+  else                                                                                                   \
+    hipLaunchKernelGGL((gemm7g_kernel<A_, B_>), g, dim3(G7_NT), 0, stream, G);
+    if (!ta && !tb) { TT2_G7G(true, true) }
+    else if (!ta && tb) { TT2_G7G(true, false) }
+    else if (ta && !tb) { TT2_G7G(false, true) }
+    else { TT2_G7G(false, false) }
 #undef TT2_G7G
-#undef TT2_G7G_ONE
+  }
+  G.ibase = 0;
   if (main_only) reduce_blocks = 0;
   G.fin_only = reduce_blocks == 0 && fin_blocks > 0;
   if (G.fin_only)
