@@ -201,7 +201,7 @@ class Arena:
 class TTSEngine:
     # overlapped backward's clip-norm partials: at most NORM_RANGES gradient ranges, each summed by
     # one work group per NORM_CHUNK gradients (NORM_PARTS_MAX at most; bandwidth-bound either way)
-    NORM_RANGES, NORM_CHUNK, NORM_PARTS_MAX = 64, 1 << 16, 512
+    NORM_RANGES, NORM_CHUNK, NORM_PARTS_MAX = 64, 1 << 13, 1024
 
     def __init__(self, cfg: TTSConfig | None = None, dtype: torch.dtype = torch.bfloat16, device="cuda",
                  seed: int = 0):
