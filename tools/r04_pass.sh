@@ -37,7 +37,7 @@ for s in $STEPS; do
           done
         done ;;
     knobs) for e in ${KNOBS:-TT2_SIDE_WG=128 TT2_SIDE_SPLIT=2 TT2_SIDE_START=1 TT2_SIDE_START=3 TT2_WGRAD_OVERLAP=1}; do
-             run "knob $e" 90 200 env $e python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-decode \
+             run "knob $e" 90 200 env ${e//,/ } python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-decode \
                > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
              echo "$e $(lastms "$OUT/ab_run.json")" >> "$OUT/knobs.txt"
            done ;;
