@@ -2277,7 +2277,8 @@ extern "C" int tt2_gemm_grouped_ex(const tt2_gemm_args* probs, int n, const tt2_
   // max_groups > 0: at most that many work groups at a time (rounded down to a multiple of 8,
   // >= 8): the items go out as consecutive launches of that many, so a launch beside other
   // work leaves the rest of the CUs free (no probe span: a capped launch is not one kernel)
-  const int grid = max_groups > 0 ? std::min(G.items, std::max(8, max_groups / 8 * 8)) : G.items;
+  // (an armed launch probe times one kernel: the cap is ignored for it)
+  const int grid = max_groups > 0 && g_probe_armed < 0 ? std::min(G.items, std::max(8, max_groups / 8 * 8)) : G.items;
   ProbeScope ps(stream, grid < G.items ? 0 : grid);
   G.p[0].span = ps.span;
   for (G.ibase = 0; G.ibase < G.items; G.ibase += grid) {
