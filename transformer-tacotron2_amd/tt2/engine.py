@@ -234,6 +234,7 @@ class TTSEngine:
         self.side_split = int(os.environ.get("TT2_SIDE_SPLIT", "1"))
         self.side_groups = int(os.environ.get("TT2_SIDE_WG", "0"))
         self.side_start = int(os.environ.get("TT2_SIDE_START", "-1"))   # decoder layer whose backward starts it
+        self.enc_overlap = int(os.environ.get("TT2_ENC_OVERLAP", "0"))   # see forward()
         self.cd = dtype
         self.dev = torch.device(device)
         self.lay = Layout(build_slots(c))
@@ -506,9 +507,38 @@ class TTSEngine:
         A["mel"].copy_(mel, non_blocking=True)
 
     def forward(self, A: Arena):
-        """Teacher-forced forward: encoder -> decoder -> heads -> post-net."""
-        self.forward_encoder(A)
-        self.forward_decoder(A)
+        """Teacher-forced forward: encoder -> decoder -> heads -> post-net.  enc_overlap (bf16,
+        dev knob TT2_ENC_OVERLAP): the encoder runs on the side stream beside the decoder's
+        pre-net and layer 0's self-attention block, which do not need the memory; 1 issues the
+        encoder first, 2 the decoder's part first (the graph executor follows issue order)."""
+        if self.enc_overlap and self.cd == torch.bfloat16:
+            if self._side is None:
+                self._side = torch.cuda.Stream()
+                self._side_ws = ops.Workspace()
+            main = torch.cuda.current_stream()
+            self._side.wait_stream(main)
+            dec = self._decoder_steps(A)
+
+            def encoder():
+                ws, self.ws = self.ws, self._side_ws
+                try:
+                    with torch.cuda.stream(self._side):
+                        self.forward_encoder(A)
+                finally:
+                    self.ws = ws
+            if self.enc_overlap == 1:
+                encoder()
+                next(dec)
+            else:
+                next(dec)
+                encoder()
+            main.wait_stream(self._side)   # the memory K/V, before layer 0's cross-attention
+            for _ in dec:
+                pass
+        else:
+            self.forward_encoder(A)
+            for _ in self._decoder_steps(A):
+                pass
         if self.training:
             for k in self.nbt:
                 self.nbt[k] += 1
@@ -562,6 +592,13 @@ class TTSEngine:
 
     @ranged("tt2.decoder")
     def forward_decoder(self, A: Arena):
+        for _ in self._decoder_steps(A):
+            pass
+
+    def _decoder_steps(self, A: Arena):
+        """The decoder forward as a generator: it yields once, right before the first use of
+        the encoder memory (layer 0's cross-attention), so forward() can overlap what comes
+        before it with the encoder."""
         c = self.cfg
         B, Tx, Ty, Md = A.B, A.Tx, A.Ty, A.Md
         d, F, H = c.d_model, c.d_ffn, c.n_heads
@@ -592,6 +629,8 @@ class TTSEngine:
             h1 = A[f"dh1{l}"]
             self._lin(h1, self.W(p + "cq.w"), A[f"dcq{l}"], Md, d, d, bias=self.P(p + "cq.b"))
             ko = 2 * d * l
+            if l == 0:
+                yield
             ops.attn_fwd(A[f"dcq{l}"], mkv[:, ko:], mkv[:, ko + d:], A[f"dcatt{l}"], A[f"dclse{l}"], d, kvld, kvld,
                          d, B, H, Ty, Tx, A["text_len"], False, scale)
             self._lin(A[f"dcatt{l}"], self.W(p + "co.w"), A[f"dco{l}"], Md, d, d, bias=self.P(p + "co.b"))
