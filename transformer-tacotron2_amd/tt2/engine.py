@@ -422,13 +422,6 @@ class TTSEngine:
         self._side.wait_stream(torch.cuda.current_stream())
         self._jobs = []
         self._side_live = False
-        # the clip norm's squared sum, one range of the flat gradients per DP bucket boundary
-        # (each range final when its job has run): on the side stream without a DP hook, else
-        # by optimizer_step once the exchange has finished (same ranges: same result)
-        if self._norm_buf is None:
-            self._norm_buf = torch.empty(self.NORM_RANGES * self.NORM_PARTS_MAX, dtype=torch.float32, device=self.dev)
-        self._norm_ranges, self._norm_hi, self._norm_side = [], self.lay.numel, self.grad_ready_hook is None
-        self._norm_used = 0
 
     def _push_job(self, q, fin=None, ready=()):
         ev = torch.cuda.Event()
@@ -447,6 +440,16 @@ class TTSEngine:
                     self.grad_ready_hook(off)
                 self._norm_range(off)
         job["done"] = True
+
+    def _norm_begin(self, side: bool):
+        """The clip norm's squared sum is taken over fixed ranges of the flat gradients, one per
+        DP bucket boundary (_ready), in every schedule, so every schedule clips identically:
+        `side` (overlapped backward without DP): each range on the side stream once its job has
+        run; otherwise all ranges by optimizer_step (with DP: after the exchange)."""
+        if self._norm_buf is None:
+            self._norm_buf = torch.empty(self.NORM_RANGES * self.NORM_PARTS_MAX, dtype=torch.float32, device=self.dev)
+        self._norm_ranges, self._norm_hi, self._norm_side = [], self.lay.numel, side
+        self._norm_used = 0
 
     def _norm_range(self, lo):
         """Gradients [lo, hi) are final (hi: the previous boundary): their squared-norm partials."""
@@ -494,7 +497,6 @@ class TTSEngine:
         torch.cuda.current_stream().wait_stream(self._side)
         self._jobs = None
         self._side_live = False
-        self._norm_pending = (list(self._norm_ranges), self._norm_side, self._norm_used)
 
     def _bias(self, dy, ld, m, n, gb):
         ops.colsum(dy, ld, m, n, gb, ws=self.ws)
@@ -688,8 +690,10 @@ class TTSEngine:
             q, self._wq = self._wq or [], None
             self._push_job(q, ready=[name])
             return
+        off = self.lay.offset(name)
         if self.grad_ready_hook is not None:
-            self.grad_ready_hook(self.lay.offset(name))
+            self.grad_ready_hook(off)
+        self._norm_range(off)
 
     @ranged("tt2.backward")
     def backward(self, A: Arena):
@@ -702,6 +706,7 @@ class TTSEngine:
         ov = self.wgrad_overlap and cd == torch.bfloat16
         self._norm_pending = None
         self._jobs = self._wq = None   # (a backward that raised leaves no queue behind)
+        self._norm_begin(side=ov and self.grad_ready_hook is None)
         if ov:
             self._ov_begin()
         # a weight-gradient dY buffer: per layer (`key`) when the side stream reads it later
@@ -914,6 +919,9 @@ class TTSEngine:
         self._ready("enc.embed")
         if ov:
             self._ov_end()
+        else:
+            self._norm_range(0)
+        self._norm_pending = (list(self._norm_ranges), self._norm_side, self._norm_used)
 
     def _wflip_buf(self, name, cout, cin, K):
         key = ("wflip", name)
