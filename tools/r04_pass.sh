@@ -41,6 +41,7 @@ for s in $STEPS; do
                > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
              echo "$e $(lastms "$OUT/ab_run.json")" >> "$OUT/knobs.txt"
            done ;;
+    otl) run otl 90 200 python -u tools/overlap_timeline.py > "$OUT/otl.txt" 2>&1 ;;
     prof) run prof 150 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
             python3 bench.py --profile-run --steps 10 --warmup 2 > "$OUT/bench_step.json" 2> "$OUT/bench_step.err" ;;
     phases) run phases 120 300 env TT2_LIB=abl/phase.so python -u tools/g7_phases.py --json "$OUT/phases.json" \
