@@ -51,14 +51,16 @@ def _grads(m, b):
     return e.grads.clone()
 
 
-@pytest.mark.parametrize("knobs", [{}, {"side_groups": 64, "side_split": 2}, {"side_start": 2}])
+@pytest.mark.parametrize("knobs", [{"enc_overlap": 0}, {"enc_overlap": 1}, {"enc_overlap": 2, "side_start": 2},
+                                   {"side_groups": 64, "side_split": 2}])
 def test_overlapped_backward_gradients_bitwise(knobs):
     """Same kernels, same split factors (side_split 1), same order per stream: the gradients of
-    the overlapped backward equal the in-place backward's bit for bit; with a capped grid
-    (the items walk the same tiles) too; with side_split 2 the weight gradients take twice the
-    split-K slabs, so those are compared at f32 rounding."""
+    the overlapped backward (with the encoder forward beside the decoder's first block, or not)
+    equal the in-place schedule's bit for bit; with a capped grid (the same tiles) too; with
+    side_split 2 the weight gradients take twice the split-K slabs, so those are compared at f32
+    rounding."""
     b = _batch()
-    ref = _grads(_model(False), b)
+    ref = _grads(_model(False, enc_overlap=0), b)
     got = _grads(_model(True, **knobs), b)
     if knobs.get("side_split", 1) == 1:
         assert torch.equal(ref, got)

@@ -234,7 +234,7 @@ class TTSEngine:
         self.side_split = int(os.environ.get("TT2_SIDE_SPLIT", "1"))
         self.side_groups = int(os.environ.get("TT2_SIDE_WG", "0"))
         self.side_start = int(os.environ.get("TT2_SIDE_START", "-1"))   # decoder layer whose backward starts it
-        self.enc_overlap = int(os.environ.get("TT2_ENC_OVERLAP", "0"))   # see forward()
+        self.enc_overlap = int(os.environ.get("TT2_ENC_OVERLAP", "1"))   # see forward()
         self.cd = dtype
         self.dev = torch.device(device)
         self.lay = Layout(build_slots(c))
@@ -509,10 +509,11 @@ class TTSEngine:
         A["mel"].copy_(mel, non_blocking=True)
 
     def forward(self, A: Arena):
-        """Teacher-forced forward: encoder -> decoder -> heads -> post-net.  enc_overlap (bf16,
-        dev knob TT2_ENC_OVERLAP): the encoder runs on the side stream beside the decoder's
-        pre-net and layer 0's self-attention block, which do not need the memory; 1 issues the
-        encoder first, 2 the decoder's part first (the graph executor follows issue order)."""
+        """Teacher-forced forward: encoder -> decoder -> heads -> post-net.  enc_overlap (bf16;
+        TT2_ENC_OVERLAP, default 1): the encoder runs on the side stream beside the decoder's
+        pre-net and layer 0's self-attention block, which do not need the memory (the step
+        6.94 vs 7.03 ms measured; 1 issues the encoder first, 2 the decoder's part first: the
+        same; 0 off)."""
         if self.enc_overlap and self.cd == torch.bfloat16:
             if self._side is None:
                 self._side = torch.cuda.Stream()
