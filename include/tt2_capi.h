@@ -186,6 +186,8 @@ typedef struct tt2_attn_args {
   float scale;
   int32_t variant;   /* 0 auto (bf16: v3 32x32 swapped MFMA products; f32: v1), 1 v1 (P through LDS),
                         2 v3 with 2-wave workgroups, 3 v3 with 4-wave workgroups (bf16 only) */
+  int32_t parts;     /* bwd: 0 dQ and dK / dV, 1 dQ only, 2 dK / dV only (the non-causal bf16 launch,
+                        whose two halves share no state: two streams may run them side by side) */
 } tt2_attn_args;
 
 /* Alignment diagnostics: probs[b*H + h][q][j] (f32) of a forward already run with these

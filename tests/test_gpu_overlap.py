@@ -52,7 +52,7 @@ def _grads(m, b):
 
 
 @pytest.mark.parametrize("knobs", [{"enc_overlap": 0}, {"enc_overlap": 1}, {"enc_overlap": 2, "side_start": 2},
-                                   {"side_groups": 64, "side_split": 2}])
+                                   {"side_groups": 64, "side_split": 2}, {"xattn_split": 1}])
 def test_overlapped_backward_gradients_bitwise(knobs):
     """Same kernels, same split factors (side_split 1), same order per stream: the gradients of
     the overlapped backward (with the encoder forward beside the decoder's first block, or not)

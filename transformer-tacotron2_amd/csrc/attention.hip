@@ -1089,10 +1089,14 @@ extern "C" int tt2_attn_bwd(const tt2_attn_args* p, hipStream_t s) {
     // Non-causal: dQ and dK / dV workgroups in one launch (the causal case gained nothing
     // from the same fusion)
     if (nq == 4 && nk == 4 && !p->causal) {
-      const int nkb = (p->tk + 127) / 128, nqb = (p->tq + 127) / 128;
+      // parts: both halves (the dK / dV blocks compute delta themselves, the dQ blocks do not
+      // publish it), or one of them alone
+      const int nkb = p->parts == 1 ? 0 : (p->tk + 127) / 128, nqb = p->parts == 2 ? 0 : (p->tq + 127) / 128;
       hipLaunchKernelGGL(attn_bwd_fused3_kernel<4>, dim3(BH, nkb + nqb), dim3(256), 0, s, a, nkb);
       return tt2_check_launch(hipGetLastError(), "tt2_attn_bwd");
     }
+    if (p->parts != 0)
+      return tt2_set_error(TT2_E_INVALID, "tt2_attn_bwd: parts needs the non-causal bf16 launch (4-wave v3)");
     if (nq == 0) hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16>, gprep, dim3(NT), 0, s, a);
     if (nq == 4) hipLaunchKernelGGL(attn_bwd_dq3_kernel<4>, dim3(BH, (p->tq + 127) / 128), dim3(256), 0, s, a);
     else if (nq == 2) hipLaunchKernelGGL(attn_bwd_dq3_kernel<2>, dim3(BH, (p->tq + 63) / 64), dim3(128), 0, s, a);
@@ -1101,6 +1105,7 @@ extern "C" int tt2_attn_bwd(const tt2_attn_args* p, hipStream_t s) {
     else if (nk == 2) hipLaunchKernelGGL(attn_bwd_dkdv3_kernel<2>, dim3(BH, (p->tk + 63) / 64), dim3(128), 0, s, a);
     else hipLaunchKernelGGL(attn_bwd_dkdv_kernel<bf16>, dim3((p->tk + BKV - 1) / BKV, BH), dim3(NT), 0, s, a);
   } else {
+    if (p->parts != 0) return tt2_set_error(TT2_E_INVALID, "tt2_attn_bwd: parts needs bf16");
     hipLaunchKernelGGL(attn_bwd_prep_kernel<float>, gprep, dim3(NT), 0, s, a);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<float>, dim3((p->tq + BQ - 1) / BQ, BH), dim3(NT), 0, s, a);
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<float>, dim3((p->tk + BKV - 1) / BKV, BH), dim3(NT), 0, s, a);

@@ -146,7 +146,7 @@ class AttnArgs(C.Structure):
         ("batch", i32), ("heads", i32), ("head_dim", i32), ("tq", i32), ("tk", i32), ("causal", i32),
         ("dtype", i32),
         ("scale", f32),
-        ("variant", i32),
+        ("variant", i32), ("parts", i32),
     ]
 
 

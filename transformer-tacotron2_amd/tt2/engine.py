@@ -235,6 +235,8 @@ class TTSEngine:
         self.side_groups = int(os.environ.get("TT2_SIDE_WG", "0"))
         self.side_start = int(os.environ.get("TT2_SIDE_START", "-1"))   # decoder layer whose backward starts it
         self.enc_overlap = int(os.environ.get("TT2_ENC_OVERLAP", "1"))   # see forward()
+        # overlapped backward, dev knob: each decoder layer's cross-attention dK / dV on the side
+        self.xattn_split = int(os.environ.get("TT2_XATTN_SPLIT", "0"))
         self.cd = dtype
         self.dev = torch.device(device)
         self.lay = Layout(build_slots(c))
@@ -767,6 +769,7 @@ class TTSEngine:
         mkv = A["mkv"]
         kvld = c.n_dec * 2 * d
         g_mkv = A["g_mkv"]
+        xsplit = ov and self.xattn_split and not self._side_live
         for l in reversed(range(c.n_dec)):
             p, base = f"dec{l}.", SITE_DEC_LAYER + 4 * l
             if ov and l == self.side_start and not self._side_live:
@@ -800,9 +803,20 @@ class TTSEngine:
             self._dgrad(g_br2, self.W(p + "co.w"), A["g_att"], Md, d, d)
             ko = 2 * d * l
             g_cq = gbuf("g_cq", l)
-            ops.attn_bwd(A[f"dcq{l}"], mkv[:, ko:], mkv[:, ko + d:], A[f"dcatt{l}"], A["g_att"], A[f"dclse{l}"],
-                         A["delta"], g_cq, g_mkv[:, ko:], g_mkv[:, ko + d:], d, kvld, kvld, d, d, d, kvld, kvld,
-                         B, H, Ty, Tx, A["text_len"], False, scale)
+            xargs = (A[f"dcq{l}"], mkv[:, ko:], mkv[:, ko + d:], A[f"dcatt{l}"], A["g_att"], A[f"dclse{l}"],
+                     A["delta"], g_cq, g_mkv[:, ko:], g_mkv[:, ko + d:], d, kvld, kvld, d, d, d, kvld, kvld,
+                     B, H, Ty, Tx, A["text_len"], False, scale)
+            if xsplit:
+                # the memory's dK / dV (needed only by the memory gradient after the decoder
+                # backward) on the side stream; dQ (the critical chain) here
+                ev = torch.cuda.Event()
+                ev.record()
+                self._side.wait_event(ev)
+                with torch.cuda.stream(self._side):
+                    ops.attn_bwd(*xargs, parts=2)
+                ops.attn_bwd(*xargs, parts=1)
+            else:
+                ops.attn_bwd(*xargs)
             self._wgrad(g_cq, h1, self.G(p + "cq.w"), d, d, Md, gb=self.G(p + "cq.b"))
             self._dgrad(g_cq, self.W(p + "cq.w"), gx2, Md, d, d, res=A["g_res"])
             gx, gx2 = gx2, gx
@@ -850,6 +864,8 @@ class TTSEngine:
         gf1 = A["g_f1"].view(-1)[:Me * F].view(Me, F)
         gatt = A["g_att"].view(-1)[:Me * d].view(Me, d)
         gq = A["g_qkv"].view(-1)[:Me * 3 * d].view(Me, 3 * d)
+        if xsplit:   # the side stream's dK / dV of every layer's memory are in g_mkv
+            torch.cuda.current_stream().wait_stream(self._side)
         self._dgrad(g_mkv, self.W("dec.kv.w"), gxe, Me, d, kvld)
         if ov and not self._side_live:   # the weight gradients queued so far run beside the encoder backward
             self._start_side()

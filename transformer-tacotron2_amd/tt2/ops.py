@@ -283,9 +283,11 @@ def attn_probs(q, k, lse, probs, q_ld, k_ld, batch, heads, tq, tk, key_len=None,
 
 
 def attn_bwd(q, k, v, o, dout, lse, delta, dq, dk, dv, q_ld, k_ld, v_ld, o_ld, do_ld, dq_ld, dk_ld, dv_ld,
-             batch, heads, tq, tk, key_len=None, causal=False, scale=0.125):
+             batch, heads, tq, tk, key_len=None, causal=False, scale=0.125, parts=0):
+    """parts: 0 dQ and dK / dV, 1 dQ only, 2 dK / dV only (non-causal bf16; see tt2_attn_args)."""
     L = lib()
     a = _attn_common(q, k, v, q_ld, k_ld, v_ld, batch, heads, tq, tk, key_len, causal, scale)
+    a.parts = parts
     a.o, a.dout, a.o_ld, a.do_ld = o.data_ptr(), dout.data_ptr(), o_ld, do_ld
     a.dq, a.dk, a.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
     a.dq_ld, a.dk_ld, a.dv_ld = dq_ld, dk_ld, dv_ld
