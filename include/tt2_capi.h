@@ -517,7 +517,8 @@ size_t tt2_adam_workspace_size(void);
 int tt2_adam_step(const tt2_adam_args* a, hipStream_t stream);
 /* parts[0 .. nparts) = partial sums of g[i]^2 over g[0, n) (fixed split: reproducible) */
 int tt2_sumsq_parts(const float* g, int64_t n, float* parts, int32_t nparts, hipStream_t stream);
-/* step += 1; seed += 1 (seed may be NULL) */
+/* step += 1; seed += 1 (either may be NULL: the pipelined optimizer bumps the dropout seed at the
+ * end of a step and the step counter once the deferred Adam has run) */
 int tt2_step_bump(int32_t* step, uint32_t* seed, hipStream_t stream);
 
 /* ---------------------------------------------------------- block-level entry points

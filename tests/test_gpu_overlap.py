@@ -152,3 +152,32 @@ def test_sumsq_parts_and_adam_norm_parts():
     torch.cuda.synchronize()
     assert (outs[0] - outs[1]).abs().max().item() <= 1e-6
     assert lib().tt2_sumsq_parts(C.c_void_p(g.data_ptr()), n, C.c_void_p(parts.data_ptr()), 0, None) != 0
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_pipelined_optimizer_bitwise(graph):
+    """The pipelined optimizer (each step's Adam deferred to the start of the next forward, the
+    encoder's share on the side stream ahead of the encoder): 3 steps + flush equal 3 plain
+    steps bit for bit (parameters, Adam moments, step counter, dropout seed), eager, and with
+    the captured step (one eager step, then two replays)."""
+    b = _batch()
+    a, p = _model(True), _model(True)
+    p.pipeline_optimizer(True)
+    la = [a.train_step(*b).clone() for _ in range(3)]
+    if graph:
+        lp = [p.train_step(*b).clone()]
+        run = p.capture_train_step(b[0].shape[0], b[0].shape[1], b[2].shape[1])
+        lp += [run(*b).clone() for _ in range(2)]
+    else:
+        lp = [p.train_step(*b).clone() for _ in range(3)]
+    p.flush_optimizer()
+    torch.cuda.synchronize()
+    for x, y in zip(la, lp):
+        assert torch.equal(x, y)
+    ea, ep = a.engine, p.engine
+    assert torch.equal(ea.params, ep.params) and torch.equal(ea.exp_avg, ep.exp_avg)
+    assert torch.equal(ea.exp_avg_sq, ep.exp_avg_sq) and torch.equal(ea.shadow, ep.shadow)
+    assert ea.step_t.item() == ep.step_t.item() == 3 and ea.seed.item() == ep.seed.item()
+    p.flush_optimizer()   # nothing pending: a no-op
+    torch.cuda.synchronize()
+    assert torch.equal(ea.params, ep.params)

@@ -541,7 +541,7 @@ __global__ __launch_bounds__(NT) void adam_kernel(AdamArgs a) {
 
 __global__ void step_bump_kernel(int32_t* step, uint32_t* seed) {
   if (threadIdx.x == 0) {
-    step[0] += 1;
+    if (step) step[0] += 1;
     if (seed) seed[0] += 1u;
   }
 }
@@ -772,6 +772,7 @@ extern "C" int tt2_sumsq_parts(const float* g, int64_t n, float* parts, int32_t 
 }
 
 extern "C" int tt2_step_bump(int32_t* step, uint32_t* seed, hipStream_t s) {
+  if (!step && !seed) return TT2_OK;
   hipLaunchKernelGGL(step_bump_kernel, dim3(1), dim3(64), 0, s, step, seed);
   return tt2_check_launch(hipGetLastError(), "tt2_step_bump");
 }

@@ -235,6 +235,12 @@ class TTSEngine:
         self.side_groups = int(os.environ.get("TT2_SIDE_WG", "0"))
         self.side_start = int(os.environ.get("TT2_SIDE_START", "-1"))   # decoder layer whose backward starts it
         self.enc_overlap = int(os.environ.get("TT2_ENC_OVERLAP", "1"))   # see forward()
+        # pipelined optimizer (opt-in: TransformerTTS.pipeline_optimizer): a step's Adam is
+        # deferred to the start of the next forward, where the encoder's share runs on the side
+        # stream ahead of the encoder and the rest on the main stream ahead of the decoder,
+        # beside the encoder's forward (the same updates in the same order: identical results)
+        self.pipeline_opt = False
+        self._adam_pending = None
         # overlapped backward, dev knob: each decoder layer's cross-attention dK / dV on the side
         self.xattn_split = int(os.environ.get("TT2_XATTN_SPLIT", "0"))
         self.cd = dtype
@@ -516,6 +522,7 @@ class TTSEngine:
         pre-net and layer 0's self-attention block, which do not need the memory (the step
         6.94 vs 7.03 ms measured; 1 issues the encoder first, 2 the decoder's part first: the
         same; 0 off)."""
+        parts, self._adam_pending = self._adam_pending, None   # pipelined optimizer: last step's Adam
         if self.enc_overlap and self.cd == torch.bfloat16:
             if self._side is None:
                 self._side = torch.cuda.Stream()
@@ -523,24 +530,41 @@ class TTSEngine:
             main = torch.cuda.current_stream()
             self._side.wait_stream(main)
             dec = self._decoder_steps(A)
+            enc_r = self._enc_param_ranges() if parts is not None else []
 
             def encoder():
                 ws, self.ws = self.ws, self._side_ws
                 try:
                     with torch.cuda.stream(self._side):
+                        for lo, hi in enc_r:   # the encoder's parameters first
+                            self._adam(lo, hi, parts)
                         self.forward_encoder(A)
                 finally:
                     self.ws = ws
+
+            def rest_adam():   # everything else, ahead of the decoder
+                lo = 0
+                for a, b in enc_r + [(self.lay.numel, self.lay.numel)]:
+                    if a > lo:
+                        self._adam(lo, a, parts)
+                    lo = b
             if self.enc_overlap == 1:
                 encoder()
+                rest_adam()
                 next(dec)
             else:
+                rest_adam()
                 next(dec)
                 encoder()
             main.wait_stream(self._side)   # the memory K/V, before layer 0's cross-attention
+            if parts is not None:
+                ops.step_bump(self.step_t, None)   # both halves of the deferred Adam have read it
             for _ in dec:
                 pass
         else:
+            if parts is not None:
+                self._adam(0, self.lay.numel, parts)
+                ops.step_bump(self.step_t, None)
             self.forward_encoder(A)
             for _ in self._decoder_steps(A):
                 pass
@@ -975,7 +999,6 @@ class TTSEngine:
 
     @ranged("tt2.optimizer")
     def optimizer_step(self):
-        o = self.opt
         parts = None
         if self._norm_pending is not None:
             ranges, done, used = self._norm_pending
@@ -984,7 +1007,34 @@ class TTSEngine:
                 for lo, hi, at, nb in ranges:
                     ops.sumsq_parts(self.grads[lo:hi], self._norm_buf[at:], nb)
             parts = self._norm_buf[:used]
-        ops.adam_step(self.params, self.grads, self.exp_avg, self.exp_avg_sq, self.shadow, self.step_t,
-                      self.lay.numel, o["lr"], o["beta1"], o["beta2"], o["eps"], o["weight_decay"], o["clip_norm"],
-                      o["warmup"], o["noam"], self.cfg.d_model, ws=self.ws, norm_parts=parts)
+        if self.pipeline_opt:
+            # pipelined: this step's Adam runs at the start of the next forward (pending), beside
+            # the encoder; only the dropout seed advances now
+            if parts is None:
+                raise RuntimeError("pipelined optimizer: no clip-norm partial sums (optimizer_step without backward)")
+            self._adam_pending = parts
+            ops.step_bump(None, self.seed)
+            return
+        self._adam(0, self.lay.numel, parts)
         ops.step_bump(self.step_t, self.seed)
+
+    def _adam(self, lo, hi, parts):
+        o = self.opt
+        sl = lambda t: t[lo:hi] if t is not None else None   # noqa: E731
+        ops.adam_step(sl(self.params), sl(self.grads), sl(self.exp_avg), sl(self.exp_avg_sq), sl(self.shadow),
+                      self.step_t, hi - lo, o["lr"], o["beta1"], o["beta2"], o["eps"], o["weight_decay"],
+                      o["clip_norm"], o["warmup"], o["noam"], self.cfg.d_model, ws=self.ws, norm_parts=parts)
+
+    def flush_optimizer(self):
+        """Pipelined optimizer: run the pending Adam now (before parameters are read, saved or
+        evaluated, or pipelining is switched off)."""
+        if self._adam_pending is not None:
+            parts, self._adam_pending = self._adam_pending, None
+            self._adam(0, self.lay.numel, parts)
+            ops.step_bump(self.step_t, None)
+
+    def _enc_param_ranges(self):
+        """Flat ranges the encoder forward reads: the encoder's slots, and the memory K/V
+        projection (dec.kv) that the encoder forward applies."""
+        L = self.lay
+        return [(0, L.offset("dec.fc1.w")), (L.offset("dec.kv.w"), L.offset("dec0.qkv.w"))]

@@ -129,13 +129,31 @@ class TransformerTTS(nn.Module):
         """Per-step dropout seed (uint32), same meaning as the oracle's set_seed."""
         self.engine.seed.fill_(seed)
 
+    def pipeline_optimizer(self, on: bool = True):
+        """Pipelined optimizer (opt-in): each train step's Adam is deferred to the start of the
+        next step's forward, where it runs beside the encoder's forward (the encoder's share on
+        the side stream ahead of the encoder, the rest ahead of the decoder).  Every update is
+        the same as without it, in the same order, so the trajectory is identical; the
+        parameters lag one Adam behind until flush_optimizer() (which state_dict(),
+        save_checkpoint() and infer() call).  A captured step must be taken after at least one
+        pipelined eager step (its graph then holds the deferred Adam)."""
+        if not on:
+            self.engine.flush_optimizer()
+        self.engine.pipeline_opt = on
+
+    def flush_optimizer(self):
+        """Run a pipelined step's pending Adam now."""
+        self.engine.flush_optimizer()
+
     # ------------------------------------------------------------ checkpoint
     def state_dict(self):
         e = self.engine
+        e.flush_optimizer()
         return to_state_dict(self.cfg, e.lay, e.params, e.slay, e.stats, e.nbt)
 
     def load_state_dict(self, sd, strict: bool = True):
         P, S, nbt = from_state_dict(self.cfg, sd)
+        self.engine._adam_pending = None   # a pending pipelined Adam belongs to the replaced weights
         self.engine.load_slots(P, S, nbt)
         self._shadow_version = self.engine.params._version
 
@@ -145,6 +163,7 @@ class TransformerTTS(nn.Module):
         flat layout), the optimizer step, its hyper-parameters and the dropout-seed RNG state.
         Written with torch.save; load_checkpoint resumes bit for bit."""
         e = self.engine
+        e.flush_optimizer()
         ck = {"format": "tt2-train-1", "cfg": self.cfg.to_dict(), "model": self.state_dict(),
               "rng": {"dropout_seed": int(e.seed.item()) & 0xFFFFFFFF}}
         if e.exp_avg is not None:
@@ -298,6 +317,7 @@ class TransformerTTS(nn.Module):
         cross K/V).  Returns (mel_after [B, T, 80] f32, out_len [B]).
         stop_threshold=None forces max_len frames.  prenet_dropout: Tacotron2's pre-net
         dropout stays on at inference; False switches it off (parity runs)."""
+        self.engine.flush_optimizer()
         from .infer import Decoder
         self._sync_shadow()
         B, Tx = text.shape
@@ -392,6 +412,9 @@ class TransformerTTS(nn.Module):
                                "the nccl backend (RCCL, captured)")
         if e.exp_avg is None:
             e.init_optimizer()
+        if e.pipeline_opt and e._adam_pending is None:
+            raise RuntimeError("capture_train_step: with the pipelined optimizer, capture after an eager step "
+                               "(the graph holds that step's deferred Adam)")
         A = e.arena(B, Tx, Ty)
         # the caller's warm-up eager steps size every workspace; capture must not allocate.
         # Every arena buffer exists before capture (the warm-ups may have run the overlapped

@@ -519,7 +519,7 @@ def adam_step(params, grads, m, v, shadow, step, n, lr, beta1=0.9, beta2=0.98, e
 
 
 def step_bump(step, seed=None):
-    check(lib().tt2_step_bump(step.data_ptr(), ptr(seed), stream_ptr()), "tt2_step_bump")
+    check(lib().tt2_step_bump(ptr(step), ptr(seed), stream_ptr()), "tt2_step_bump")
 
 
 def attn_decode(q, k, v, out, q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld, batch, heads, tk, key_len=None,
