@@ -154,14 +154,15 @@ def test_sumsq_parts_and_adam_norm_parts():
     assert lib().tt2_sumsq_parts(C.c_void_p(g.data_ptr()), n, C.c_void_p(parts.data_ptr()), 0, None) != 0
 
 
+@pytest.mark.parametrize("adam_layers", [0, 1])
 @pytest.mark.parametrize("graph", [False, True])
-def test_pipelined_optimizer_bitwise(graph):
+def test_pipelined_optimizer_bitwise(graph, adam_layers):
     """The pipelined optimizer (each step's Adam deferred to the start of the next forward, the
     encoder's share on the side stream ahead of the encoder): 3 steps + flush equal 3 plain
     steps bit for bit (parameters, Adam moments, step counter, dropout seed), eager, and with
     the captured step (one eager step, then two replays)."""
     b = _batch()
-    a, p = _model(True), _model(True)
+    a, p = _model(True), _model(True, adam_layers=adam_layers)
     p.pipeline_optimizer(True)
     la = [a.train_step(*b).clone() for _ in range(3)]
     if graph:

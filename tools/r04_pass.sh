@@ -41,6 +41,18 @@ for s in $STEPS; do
                > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
              echo "$e $(lastms "$OUT/ab_run.json")" >> "$OUT/knobs.txt"
            done ;;
+    pipe) for i in 1 2; do
+            for f in --no-pipeline ""; do
+              run "pipe $f" 90 200 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-decode $f \
+                > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
+              echo "pipe${f:- on} $(lastms "$OUT/ab_run.json")" >> "$OUT/pipe.txt"
+            done
+          done ;;
+    attn) for v in ${ATTN_VARIANTS:-3 4 5 3 4 5}; do
+            run "attn $v" 60 120 env TT2_ATTN_VARIANT=$v python -u tools/attn_bench.py >> "$OUT/attn_v$v.txt" 2>&1
+          done ;;
+    attnt) run attnt 60 300 python -u -m pytest tests/test_gpu_attention.py -x -q --timeout 120 --timeout-method thread \
+             > "$OUT/attn_tests.log" 2>&1 ;;
     otl) run otl 90 200 python -u tools/overlap_timeline.py > "$OUT/otl.txt" 2>&1 ;;
     prof) run prof 150 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
             python3 bench.py --profile-run --steps 10 --warmup 2 > "$OUT/bench_step.json" 2> "$OUT/bench_step.err" ;;

@@ -240,6 +240,10 @@ class TTSEngine:
         # stream ahead of the encoder and the rest on the main stream ahead of the decoder,
         # beside the encoder's forward (the same updates in the same order: identical results)
         self.pipeline_opt = False
+        # pipelined optimizer: each decoder layer's (and the heads' / post-net's) share of the
+        # deferred Adam on the side stream too, the main stream waiting for it at that layer
+        self.adam_layers = int(os.environ.get("TT2_ADAM_LAYERS", "0"))
+        self._layer_wait = None
         self._adam_pending = None
         # overlapped backward, dev knob: each decoder layer's cross-attention dK / dV on the side
         self.xattn_split = int(os.environ.get("TT2_XATTN_SPLIT", "0"))
@@ -548,6 +552,9 @@ class TTSEngine:
                     if a > lo:
                         self._adam(lo, a, parts)
                     lo = b
+            if parts is not None and self.adam_layers and self.enc_overlap == 1:
+                self._forward_adam_layers(A, parts, dec, encoder)
+                return self._count_batches()
             if self.enc_overlap == 1:
                 encoder()
                 rest_adam()
@@ -568,9 +575,51 @@ class TTSEngine:
             self.forward_encoder(A)
             for _ in self._decoder_steps(A):
                 pass
+        self._count_batches()
+
+    def _count_batches(self):
         if self.training:
             for k in self.nbt:
                 self.nbt[k] += 1
+
+    def _forward_adam_layers(self, A, parts, dec, encoder):
+        """forward() with the deferred Adam spread over the side stream (TT2_ADAM_LAYERS): decoder
+        layer 0's share first, then the encoder's (with the encoder forward), then layers 1..5
+        and the heads / post-net; the main stream runs only the decoder pre-net's share and waits
+        for layer l's share right before layer l (and for the rest before the heads).  Every
+        element gets the same update as from one Adam launch."""
+        L, side, main = self.lay, self._side, torch.cuda.current_stream()
+        nd = self.cfg.n_dec
+        cuts = [L.offset(f"dec{l}.qkv.w") for l in range(nd)] + [L.offset("heads.w"), L.numel]
+        evs = [torch.cuda.Event() for _ in range(nd + 1)]
+        ws, self.ws = self.ws, self._side_ws
+        try:
+            with torch.cuda.stream(side):
+                self._adam(cuts[0], cuts[1], parts)
+                evs[0].record(side)
+        finally:
+            self.ws = ws
+        self._adam(L.offset("dec.fc1.w"), L.offset("dec.kv.w"), parts)   # the decoder pre-net
+        encoder()
+        self._layer_wait = lambda l: main.wait_event(evs[l])
+        try:
+            next(dec)
+            main.wait_stream(side)   # the memory K/V, before layer 0's cross-attention
+            ws, self.ws = self.ws, self._side_ws
+            try:
+                with torch.cuda.stream(side):
+                    for l in range(1, nd):
+                        self._adam(cuts[l], cuts[l + 1], parts)
+                        evs[l].record(side)
+                    self._adam(cuts[nd], cuts[nd + 1], parts)
+                    ops.step_bump(self.step_t, None)   # after every share has read it
+                    evs[nd].record(side)
+            finally:
+                self.ws = ws
+            for _ in dec:
+                pass
+        finally:
+            self._layer_wait = None
 
     @ranged("tt2.encoder")
     def forward_encoder(self, A: Arena):
@@ -648,6 +697,8 @@ class TTSEngine:
         # ---------------- decoder layers
         for l in range(c.n_dec):
             p, base = f"dec{l}.", SITE_DEC_LAYER + 4 * l
+            if self._layer_wait is not None:
+                self._layer_wait(l)
             qkv = A[f"dqkv{l}"]
             self._lin(x, self.W(p + "qkv.w"), qkv, Md, 3 * d, d, bias=self.P(p + "qkv.b"))
             ops.attn_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"datt{l}"], A[f"dlse{l}"], 3 * d, 3 * d, 3 * d, d,
@@ -673,6 +724,8 @@ class TTSEngine:
                               A[f"dln3m{l}"], A[f"dln3r{l}"], Md, c.ln_eps, drop=self.drop(base + 3, c.dropout))
             x = A[f"dx{l + 1}"]
         # ---------------- heads (mel 80 + stop 1 in one GEMM, f32 out)
+        if self._layer_wait is not None:
+            self._layer_wait(c.n_dec)
         nh = c.n_mels + 1
         self._lin(x, self.W("heads.w"), A["heads"], Md, nh, d, bias=self.P("heads.b"), ldo=A.heads_ld)
         # ---------------- post-net
