@@ -701,178 +701,6 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
   }
 }
 
-// v5 forward: each wave owns 64 queries as two 32-row blocks over the same K / V fragments
-// (each fragment read from LDS once feeds both blocks' MFMAs: half the LDS reads per score of
-// the v3 kernel), and the two blocks' chains are independent, so one block's softmax (VALU)
-// issues between the other block's MFMAs.  Per query row the operations and their order are
-// the v3 kernel's, so the outputs equal attn_fwd3_kernel's bit for bit.
-// PIPE: the tile body is one basic block (masks and the running-max rescale applied
-// unconditionally: exact, a select and a multiply by 1) whose schedule is pinned: block 1's
-// QK^T MFMAs between block 0's softmax instructions, block 0's PV MFMAs between block 1's.
-template <int NW, bool PIPE>
-__global__ __launch_bounds__(NW * 64) void attn_fwd5_kernel(AttnArgs a) {
-  constexpr int NTH = NW * 64, PER = Stage3<NTH>::PER, QB = 64 * NW;
-  __shared__ __attribute__((aligned(16))) bf16 sK[2][64 * D];
-  __shared__ __attribute__((aligned(16))) bf16 sV[2][64 * D];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int ql = lane & 31, hi = lane >> 5;
-  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
-  const int qblk = a.causal ? (int)gridDim.y - 1 - (int)blockIdx.y : (int)blockIdx.y;
-  const int q0 = qblk * QB, qw = q0 + 64 * w;   // block j: rows qw + 32 j + ql
-  const RowBuf Q = row_buf(reinterpret_cast<const bf16*>(a.q) + (int64_t)b * a.Tq * a.q_ld + h * D, a.q_ld, a.Tq);
-  const RowBuf K = row_buf(reinterpret_cast<const bf16*>(a.k) + (int64_t)b * a.Tk * a.k_ld + h * D, a.k_ld, a.Tk);
-  const RowBuf V = row_buf(reinterpret_cast<const bf16*>(a.v) + (int64_t)b * a.Tk * a.v_ld + h * D, a.v_ld, a.Tk);
-  bf16* O = reinterpret_cast<bf16*>(a.out) + (int64_t)b * a.Tq * a.o_ld + h * D;
-
-  bf16x8 fq[2][4];
-  own_frags(fq[0], Q, qw + ql, hi);
-  own_frags(fq[1], Q, qw + 32 + ql, hi);
-  const float c = a.scale * LOG2E;
-  float m_r[2] = {-INFINITY, -INFINITY}, l_r[2] = {0.f, 0.f};
-  f32x16 o[2][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    zero16(o[j][0]);
-    zero16(o[j][1]);
-  }
-  const int klim = key_limit(a, b);
-  int kend = klim;
-  if (a.causal) kend = min(kend, q0 + QB);
-  const int ntile = kend > 0 ? (kend + 63) / 64 : 0;
-  uint4 rk[PER], rv[PER];
-  if (ntile > 0) {
-    g2r3<NTH>(rk, K, 0, tid);
-    g2r3<NTH>(rv, V, 0, tid);
-    r2s3<NTH>(rk, sK[0], tid);
-    r2s3<NTH>(rv, sV[0], tid);
-  }
-  __syncthreads();
-  // scores of block j -> probabilities (bf16 MFMA operands), running max / sum / rescale
-  auto softmax = [&](f32x16 (&s)[2], int j, int k0, bf16x8 (&pf)[2][2]) {
-    const int qb = qw + 32 * j;
-    if (PIPE || k0 + 64 > klim || (a.causal && k0 + 63 > qb)) {
-      const int lim = (a.causal ? min(klim - 1, qb + ql) : klim - 1) - k0 - 4 * hi;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[kb][r] = 32 * kb + crow(r, 0) > lim ? -INFINITY : s[kb][r];
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
-    mx = xor32_max(mx);
-    const float mn = fmaxf(m_r[j], mx * c);
-    const float base = mn == -INFINITY ? 0.f : mn;
-    if (PIPE || __any(mn != m_r[j])) {
-      const float alpha = fast_exp2(m_r[j] - base);
-      l_r[j] *= alpha;
-#pragma unroll
-      for (int db = 0; db < 2; ++db) o[j][db] *= alpha;
-    }
-    m_r[j] = mn;
-    float rs = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fast_exp2(fmaf(s[kb][r], c, -base));
-        rs += p;
-        pf[kb][r >> 3][r & 7] = (bf16)p;
-      }
-    l_r[j] += rs;
-  };
-  auto tile = [&](auto BUFC, int t) {
-    constexpr int BUF = decltype(BUFC)::value;
-    const int k0 = 64 * t;
-    const bool more = t + 1 < ntile;
-    if (more) {
-      g2r3<NTH>(rk, K, k0 + 64, tid);
-      g2r3<NTH>(rv, V, k0 + 64, tid);
-    }
-    const bf16* cK = sK[BUF];
-    const bf16* cV = sV[BUF];
-    // wave-uniform: a row of the wave is a query and some key of the tile is visible to it
-    // (64-aligned tiles and waves: block 1 sees a tile iff block 0 does)
-    if (qw < a.Tq && !(a.causal && k0 > qw + 31)) {
-      f32x16 s0[2], s1[2];
-      bf16x8 kf[2][4];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int st = 0; st < 4; ++st) kf[kb][st] = rowfrag(cK, 32 * kb + ql, 2 * st + hi);
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        zero16(s0[kb]);
-#pragma unroll
-        for (int st = 0; st < 4; ++st) mma32(kf[kb][st], fq[0][st], s0[kb]);
-      }
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        zero16(s1[kb]);
-#pragma unroll
-        for (int st = 0; st < 4; ++st) mma32(kf[kb][st], fq[1][st], s1[kb]);
-      }
-      bf16x8 pf0[2][2], pf1[2][2];
-      softmax(s0, 0, k0, pf0);
-      bf16x8 vf[2][2][2];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            vf[kb][hh][db] = trfrag(cV, 32 * kb + 16 * hh, db, lane);
-            mma32(vf[kb][hh][db], pf0[kb][hh], o[0][db]);
-          }
-      softmax(s1, 1, k0, pf1);
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-          for (int db = 0; db < 2; ++db) mma32(vf[kb][hh][db], pf1[kb][hh], o[1][db]);
-      if constexpr (PIPE) {
-        // K fragments, block 0's QK^T; block 1's QK^T between block 0's softmax; V fragments;
-        // block 0's PV between block 1's softmax; block 1's PV
-        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 24, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 24, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-      }
-    }
-    if (more) {
-      r2s3<NTH>(rk, sK[BUF ^ 1], tid);
-      r2s3<NTH>(rv, sV[BUF ^ 1], tid);
-    }
-    __syncthreads();
-  };
-  for (int t = 0; t < ntile; t += 2) {
-    tile(std::integral_constant<int, 0>{}, t);
-    if (t + 1 < ntile) tile(std::integral_constant<int, 1>{}, t + 1);
-  }
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int qv = qw + 32 * j + ql;
-    const float l = xor32_sum(l_r[j]);
-    if (qv < a.Tq) {
-      store_rowT(O + (int64_t)qv * a.o_ld, o[j], l > 0.f ? 1.f / l : 0.f, hi);
-      if (hi == 0) a.lse[(int64_t)bh * a.Tq + qv] = l > 0.f ? m_r[j] + log2f(l) : INFINITY;
-    }
-  }
-}
-
 // dQ: wave = 32 queries (query on the lane), workgroup walks 64-key tiles in two
 // 32-key halves.
 template <int NW>
@@ -1150,332 +978,6 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_fused3_kernel(AttnArgs a, in
   else attn_bwd_dq3_body<NW>(a, blockIdx.x, (int)blockIdx.y - nkb, (int)gridDim.y - nkb, smem, false);
 }
 
-// ---------------------------------------------------------------- v5 backward
-// The v3 bodies with each wave owning 64 rows as two 32-row blocks: the dQ wave's 64 queries
-// share every K / V fragment it reads from LDS, the dK / dV wave's 64 keys share every Q / dO
-// fragment and the tile's LSE / delta values.  A block whose rows see no key of a 32-wide half
-// computes zero probabilities there (the v3 wave would skip it): adding exact zeros leaves
-// every accumulator's bits as the v3 kernels leave them.
-template <int NW>
-TT2_DEV void attn_bwd_dq5_body(const AttnArgs& a, int bx, int by, int ny, char* smem, bool publish) {
-  constexpr int NTH = NW * 64, PER = Stage3<NTH>::PER, QB = 64 * NW;
-  bf16 (*sK)[64 * D] = reinterpret_cast<bf16 (*)[64 * D]>(smem);
-  bf16 (*sV)[64 * D] = reinterpret_cast<bf16 (*)[64 * D]>(smem + 2 * 64 * D * sizeof(bf16));
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int ql = lane & 31, hi = lane >> 5;
-  const int bh = bx, b = bh / a.H, h = bh % a.H;
-  const int qblk = a.causal ? ny - 1 - by : by;
-  const int q0 = qblk * QB, qw = q0 + 64 * w;
-  const RowBuf Q = row_buf(reinterpret_cast<const bf16*>(a.q) + (int64_t)b * a.Tq * a.q_ld + h * D, a.q_ld, a.Tq);
-  const RowBuf dO =
-      row_buf(reinterpret_cast<const bf16*>(a.dout) + (int64_t)b * a.Tq * a.do_ld + h * D, a.do_ld, a.Tq);
-  const RowBuf K = row_buf(reinterpret_cast<const bf16*>(a.k) + (int64_t)b * a.Tk * a.k_ld + h * D, a.k_ld, a.Tk);
-  const RowBuf V = row_buf(reinterpret_cast<const bf16*>(a.v) + (int64_t)b * a.Tk * a.v_ld + h * D, a.v_ld, a.Tk);
-  const RowBuf Ob = row_buf(reinterpret_cast<const bf16*>(a.o) + (int64_t)b * a.Tq * a.o_ld + h * D, a.o_ld, a.Tq);
-  bf16* dQ = reinterpret_cast<bf16*>(a.dq) + (int64_t)b * a.Tq * a.dq_ld + h * D;
-
-  bf16x8 fq[2][4], fdo[2][4];
-  float lse[2], dl[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int qv = qw + 32 * j + ql;
-    const bool qok = qv < a.Tq;
-    bf16x8 fo[4];
-    own_frags(fq[j], Q, qv, hi);
-    own_frags(fdo[j], dO, qv, hi);
-    own_frags(fo, Ob, qv, hi);
-    float dsum = 0.f;
-#pragma unroll
-    for (int st = 0; st < 4; ++st)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dsum += (float)fdo[j][st][e] * (float)fo[st][e];
-    dsum += __shfl_xor(dsum, 32, 64);
-    dl[j] = qok ? dsum : 0.f;
-    lse[j] = qok ? a.lse[(int64_t)bh * a.Tq + qv] : INFINITY;
-    if (publish && qok && hi == 0) a.delta[(int64_t)bh * a.Tq + qv] = dsum;
-  }
-  const float c = a.scale * LOG2E;
-  f32x16 dq[2][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    zero16(dq[j][0]);
-    zero16(dq[j][1]);
-  }
-  const int klim = key_limit(a, b);
-  int kend = klim;
-  if (a.causal) kend = min(kend, q0 + QB);
-  const int ntile = kend > 0 ? (kend + 63) / 64 : 0;
-  uint4 rk[PER], rv[PER];
-  if (ntile > 0) {
-    g2r3<NTH>(rk, K, 0, tid);
-    g2r3<NTH>(rv, V, 0, tid);
-    r2s3<NTH>(rk, sK[0], tid);
-    r2s3<NTH>(rv, sV[0], tid);
-  }
-  __syncthreads();
-  // probabilities -> dS of block j over one 32-key half
-  auto dsoft = [&](const f32x16& s, const f32x16& dp, int j, int kb0, bf16x8 (&dsf)[2]) {
-    float p[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) p[r] = fast_exp2(fmaf(s[r], c, -lse[j]));
-    const int qb = qw + 32 * j;
-    if (kb0 + 32 > klim || (a.causal && kb0 + 31 > qb)) {
-      const int lim = (a.causal ? min(klim - 1, qb + ql) : klim - 1) - kb0 - 4 * hi;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) p[r] = crow(r, 0) > lim ? 0.f : p[r];
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dsf[r >> 3][r & 7] = (bf16)(p[r] * (dp[r] - dl[j]));
-  };
-  auto tile = [&](auto BUFC, int t) {
-    constexpr int BUF = decltype(BUFC)::value;
-    const int k0 = 64 * t;
-    const bool more = t + 1 < ntile;
-    if (more) {
-      g2r3<NTH>(rk, K, k0 + 64, tid);
-      g2r3<NTH>(rv, V, k0 + 64, tid);
-    }
-    const bf16* cK = sK[BUF];
-    const bf16* cV = sV[BUF];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int kb0 = k0 + 32 * kb;
-      if (qw >= a.Tq || (a.causal && kb0 > qw + 63)) continue;   // wave-uniform: no block sees the half
-      f32x16 s[2], dp[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        zero16(s[j]);
-        zero16(dp[j]);
-      }
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const bf16x8 kf = rowfrag(cK, 32 * kb + ql, 2 * st + hi);
-        const bf16x8 vf = rowfrag(cV, 32 * kb + ql, 2 * st + hi);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          mma32(kf, fq[j][st], s[j]);
-          mma32(vf, fdo[j][st], dp[j]);
-        }
-      }
-      bf16x8 dsf0[2], dsf1[2];
-      dsoft(s[0], dp[0], 0, kb0, dsf0);
-      bf16x8 kt[2][2];
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          kt[hh][db] = trfrag(cK, 32 * kb + 16 * hh, db, lane);
-          mma32(kt[hh][db], dsf0[hh], dq[0][db]);
-        }
-      dsoft(s[1], dp[1], 1, kb0, dsf1);
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int db = 0; db < 2; ++db) mma32(kt[hh][db], dsf1[hh], dq[1][db]);
-    }
-    if (more) {
-      r2s3<NTH>(rk, sK[BUF ^ 1], tid);
-      r2s3<NTH>(rv, sV[BUF ^ 1], tid);
-    }
-    __syncthreads();
-  };
-  for (int t = 0; t < ntile; t += 2) {
-    tile(std::integral_constant<int, 0>{}, t);
-    if (t + 1 < ntile) tile(std::integral_constant<int, 1>{}, t + 1);
-  }
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int qv = qw + 32 * j + ql;
-    if (qv < a.Tq) store_rowT(dQ + (int64_t)qv * a.dq_ld, dq[j], a.scale, hi);
-  }
-}
-
-template <int NW>
-TT2_DEV void attn_bwd_dkdv5_body(const AttnArgs& a, int bx, int by, char* smem, bool self_delta) {
-  constexpr int NTH = NW * 64, PER = Stage3<NTH>::PER, KB = 64 * NW;
-  bf16 (*sQ)[64 * D] = reinterpret_cast<bf16 (*)[64 * D]>(smem);
-  bf16 (*sdO)[64 * D] = reinterpret_cast<bf16 (*)[64 * D]>(smem + 2 * 64 * D * sizeof(bf16));
-  float (*sL)[64] = reinterpret_cast<float (*)[64]>(smem + 4 * 64 * D * sizeof(bf16));
-  float (*sDl)[64] = reinterpret_cast<float (*)[64]>(smem + 4 * 64 * D * sizeof(bf16) + 2 * 64 * sizeof(float));
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int kl = lane & 31, hi = lane >> 5;
-  const int bh = bx, b = bh / a.H, h = bh % a.H;
-  const int k0 = by * KB, kw = k0 + 64 * w;   // block j: keys kw + 32 j + kl
-  const RowBuf Q = row_buf(reinterpret_cast<const bf16*>(a.q) + (int64_t)b * a.Tq * a.q_ld + h * D, a.q_ld, a.Tq);
-  const RowBuf dO =
-      row_buf(reinterpret_cast<const bf16*>(a.dout) + (int64_t)b * a.Tq * a.do_ld + h * D, a.do_ld, a.Tq);
-  const RowBuf K = row_buf(reinterpret_cast<const bf16*>(a.k) + (int64_t)b * a.Tk * a.k_ld + h * D, a.k_ld, a.Tk);
-  const RowBuf V = row_buf(reinterpret_cast<const bf16*>(a.v) + (int64_t)b * a.Tk * a.v_ld + h * D, a.v_ld, a.Tk);
-  const RowBuf Ob = row_buf(reinterpret_cast<const bf16*>(a.o) + (int64_t)b * a.Tq * a.o_ld + h * D, a.o_ld, a.Tq);
-  bf16* dK = reinterpret_cast<bf16*>(a.dk) + (int64_t)b * a.Tk * a.dk_ld + h * D;
-  bf16* dV = reinterpret_cast<bf16*>(a.dv) + (int64_t)b * a.Tk * a.dv_ld + h * D;
-  const float* LSE = a.lse + (int64_t)bh * a.Tq;
-  const float* DL = a.delta + (int64_t)bh * a.Tq;
-
-  bf16x8 fk[2][4], fv[2][4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    own_frags(fk[j], K, kw + 32 * j + kl, hi);
-    own_frags(fv[j], V, kw + 32 * j + kl, hi);
-  }
-  const float c = a.scale * LOG2E;
-  f32x16 dk[2][2], dv[2][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      zero16(dk[j][db]);
-      zero16(dv[j][db]);
-    }
-  const int klim = key_limit(a, b);
-  const int qstart = a.causal ? (k0 / 64) * 64 : 0;
-  const int ntile = k0 < klim && a.Tq > qstart ? (a.Tq - qstart + 63) / 64 : 0;
-  uint4 rq[PER], rd[PER], ro[PER];
-  auto stats = [&](int buf, int qb) {
-    if (tid < 64) {
-      const int q = qb + tid;
-      sL[buf][tid] = q < a.Tq ? LSE[q] : INFINITY;
-      if (!self_delta) sDl[buf][tid] = q < a.Tq ? DL[q] : 0.f;
-    }
-    if (self_delta) {
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        union { uint4 u; bf16x8 v; } x, y;
-        x.u = rd[i];
-        y.u = ro[i];
-        float d = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d += (float)x.v[e] * (float)y.v[e];
-        d += __shfl_xor(d, 1, 64);
-        d += __shfl_xor(d, 2, 64);
-        d += __shfl_xor(d, 4, 64);
-        if ((tid & 7) == 0) sDl[buf][(tid + NTH * i) >> 3] = d;
-      }
-    }
-  };
-  if (ntile > 0) {
-    g2r3<NTH>(rq, Q, qstart, tid);
-    g2r3<NTH>(rd, dO, qstart, tid);
-    if (self_delta) g2r3<NTH>(ro, Ob, qstart, tid);
-    r2s3<NTH>(rq, sQ[0], tid);
-    r2s3<NTH>(rd, sdO[0], tid);
-    stats(0, qstart);
-  }
-  __syncthreads();
-  auto tile = [&](auto BUFC, int t) {
-    constexpr int BUF = decltype(BUFC)::value;
-    const int q0 = qstart + 64 * t;
-    const bool more = t + 1 < ntile;
-    if (more) {
-      g2r3<NTH>(rq, Q, q0 + 64, tid);
-      g2r3<NTH>(rd, dO, q0 + 64, tid);
-      if (self_delta) g2r3<NTH>(ro, Ob, q0 + 64, tid);
-    }
-    const bf16* cQ = sQ[BUF];
-    const bf16* cD = sdO[BUF];
-    const float* cL = sL[BUF];
-    const float* cDl = sDl[BUF];
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      const int qb0 = q0 + 32 * qb;
-      if (kw >= klim || (a.causal && qb0 + 31 < kw)) continue;   // wave-uniform: block 0 (the lower keys) sees nothing
-      f32x16 s[2], dp[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        zero16(s[j]);
-        zero16(dp[j]);
-      }
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const bf16x8 qf = rowfrag(cQ, 32 * qb + kl, 2 * st + hi);
-        const bf16x8 df = rowfrag(cD, 32 * qb + kl, 2 * st + hi);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          mma32(qf, fk[j][st], s[j]);
-          mma32(df, fv[j][st], dp[j]);
-        }
-      }
-      float L[16], Dl[16];
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int qi = 32 * qb + 8 * rr + 4 * hi;
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(cL + qi);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(cDl + qi);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          L[4 * rr + i] = l4[i];
-          Dl[4 * rr + i] = d4[i];
-        }
-      }
-      bf16x8 pf[2][2], dsf[2][2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int kwj = kw + 32 * j, kv = kwj + kl;
-        float p[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) p[r] = fast_exp2(fmaf(s[j][r], c, -L[r]));
-        if (kwj + 32 > klim || (a.causal && qb0 < kwj + 31)) {
-          const int qlo = (kv >= klim ? 1 << 20 : (a.causal ? kv - qb0 : -1)) - 4 * hi;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) p[r] = crow(r, 0) < qlo ? 0.f : p[r];
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          pf[j][r >> 3][r & 7] = (bf16)p[r];
-          dsf[j][r >> 3][r & 7] = (bf16)(p[r] * (dp[j][r] - Dl[r]));
-        }
-      }
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          const bf16x8 dT = trfrag(cD, 32 * qb + 16 * hh, db, lane);
-          const bf16x8 qT = trfrag(cQ, 32 * qb + 16 * hh, db, lane);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            mma32(dT, pf[j][hh], dv[j][db]);
-            mma32(qT, dsf[j][hh], dk[j][db]);
-          }
-        }
-    }
-    if (more) {
-      r2s3<NTH>(rq, sQ[BUF ^ 1], tid);
-      r2s3<NTH>(rd, sdO[BUF ^ 1], tid);
-      stats(BUF ^ 1, q0 + 64);
-    }
-    __syncthreads();
-  };
-  for (int t = 0; t < ntile; t += 2) {
-    tile(std::integral_constant<int, 0>{}, t);
-    if (t + 1 < ntile) tile(std::integral_constant<int, 1>{}, t + 1);
-  }
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int kv = kw + 32 * j + kl;
-    if (kv < a.Tk) {
-      store_rowT(dK + (int64_t)kv * a.dk_ld, dk[j], a.scale, hi);
-      store_rowT(dV + (int64_t)kv * a.dv_ld, dv[j], 1.f, hi);
-    }
-  }
-}
-
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dq5_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * 64 * D * sizeof(bf16)];
-  attn_bwd_dq5_body<NW>(a, blockIdx.x, blockIdx.y, gridDim.y, smem, true);
-}
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv5_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[ATTN_BWD3_SMEM];
-  attn_bwd_dkdv5_body<NW>(a, blockIdx.x, blockIdx.y, smem, false);
-}
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_bwd_fused5_kernel(AttnArgs a, int nkb) {
-  __shared__ __attribute__((aligned(16))) char smem[ATTN_BWD3_SMEM];
-  if ((int)blockIdx.y < nkb) attn_bwd_dkdv5_body<NW>(a, blockIdx.x, blockIdx.y, smem, true);
-  else attn_bwd_dq5_body<NW>(a, blockIdx.x, (int)blockIdx.y - nkb, (int)gridDim.y - nkb, smem, false);
-}
-
 AttnArgs to_args(const tt2_attn_args* p) {
   AttnArgs a;
   a.q = p->q; a.k = p->k; a.v = p->v; a.o = p->o; a.dout = p->dout;
@@ -1561,17 +1063,7 @@ extern "C" int tt2_attn_fwd(const tt2_attn_args* p, hipStream_t s) {
   if (p->batch * p->tq == 0) return TT2_OK;
   AttnArgs a = to_args(p);
   const int nw = v3_waves(p, p->tq, true);
-  if (p->dtype == TT2_DT_BF16 && p->variant >= 4 && p->variant <= 6) {   // v5: 64 queries per wave
-    if (p->variant == 4)
-      hipLaunchKernelGGL((attn_fwd5_kernel<2, false>), dim3(p->batch * p->heads, (p->tq + 127) / 128), dim3(128), 0,
-                         s, a);
-    else if (p->variant == 5)
-      hipLaunchKernelGGL((attn_fwd5_kernel<4, false>), dim3(p->batch * p->heads, (p->tq + 255) / 256), dim3(256), 0,
-                         s, a);
-    else
-      hipLaunchKernelGGL((attn_fwd5_kernel<2, true>), dim3(p->batch * p->heads, (p->tq + 127) / 128), dim3(128), 0,
-                         s, a);
-  } else if (nw == 4) {
+  if (nw == 4) {
     hipLaunchKernelGGL(attn_fwd3_kernel<4>, dim3(p->batch * p->heads, (p->tq + 127) / 128), dim3(256), 0, s, a);
   } else if (nw == 2) {
     hipLaunchKernelGGL(attn_fwd3_kernel<2>, dim3(p->batch * p->heads, (p->tq + 63) / 64), dim3(128), 0, s, a);
@@ -1592,19 +1084,6 @@ extern "C" int tt2_attn_bwd(const tt2_attn_args* p, hipStream_t s) {
   const int BH = p->batch * p->heads;
   dim3 gprep((p->batch * p->tq + 3) / 4);
   if (p->dtype == TT2_DT_BF16) {
-    if (p->variant >= 4 && p->variant <= 6) {   // v5: 64 rows per wave, 2-wave workgroups
-      const int nkb = (p->tk + 127) / 128, nqb = (p->tq + 127) / 128;
-      if (!p->causal) {
-        const int kb = p->parts == 1 ? 0 : nkb, qb = p->parts == 2 ? 0 : nqb;
-        hipLaunchKernelGGL(attn_bwd_fused5_kernel<2>, dim3(BH, kb + qb), dim3(128), 0, s, a, kb);
-        return tt2_check_launch(hipGetLastError(), "tt2_attn_bwd");
-      }
-      if (p->parts != 0)
-        return tt2_set_error(TT2_E_INVALID, "tt2_attn_bwd: parts needs the non-causal bf16 launch");
-      hipLaunchKernelGGL(attn_bwd_dq5_kernel<2>, dim3(BH, nqb), dim3(128), 0, s, a);
-      hipLaunchKernelGGL(attn_bwd_dkdv5_kernel<2>, dim3(BH, nkb), dim3(128), 0, s, a);
-      return tt2_check_launch(hipGetLastError(), "tt2_attn_bwd");
-    }
     const int nq = v3_waves(p, p->tq, false), nk = v3_waves(p, p->tk, false);
     // the v3 dQ kernel computes delta = rowsum(dO * O) itself (and stores it for dK / dV).
     // Non-causal: dQ and dK / dV workgroups in one launch (the causal case gained nothing
