@@ -4,7 +4,7 @@ serialises the dispatches it times, the spans are recorded by the kernels themse
 an unprofiled replay, so kernels of the overlapped backward's side stream show where they
 really run against the main stream's.
 
-    python tools/overlap_timeline.py [--from-ms X]
+    python tools/overlap_timeline.py [--from-ms X] [--pipeline]
 """
 import ctypes as C
 import os
@@ -28,6 +28,8 @@ def main():
     model = TransformerTTS(TTSConfig(), dtype=torch.bfloat16)
     model.configure_optimizer(lr=1e-4, warmup=4000.0, clip_norm=1.0)
     model.train()
+    if "--pipeline" in sys.argv:   # the bench's mode: the deferred Adam in the forward
+        model.pipeline_optimizer(True)
     text, tl, mel, ml = bench.synth_batch(0)
     for _ in range(2):
         model.train_step(text, tl, mel, ml)

@@ -17,7 +17,7 @@ run() {   # run <name> <need_s> <timeout_s> <cmd...>
   local t=$(date +%s)
   timeout -k 10 "$to" "$@"
   local rc=$?
-  echo "$name rc=$rc $(( $(date +%s) - t ))s" >> "$OUT/pass.txt"
+  echo "$name rc=$rc $(( $(date +%s) - t ))s left=$(left)" >> "$OUT/pass.txt"
   echo "$name rc=$rc" >&2
   case $rc in 124|137|134|139) echo "stop after $name" >&2; cat "$OUT/pass.txt" >&2; exit $rc ;; esac
   return 0
@@ -54,6 +54,7 @@ for s in $STEPS; do
     attnt) run attnt 60 300 python -u -m pytest tests/test_gpu_attention.py -x -q --timeout 120 --timeout-method thread \
              > "$OUT/attn_tests.log" 2>&1 ;;
     otl) run otl 90 200 python -u tools/overlap_timeline.py > "$OUT/otl.txt" 2>&1 ;;
+    otlp) run otlp 90 200 python -u tools/overlap_timeline.py --pipeline > "$OUT/otlp.txt" 2>&1 ;;
     prof) run prof 150 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
             python3 bench.py --profile-run --steps 10 --warmup 2 > "$OUT/bench_step.json" 2> "$OUT/bench_step.err" ;;
     phases) run phases 120 300 env TT2_LIB=abl/phase.so python -u tools/g7_phases.py --json "$OUT/phases.json" \
@@ -65,6 +66,13 @@ for s in $STEPS; do
                echo "$lib $(python -c "import json,sys;print(json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])['decode']['value'])" "$OUT/dec_run.json" 2>&1 | tail -1)" >> "$OUT/decab.txt"
              done
            done ;;
+    pmc) run pmc_f 120 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
+           python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-decode > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.err"
+         run pmc_w 120 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
+           python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-decode > "$OUT/bench_write.json" 2> "$OUT/bench_write.err" ;;
+    mfma) run mfma 120 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/mfma" -o run \
+            --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-decode --no-cpu-baseline --no-ragged \
+            > "$OUT/bench_mfma.json" 2> "$OUT/bench_mfma.err" ;;
     dpmc) run dpmc_f 120 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/dtr/fetch" -o run --output-format csv -- \
             python3 tools/decode_traffic.py --out="$OUT/dtr" > "$OUT/dtr_fetch.log" 2>&1
           run dpmc_w 120 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/dtr/write" -o run --output-format csv -- \

@@ -243,7 +243,8 @@ class TTSEngine:
         # pipelined optimizer: each decoder layer's (and the heads' / post-net's) share of the
         # deferred Adam on the side stream too, the main stream waiting for it at that layer
         self.adam_layers = int(os.environ.get("TT2_ADAM_LAYERS", "0"))
-        self._layer_wait = None
+        self._layer_wait = self._enc_wait = None
+        self._adam_stream = self._adam_ws = None
         self._adam_pending = None
         # overlapped backward, dev knob: each decoder layer's cross-attention dK / dV on the side
         self.xattn_split = int(os.environ.get("TT2_XATTN_SPLIT", "0"))
@@ -547,13 +548,15 @@ class TTSEngine:
                     self.ws = ws
 
             def rest_adam():   # everything else, ahead of the decoder
+                if parts is None:
+                    return
                 lo = 0
                 for a, b in enc_r + [(self.lay.numel, self.lay.numel)]:
                     if a > lo:
                         self._adam(lo, a, parts)
                     lo = b
             if parts is not None and self.adam_layers and self.enc_overlap == 1:
-                self._forward_adam_layers(A, parts, dec, encoder)
+                self._forward_adam_layers(A, parts, dec)
                 return self._count_batches()
             if self.enc_overlap == 1:
                 encoder()
@@ -582,44 +585,57 @@ class TTSEngine:
             for k in self.nbt:
                 self.nbt[k] += 1
 
-    def _forward_adam_layers(self, A, parts, dec, encoder):
-        """forward() with the deferred Adam spread over the side stream (TT2_ADAM_LAYERS): decoder
-        layer 0's share first, then the encoder's (with the encoder forward), then layers 1..5
-        and the heads / post-net; the main stream runs only the decoder pre-net's share and waits
-        for layer l's share right before layer l (and for the rest before the heads).  Every
-        element gets the same update as from one Adam launch."""
+    def _forward_adam_layers(self, A, parts, dec):
+        """forward() with the deferred Adam on a stream of its own (TT2_ADAM_LAYERS=1), in the
+        order the forward reads the parameters: the encoder's pre-net and each encoder layer's
+        share, the memory K/V projection's, the decoder pre-net's, each decoder layer's, the
+        heads' and post-net's.  The encoder (side stream) waits for each layer's share right
+        before that layer, the decoder (main stream) likewise, so the Adam runs beside the
+        encoder's latency-bound chain instead of ahead of it.  Every element gets the update one
+        Adam launch would give it (same clip coefficient from the same norm partials)."""
         L, side, main = self.lay, self._side, torch.cuda.current_stream()
-        nd = self.cfg.n_dec
-        cuts = [L.offset(f"dec{l}.qkv.w") for l in range(nd)] + [L.offset("heads.w"), L.numel]
-        evs = [torch.cuda.Event() for _ in range(nd + 1)]
-        ws, self.ws = self.ws, self._side_ws
+        c = self.cfg
+        ne, nd = c.n_enc, c.n_dec
+        if self._adam_stream is None:
+            self._adam_stream = torch.cuda.Stream()
+            self._adam_ws = ops.Workspace()
+        xs = self._adam_stream
+        xs.wait_stream(main)
+        eo = [L.offset(f"enc{l}.qkv.w") for l in range(ne)] + [L.offset("dec.fc1.w")]
+        do = [L.offset(f"dec{l}.qkv.w") for l in range(nd)] + [L.offset("heads.w"), L.numel]
+        kv0, kv1 = L.offset("dec.kv.w"), L.offset("dec0.qkv.w")
+        shares = ([(("e", -1), 0, eo[0])] + [(("e", l), eo[l], eo[l + 1]) for l in range(ne)]
+                  + [(("kv", 0), kv0, kv1), (("p", 0), eo[ne], kv0)]
+                  + [(("d", l), do[l], do[l + 1]) for l in range(nd)] + [(("d", nd), do[nd], do[nd + 1])])
+        ev = {}
+        ws, self.ws = self.ws, self._adam_ws
         try:
-            with torch.cuda.stream(side):
-                self._adam(cuts[0], cuts[1], parts)
-                evs[0].record(side)
+            with torch.cuda.stream(xs):
+                for key, lo, hi in shares:
+                    self._adam(lo, hi, parts)
+                    ev[key] = torch.cuda.Event()
+                    ev[key].record(xs)
+                ops.step_bump(self.step_t, None)   # after every share has read it
+                ev[("d", nd)] = torch.cuda.Event()
+                ev[("d", nd)].record(xs)           # the heads wait for this one: joins the stream
         finally:
             self.ws = ws
-        self._adam(L.offset("dec.fc1.w"), L.offset("dec.kv.w"), parts)   # the decoder pre-net
-        encoder()
-        self._layer_wait = lambda l: main.wait_event(evs[l])
+        self._enc_wait = lambda key: side.wait_event(ev[key])
+        self._layer_wait = lambda l: main.wait_event(ev[("d", l)])
         try:
-            next(dec)
-            main.wait_stream(side)   # the memory K/V, before layer 0's cross-attention
+            main.wait_event(ev[("p", 0)])
             ws, self.ws = self.ws, self._side_ws
             try:
                 with torch.cuda.stream(side):
-                    for l in range(1, nd):
-                        self._adam(cuts[l], cuts[l + 1], parts)
-                        evs[l].record(side)
-                    self._adam(cuts[nd], cuts[nd + 1], parts)
-                    ops.step_bump(self.step_t, None)   # after every share has read it
-                    evs[nd].record(side)
+                    self.forward_encoder(A)
             finally:
                 self.ws = ws
+            next(dec)
+            main.wait_stream(side)   # the memory K/V, before layer 0's cross-attention
             for _ in dec:
                 pass
         finally:
-            self._layer_wait = None
+            self._layer_wait = self._enc_wait = None
 
     @ranged("tt2.encoder")
     def forward_encoder(self, A: Arena):
@@ -632,6 +648,8 @@ class TTSEngine:
         tr = self.training
         scale = 1.0 / math.sqrt(c.head_dim)
         # ---------------- encoder pre-net
+        if self._enc_wait is not None:
+            self._enc_wait(("e", -1))
         ops.embedding_fwd(A["text"], self.W("enc.embed"), A["emb"], Me, c.vocab)
         x = A["emb"]
         for i in range(c.enc_conv_layers):
@@ -650,6 +668,8 @@ class TTSEngine:
         # ---------------- encoder layers
         for l in range(c.n_enc):
             p, base = f"enc{l}.", SITE_ENC_LAYER + 4 * l
+            if self._enc_wait is not None:
+                self._enc_wait(("e", l))
             qkv = A[f"eqkv{l}"]
             self._lin(x, self.W(p + "qkv.w"), qkv, Me, 3 * d, d, bias=self.P(p + "qkv.b"))
             ops.attn_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"eatt{l}"], A[f"else{l}"], 3 * d, 3 * d, 3 * d, d,
@@ -666,6 +686,8 @@ class TTSEngine:
             x = A[f"ex{l + 1}"]
         mem = x
         # one GEMM projects the memory to K/V for all decoder layers
+        if self._enc_wait is not None:
+            self._enc_wait(("kv", 0))
         self._lin(mem, self.W("dec.kv.w"), A["mkv"], Me, c.n_dec * 2 * d, d, bias=self.P("dec.kv.b"))
 
     @ranged("tt2.decoder")
