@@ -19,6 +19,9 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# one dispatch per step in every schedule (the pipelined optimizer splits Adam over two launches
+# in the next step's forward): the loss kernel's dispatches delimit the steps
+DELIM = "_ZN12_GLOBAL__N_111loss_kernel"
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from summarize_step import short  # noqa: E402
 
@@ -48,8 +51,8 @@ def main(tag: str, src: str | None = None):
     K, W = bench["steps"], bench["warmup"]
     rows = list(csv.DictReader(open(trace)))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in rows)
-    adam = [e for e in ev if e[2].startswith("adam_kernel")]
-    assert len(adam) >= W + 2 + K + 1, f"{len(adam)} adam dispatches, expected >= {W + 2 + K + 1}"
+    adam = [e for e in ev if e[2].startswith(DELIM)]
+    assert len(adam) >= W + 2 + K + 1, f"{len(adam)} {DELIM} dispatches, expected >= {W + 2 + K + 1}"
     seams: dict[tuple[str, str], list] = {}
     hist = [0] * 8   # < 1, 1-2, 2-3, 3-4, 4-6, 6-10, 10-20, >= 20 us
     edges = [1, 2, 3, 4, 6, 10, 20]
@@ -62,9 +65,9 @@ def main(tag: str, src: str | None = None):
         g, busy = gaps(win)
         wall += t1 - t0
         busy_tot += busy
-        # the idle time between the previous step's adam and this step's first dispatch
+        # the idle time between the previous step's loss and this window's first dispatch
         lead = win[0][0] - t0
-        g.insert(0, (lead, "adam_kernel(prev step)", win[0][2]))
+        g.insert(0, (lead, "loss_kernel(prev step)", win[0][2]))
         for ns, a, b in g:
             gap_tot += ns
             us = ns / 1e3

@@ -21,6 +21,9 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# one dispatch per step in every schedule (the pipelined optimizer splits Adam over two launches
+# in the next step's forward): the loss kernel's dispatches delimit the steps
+DELIM = "_ZN12_GLOBAL__N_111loss_kernel"
 
 
 def short(name: str) -> str:
@@ -36,9 +39,9 @@ def main(tag: str, src: str | None = None):
     K, W = bench["steps"], bench["warmup"]
     rows = list(csv.DictReader(open(trace)))
     ev = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows))
-    adam = [e for e in ev if short(e[2]).startswith("adam_kernel")]
+    adam = [e for e in ev if short(e[2]).startswith(DELIM)]
     # W eager + 2 untimed replays + K timed, then the probe steps (eager, graph-node replays)
-    assert len(adam) >= W + 2 + K + 1, f"{len(adam)} adam dispatches, expected >= {W + 2 + K + 1}"
+    assert len(adam) >= W + 2 + K + 1, f"{len(adam)} {DELIM} dispatches, expected >= {W + 2 + K + 1}"
     t0, t1 = adam[W + 1][1], adam[W + 1 + K][1]
     timed = [e for e in ev if e[0] >= t0 and e[1] <= t1]
     wall_ms = (t1 - t0) / 1e6 / K
@@ -52,7 +55,7 @@ def main(tag: str, src: str | None = None):
     lines = [f"# Timed training steps under rocprofv3 — {tag}", "",
              f"`rocprofv3 --kernel-trace --stats -- python3 bench.py --profile-run --steps {K} --warmup {W}` "
              f"(tools/prof_step.sh); summary by tools/summarize_step.py over the {K} timed graph replays only "
-             "(the adam dispatches delimit steps; eager warm-up, untimed replays and the probe step excluded).", "",
+             "(the loss-kernel dispatches delimit steps; eager warm-up, untimed replays and the probe step excluded).", "",
              f"bench under the profiler: {bench['ms_per_step']} ms/step.  Timed window: {wall_ms:.3f} ms/step "
              f"wall, {busy / 1e3:.3f} ms/step of kernel time, {len(timed) / K:.0f} kernels/step.", "",
              "| kernel | launches/step | avg us | ms/step | % of kernel time |", "|---|---|---|---|---|"]
