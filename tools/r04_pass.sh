@@ -53,6 +53,7 @@ for s in $STEPS; do
           done ;;
     attnt) run attnt 60 300 python -u -m pytest tests/test_gpu_attention.py -x -q --timeout 120 --timeout-method thread \
              > "$OUT/attn_tests.log" 2>&1 ;;
+    encg) run encg 60 200 python -u tools/enc_gemm_ab.py > "$OUT/enc_gemm.txt" 2>&1 ;;
     otl) run otl 90 200 python -u tools/overlap_timeline.py > "$OUT/otl.txt" 2>&1 ;;
     otlp) run otlp 90 200 python -u tools/overlap_timeline.py --pipeline > "$OUT/otlp.txt" 2>&1 ;;
     prof) run prof 150 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \

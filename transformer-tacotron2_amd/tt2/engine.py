@@ -528,7 +528,10 @@ class TTSEngine:
         6.94 vs 7.03 ms measured; 1 issues the encoder first, 2 the decoder's part first: the
         same; 0 off)."""
         parts, self._adam_pending = self._adam_pending, None   # pipelined optimizer: last step's Adam
-        if self.enc_overlap and self.cd == torch.bfloat16:
+        # not with SyncBatchNorm: its statistics exchange forked onto the comm stream from the side
+        # stream made the captured step's hipStreamEndCapture segfault (ROCm 7.2, RCCL in-graph,
+        # tests/test_gpu_dist.py cfg2 sync_bn); the encoder then runs on the main stream
+        if self.enc_overlap and self.cd == torch.bfloat16 and self.bn_sync is None:
             if self._side is None:
                 self._side = torch.cuda.Stream()
                 self._side_ws = ops.Workspace()
