@@ -599,9 +599,7 @@ class TTSEngine:
         L, side, main = self.lay, self._side, torch.cuda.current_stream()
         c = self.cfg
         ne, nd = c.n_enc, c.n_dec
-        if self._adam_stream is None:
-            self._adam_stream = torch.cuda.Stream()
-            self._adam_ws = ops.Workspace()
+        self._adam_stream_ready()
         xs = self._adam_stream
         xs.wait_stream(main)
         eo = [L.offset(f"enc{l}.qkv.w") for l in range(ne)] + [L.offset("dec.fc1.w")]
@@ -639,6 +637,14 @@ class TTSEngine:
                 pass
         finally:
             self._layer_wait = self._enc_wait = None
+
+    def _adam_stream_ready(self):
+        """The TT2_ADAM_LAYERS stream and its Adam workspace, sized outside any capture (the
+        pipelined optimizer_step calls this, so the eager step before a capture has)."""
+        if self._adam_stream is None:
+            self._adam_stream = torch.cuda.Stream()
+            self._adam_ws = ops.Workspace()
+            self._adam_ws.get(ops.lib().tt2_adam_workspace_size())
 
     @ranged("tt2.encoder")
     def forward_encoder(self, A: Arena):
@@ -1092,6 +1098,8 @@ class TTSEngine:
                 raise RuntimeError("pipelined optimizer: no clip-norm partial sums (optimizer_step without backward)")
             self._adam_pending = parts
             ops.step_bump(None, self.seed)
+            if self.adam_layers and not torch.cuda.is_current_stream_capturing():
+                self._adam_stream_ready()
             return
         self._adam(0, self.lay.numel, parts)
         ops.step_bump(self.step_t, self.seed)
