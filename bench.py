@@ -483,8 +483,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="run each step's Adam at its end (default: pipelined into the next step, identical updates)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="pipelined optimizer: each step's Adam at the start of the next step, beside the encoder "
+                         "(identical updates; measured neutral, DESIGN.md section 0.3)")
+    ap.add_argument("--no-pipeline", action="store_true", help="(the default) each step's Adam at its end")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the cfg3 / cfg5 decode measurements")
     ap.add_argument("--no-longform", action="store_true", help="skip the cfg5 long-form decode measurement")
@@ -534,7 +536,7 @@ def main():
     model.train()
     # pipelined optimizer: each step's Adam runs at the start of the next step beside the encoder
     # forward (identical updates); the last step's Adam is flushed INSIDE the timed region
-    pipelined = not args.no_pipeline
+    pipelined = args.pipeline and not args.no_pipeline
     model.pipeline_optimizer(pipelined)
     text, tl, mel, ml = synth_batch(rank)
     sync_fn = sync.finish if sync is not None else None

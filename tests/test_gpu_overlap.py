@@ -51,7 +51,8 @@ def _grads(m, b):
     return e.grads.clone()
 
 
-@pytest.mark.parametrize("knobs", [{"enc_overlap": 0}, {"enc_overlap": 1}, {"enc_overlap": 2, "side_start": 2},
+@pytest.mark.parametrize("knobs", [{"enc_overlap": 0}, {"enc_overlap": 1}, {"enc_overlap": 1, "enc_prio": 1},
+                                   {"enc_overlap": 2, "side_start": 2},
                                    {"side_groups": 64, "side_split": 2}, {"xattn_split": 1}])
 def test_overlapped_backward_gradients_bitwise(knobs):
     """Same kernels, same split factors (side_split 1), same order per stream: the gradients of
@@ -154,15 +155,14 @@ def test_sumsq_parts_and_adam_norm_parts():
     assert lib().tt2_sumsq_parts(C.c_void_p(g.data_ptr()), n, C.c_void_p(parts.data_ptr()), 0, None) != 0
 
 
-@pytest.mark.parametrize("adam_layers", [0, 1])
 @pytest.mark.parametrize("graph", [False, True])
-def test_pipelined_optimizer_bitwise(graph, adam_layers):
+def test_pipelined_optimizer_bitwise(graph):
     """The pipelined optimizer (each step's Adam deferred to the start of the next forward, the
     encoder's share on the side stream ahead of the encoder): 3 steps + flush equal 3 plain
     steps bit for bit (parameters, Adam moments, step counter, dropout seed), eager, and with
     the captured step (one eager step, then two replays)."""
     b = _batch()
-    a, p = _model(True), _model(True, adam_layers=adam_layers)
+    a, p = _model(True), _model(True)
     p.pipeline_optimizer(True)
     la = [a.train_step(*b).clone() for _ in range(3)]
     if graph:

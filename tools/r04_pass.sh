@@ -42,10 +42,10 @@ for s in $STEPS; do
              echo "$e $(lastms "$OUT/ab_run.json")" >> "$OUT/knobs.txt"
            done ;;
     pipe) for i in 1 2; do
-            for f in --no-pipeline ""; do
+            for f in --pipeline ""; do
               run "pipe $f" 90 200 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-decode $f \
                 > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
-              echo "pipe${f:- on} $(lastms "$OUT/ab_run.json")" >> "$OUT/pipe.txt"
+              echo "pipe${f:- off} $(lastms "$OUT/ab_run.json")" >> "$OUT/pipe.txt"
             done
           done ;;
     attn) for v in ${ATTN_VARIANTS:-3 4 5 3 4 5}; do

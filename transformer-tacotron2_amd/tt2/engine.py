@@ -240,11 +240,10 @@ class TTSEngine:
         # stream ahead of the encoder and the rest on the main stream ahead of the decoder,
         # beside the encoder's forward (the same updates in the same order: identical results)
         self.pipeline_opt = False
-        # pipelined optimizer: each decoder layer's (and the heads' / post-net's) share of the
-        # deferred Adam on the side stream too, the main stream waiting for it at that layer
-        self.adam_layers = int(os.environ.get("TT2_ADAM_LAYERS", "0"))
-        self._layer_wait = self._enc_wait = None
-        self._adam_stream = self._adam_ws = None
+        # encoder forward stream (enc_overlap) at high priority (dev knob TT2_ENC_PRIO): the
+        # encoder chain is the forward's critical path; its work groups then dispatch first
+        self.enc_prio = int(os.environ.get("TT2_ENC_PRIO", "0"))
+        self._enc_side = None
         self._adam_pending = None
         # overlapped backward, dev knob: each decoder layer's cross-attention dK / dV on the side
         self.xattn_split = int(os.environ.get("TT2_XATTN_SPLIT", "0"))
@@ -535,15 +534,18 @@ class TTSEngine:
             if self._side is None:
                 self._side = torch.cuda.Stream()
                 self._side_ws = ops.Workspace()
+            if self._enc_side is None:
+                self._enc_side = torch.cuda.Stream(priority=-1) if self.enc_prio else self._side
+            side = self._enc_side
             main = torch.cuda.current_stream()
-            self._side.wait_stream(main)
+            side.wait_stream(main)
             dec = self._decoder_steps(A)
             enc_r = self._enc_param_ranges() if parts is not None else []
 
             def encoder():
                 ws, self.ws = self.ws, self._side_ws
                 try:
-                    with torch.cuda.stream(self._side):
+                    with torch.cuda.stream(side):
                         for lo, hi in enc_r:   # the encoder's parameters first
                             self._adam(lo, hi, parts)
                         self.forward_encoder(A)
@@ -558,9 +560,6 @@ class TTSEngine:
                     if a > lo:
                         self._adam(lo, a, parts)
                     lo = b
-            if parts is not None and self.adam_layers and self.enc_overlap == 1:
-                self._forward_adam_layers(A, parts, dec)
-                return self._count_batches()
             if self.enc_overlap == 1:
                 encoder()
                 rest_adam()
@@ -569,7 +568,7 @@ class TTSEngine:
                 rest_adam()
                 next(dec)
                 encoder()
-            main.wait_stream(self._side)   # the memory K/V, before layer 0's cross-attention
+            main.wait_stream(side)   # the memory K/V, before layer 0's cross-attention
             if parts is not None:
                 ops.step_bump(self.step_t, None)   # both halves of the deferred Adam have read it
             for _ in dec:
@@ -588,64 +587,6 @@ class TTSEngine:
             for k in self.nbt:
                 self.nbt[k] += 1
 
-    def _forward_adam_layers(self, A, parts, dec):
-        """forward() with the deferred Adam on a stream of its own (TT2_ADAM_LAYERS=1), in the
-        order the forward reads the parameters: the encoder's pre-net and each encoder layer's
-        share, the memory K/V projection's, the decoder pre-net's, each decoder layer's, the
-        heads' and post-net's.  The encoder (side stream) waits for each layer's share right
-        before that layer, the decoder (main stream) likewise, so the Adam runs beside the
-        encoder's latency-bound chain instead of ahead of it.  Every element gets the update one
-        Adam launch would give it (same clip coefficient from the same norm partials)."""
-        L, side, main = self.lay, self._side, torch.cuda.current_stream()
-        c = self.cfg
-        ne, nd = c.n_enc, c.n_dec
-        self._adam_stream_ready()
-        xs = self._adam_stream
-        xs.wait_stream(main)
-        eo = [L.offset(f"enc{l}.qkv.w") for l in range(ne)] + [L.offset("dec.fc1.w")]
-        do = [L.offset(f"dec{l}.qkv.w") for l in range(nd)] + [L.offset("heads.w"), L.numel]
-        kv0, kv1 = L.offset("dec.kv.w"), L.offset("dec0.qkv.w")
-        shares = ([(("e", -1), 0, eo[0])] + [(("e", l), eo[l], eo[l + 1]) for l in range(ne)]
-                  + [(("kv", 0), kv0, kv1), (("p", 0), eo[ne], kv0)]
-                  + [(("d", l), do[l], do[l + 1]) for l in range(nd)] + [(("d", nd), do[nd], do[nd + 1])])
-        ev = {}
-        ws, self.ws = self.ws, self._adam_ws
-        try:
-            with torch.cuda.stream(xs):
-                for key, lo, hi in shares:
-                    self._adam(lo, hi, parts)
-                    ev[key] = torch.cuda.Event()
-                    ev[key].record(xs)
-                ops.step_bump(self.step_t, None)   # after every share has read it
-                ev[("d", nd)] = torch.cuda.Event()
-                ev[("d", nd)].record(xs)           # the heads wait for this one: joins the stream
-        finally:
-            self.ws = ws
-        self._enc_wait = lambda key: side.wait_event(ev[key])
-        self._layer_wait = lambda l: main.wait_event(ev[("d", l)])
-        try:
-            main.wait_event(ev[("p", 0)])
-            ws, self.ws = self.ws, self._side_ws
-            try:
-                with torch.cuda.stream(side):
-                    self.forward_encoder(A)
-            finally:
-                self.ws = ws
-            next(dec)
-            main.wait_stream(side)   # the memory K/V, before layer 0's cross-attention
-            for _ in dec:
-                pass
-        finally:
-            self._layer_wait = self._enc_wait = None
-
-    def _adam_stream_ready(self):
-        """The TT2_ADAM_LAYERS stream and its Adam workspace, sized outside any capture (the
-        pipelined optimizer_step calls this, so the eager step before a capture has)."""
-        if self._adam_stream is None:
-            self._adam_stream = torch.cuda.Stream()
-            self._adam_ws = ops.Workspace()
-            self._adam_ws.get(ops.lib().tt2_adam_workspace_size())
-
     @ranged("tt2.encoder")
     def forward_encoder(self, A: Arena):
         """Encoder pre-net + layers, then the K/V projection of the memory for
@@ -657,8 +598,6 @@ class TTSEngine:
         tr = self.training
         scale = 1.0 / math.sqrt(c.head_dim)
         # ---------------- encoder pre-net
-        if self._enc_wait is not None:
-            self._enc_wait(("e", -1))
         ops.embedding_fwd(A["text"], self.W("enc.embed"), A["emb"], Me, c.vocab)
         x = A["emb"]
         for i in range(c.enc_conv_layers):
@@ -677,8 +616,6 @@ class TTSEngine:
         # ---------------- encoder layers
         for l in range(c.n_enc):
             p, base = f"enc{l}.", SITE_ENC_LAYER + 4 * l
-            if self._enc_wait is not None:
-                self._enc_wait(("e", l))
             qkv = A[f"eqkv{l}"]
             self._lin(x, self.W(p + "qkv.w"), qkv, Me, 3 * d, d, bias=self.P(p + "qkv.b"))
             ops.attn_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"eatt{l}"], A[f"else{l}"], 3 * d, 3 * d, 3 * d, d,
@@ -695,8 +632,6 @@ class TTSEngine:
             x = A[f"ex{l + 1}"]
         mem = x
         # one GEMM projects the memory to K/V for all decoder layers
-        if self._enc_wait is not None:
-            self._enc_wait(("kv", 0))
         self._lin(mem, self.W("dec.kv.w"), A["mkv"], Me, c.n_dec * 2 * d, d, bias=self.P("dec.kv.b"))
 
     @ranged("tt2.decoder")
@@ -728,8 +663,6 @@ class TTSEngine:
         # ---------------- decoder layers
         for l in range(c.n_dec):
             p, base = f"dec{l}.", SITE_DEC_LAYER + 4 * l
-            if self._layer_wait is not None:
-                self._layer_wait(l)
             qkv = A[f"dqkv{l}"]
             self._lin(x, self.W(p + "qkv.w"), qkv, Md, 3 * d, d, bias=self.P(p + "qkv.b"))
             ops.attn_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], A[f"datt{l}"], A[f"dlse{l}"], 3 * d, 3 * d, 3 * d, d,
@@ -755,8 +688,6 @@ class TTSEngine:
                               A[f"dln3m{l}"], A[f"dln3r{l}"], Md, c.ln_eps, drop=self.drop(base + 3, c.dropout))
             x = A[f"dx{l + 1}"]
         # ---------------- heads (mel 80 + stop 1 in one GEMM, f32 out)
-        if self._layer_wait is not None:
-            self._layer_wait(c.n_dec)
         nh = c.n_mels + 1
         self._lin(x, self.W("heads.w"), A["heads"], Md, nh, d, bias=self.P("heads.b"), ldo=A.heads_ld)
         # ---------------- post-net
@@ -1098,8 +1029,6 @@ class TTSEngine:
                 raise RuntimeError("pipelined optimizer: no clip-norm partial sums (optimizer_step without backward)")
             self._adam_pending = parts
             ops.step_bump(None, self.seed)
-            if self.adam_layers and not torch.cuda.is_current_stream_capturing():
-                self._adam_stream_ready()
             return
         self._adam(0, self.lay.numel, parts)
         ops.step_bump(self.step_t, self.seed)
