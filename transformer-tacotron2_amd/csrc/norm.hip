@@ -170,8 +170,8 @@ __global__ __launch_bounds__(NT) void ln_combine_kernel(const T* x, const float*
 }
 
 // Backward: 8 waves per workgroup, one 512-wide row per wave at a time, software-
-// pipelined: the raw x / branch / dy chunks of the wave's next row are loaded before the
-// current row is reduced, so every wave always has a row of loads in flight.  The
+// pipelined: the raw x / branch / dy chunks of the wave's next two rows are loaded before the
+// current two are reduced, so every wave always has two rows of loads in flight.  The
 // dropout keep-mask of an element is hashed once and used for both s = x + drop(br)
 // and dbranch = drop(ds).  Per-workgroup (dgamma, dbeta, dbias) column partials go to
 // part[block][3][C]; ln_bwd_finalize sums them (fixed order: bitwise reproducible).
@@ -237,11 +237,8 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
   for (int j = 0; j < 8; ++j) pg[j] = pb[j] = pd[j] = 0.f;
   const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
   const int stride = gridDim.x * 8;
-  int row = blockIdx.x * 8 + w;
-  LnRow<T> cur, nxt;
-  if (row < a.M) ln_row_load<T>(cur, a, row, c0);
-  for (; row < a.M; row += stride) {
-    if (row + stride < a.M) ln_row_load<T>(nxt, a, row + stride, c0);
+  // one row of the wave: s = x + drop(br), the LN backward, dx / dbranch, column partials
+  auto row_bwd = [&](const LnRow<T>& cur, int row) {
     const int64_t off = (int64_t)row * a.C + c0;
     float s[8], dy[8], keep[8];
     unpack8<T>(cur.x, s);
@@ -279,7 +276,21 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
     }
     st8nt(reinterpret_cast<T*>(a.dx) + off, ds);
     if (a.dbranch) st8nt(reinterpret_cast<T*>(a.dbranch) + off, db);
-    cur = nxt;
+  };
+  // two rows per iteration with the next two in flight (up to four rows of loads per wave:
+  // one row of lookahead left the HBM queue half empty); rows in the same order as one at a
+  // time, so the column partials are summed in the same order
+  int row = blockIdx.x * 8 + w;
+  LnRow<T> r0, r1, n0, n1;
+  if (row < a.M) ln_row_load<T>(r0, a, row, c0);
+  if (row + stride < a.M) ln_row_load<T>(r1, a, row + stride, c0);
+  for (; row < a.M; row += 2 * stride) {
+    if (row + 2 * stride < a.M) ln_row_load<T>(n0, a, row + 2 * stride, c0);
+    if (row + 3 * stride < a.M) ln_row_load<T>(n1, a, row + 3 * stride, c0);
+    row_bwd(r0, row);
+    if (row + stride < a.M) row_bwd(r1, row + stride);
+    r0 = n0;
+    r1 = n1;
   }
   // 8 waves -> 4 rows of LDS partials -> 1
   if (w >= 4) {
