@@ -402,15 +402,23 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   if (rl < nrl) {
-    for (int r = r0 + rl; r < r1; r += nrl) {
-      float v[8];
-      ld8(y + (int64_t)r * a.C + cg * 8, v);
+    // 4 rows' loads in flight per thread, then the rows in their order (the sums as one row
+    // at a time: one row of loads per thread left the HBM queue mostly empty)
+    for (int r = r0 + rl; r < r1; r += 4 * nrl) {
+      float v[4][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = v[j] - k[j];
-        s1[j] += d;
-        s2[j] += d * d;
-      }
+      for (int u = 0; u < 4; ++u)
+        if (r + u * nrl < r1) ld8(y + (int64_t)(r + u * nrl) * a.C + cg * 8, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (r + u * nrl < r1) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float d = v[u][j] - k[j];
+            s1[j] += d;
+            s2[j] += d * d;
+          }
+        }
     }
   }
 #pragma unroll
@@ -622,19 +630,30 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   col8(a.mean, c0, mu); col8(a.rstd, c0, rs); col8(a.gamma, c0, g); col8(a.beta, c0, b);
   if (rl < nrl) {
-    for (int r = r0 + rl; r < r1; r += nrl) {
-      const int64_t i0 = (int64_t)r * a.C + c0;
-      float v[8], d[8], kp[8];
-      ld8(y + i0, v);
-      ld8(dout + i0, d);
-      bn_keep8(a, seed, i0, kp);
+    // 4 rows' loads in flight per thread, then the rows in their order (as bn_stats_kernel)
+    for (int r = r0 + rl; r < r1; r += 4 * nrl) {
+      float v[4][8], d[4][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xh = (v[j] - mu[j]) * rs[j];
-        const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[j]);
-        s1[j] += dp;
-        s2[j] += dp * xh;
-      }
+      for (int u = 0; u < 4; ++u)
+        if (r + u * nrl < r1) {
+          const int64_t i0 = (int64_t)(r + u * nrl) * a.C + c0;
+          ld8(y + i0, v[u]);
+          ld8(dout + i0, d[u]);
+        }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (r + u * nrl < r1) {
+          const int64_t i0 = (int64_t)(r + u * nrl) * a.C + c0;
+          float kp[8];
+          bn_keep8(a, seed, i0, kp);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xh = (v[u][j] - mu[j]) * rs[j];
+            const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[u][j]);
+            s1[j] += dp;
+            s2[j] += dp * xh;
+          }
+        }
     }
   }
 #pragma unroll
