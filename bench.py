@@ -336,7 +336,7 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
     traffic, tsrc = None, None
     prof = os.path.join(ROOT, "profiles")
     tfiles = sorted(f for f in os.listdir(prof) if f.endswith("_traffic.json")
-                    and not f.endswith("_decode_traffic.json")) if os.path.isdir(prof) else []
+                    and not f.endswith(("_decode_traffic.json", "_longform_traffic.json"))) if os.path.isdir(prof) else []
     if tfiles:
         t = json.load(open(os.path.join(prof, tfiles[-1])))
         if t.get("kernel", "") == kname:

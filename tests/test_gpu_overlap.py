@@ -51,7 +51,7 @@ def _grads(m, b):
     return e.grads.clone()
 
 
-@pytest.mark.parametrize("knobs", [{"enc_overlap": 0}, {"enc_overlap": 1}, {"enc_overlap": 1, "enc_prio": 1},
+@pytest.mark.parametrize("knobs", [{"enc_overlap": 0}, {"enc_overlap": 1},
                                    {"enc_overlap": 2, "side_start": 2},
                                    {"side_groups": 64, "side_split": 2}, {"xattn_split": 1}])
 def test_overlapped_backward_gradients_bitwise(knobs):

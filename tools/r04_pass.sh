@@ -54,6 +54,11 @@ for s in $STEPS; do
     attnt) run attnt 60 300 python -u -m pytest tests/test_gpu_attention.py -x -q --timeout 120 --timeout-method thread \
              > "$OUT/attn_tests.log" 2>&1 ;;
     encg) run encg 60 200 python -u tools/enc_gemm_ab.py > "$OUT/enc_gemm.txt" 2>&1 ;;
+    normab) for i in 1 2; do
+              for lib in abl/norm0.so transformer-tacotron2_amd/tt2/libtt2.so; do
+                run "normab $lib" 60 120 env TT2_LIB=$lib python -u tools/norm_ab.py >> "$OUT/normab.txt" 2>&1
+              done
+            done ;;
     otl) run otl 90 200 python -u tools/overlap_timeline.py > "$OUT/otl.txt" 2>&1 ;;
     otlp) run otlp 90 200 python -u tools/overlap_timeline.py --pipeline > "$OUT/otlp.txt" 2>&1 ;;
     prof) run prof 150 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \

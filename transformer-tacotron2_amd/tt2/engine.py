@@ -240,10 +240,6 @@ class TTSEngine:
         # stream ahead of the encoder and the rest on the main stream ahead of the decoder,
         # beside the encoder's forward (the same updates in the same order: identical results)
         self.pipeline_opt = False
-        # encoder forward stream (enc_overlap) at high priority (dev knob TT2_ENC_PRIO): the
-        # encoder chain is the forward's critical path; its work groups then dispatch first
-        self.enc_prio = int(os.environ.get("TT2_ENC_PRIO", "0"))
-        self._enc_side = None
         self._adam_pending = None
         # overlapped backward, dev knob: each decoder layer's cross-attention dK / dV on the side
         self.xattn_split = int(os.environ.get("TT2_XATTN_SPLIT", "0"))
@@ -534,9 +530,7 @@ class TTSEngine:
             if self._side is None:
                 self._side = torch.cuda.Stream()
                 self._side_ws = ops.Workspace()
-            if self._enc_side is None:
-                self._enc_side = torch.cuda.Stream(priority=-1) if self.enc_prio else self._side
-            side = self._enc_side
+            side = self._side
             main = torch.cuda.current_stream()
             side.wait_stream(main)
             dec = self._decoder_steps(A)
