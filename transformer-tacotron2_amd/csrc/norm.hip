@@ -170,8 +170,8 @@ __global__ __launch_bounds__(NT) void ln_combine_kernel(const T* x, const float*
 }
 
 // Backward: 8 waves per workgroup, one 512-wide row per wave at a time, software-
-// pipelined: the raw x / branch / dy chunks of the wave's next two rows are loaded before the
-// current two are reduced, so every wave always has two rows of loads in flight.  The
+// pipelined: the raw x / branch / dy chunks of the wave's next row are loaded before the
+// current row is reduced, so every wave always has a row of loads in flight.  The
 // dropout keep-mask of an element is hashed once and used for both s = x + drop(br)
 // and dbranch = drop(ds).  Per-workgroup (dgamma, dbeta, dbias) column partials go to
 // part[block][3][C]; ln_bwd_finalize sums them (fixed order: bitwise reproducible).
@@ -237,8 +237,11 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
   for (int j = 0; j < 8; ++j) pg[j] = pb[j] = pd[j] = 0.f;
   const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
   const int stride = gridDim.x * 8;
-  // one row of the wave: s = x + drop(br), the LN backward, dx / dbranch, column partials
-  auto row_bwd = [&](const LnRow<T>& cur, int row) {
+  int row = blockIdx.x * 8 + w;
+  LnRow<T> cur, nxt;
+  if (row < a.M) ln_row_load<T>(cur, a, row, c0);
+  for (; row < a.M; row += stride) {
+    if (row + stride < a.M) ln_row_load<T>(nxt, a, row + stride, c0);
     const int64_t off = (int64_t)row * a.C + c0;
     float s[8], dy[8], keep[8];
     unpack8<T>(cur.x, s);
@@ -276,21 +279,7 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
     }
     st8nt(reinterpret_cast<T*>(a.dx) + off, ds);
     if (a.dbranch) st8nt(reinterpret_cast<T*>(a.dbranch) + off, db);
-  };
-  // two rows per iteration with the next two in flight (up to four rows of loads per wave:
-  // one row of lookahead left the HBM queue half empty); rows in the same order as one at a
-  // time, so the column partials are summed in the same order
-  int row = blockIdx.x * 8 + w;
-  LnRow<T> r0, r1, n0, n1;
-  if (row < a.M) ln_row_load<T>(r0, a, row, c0);
-  if (row + stride < a.M) ln_row_load<T>(r1, a, row + stride, c0);
-  for (; row < a.M; row += 2 * stride) {
-    if (row + 2 * stride < a.M) ln_row_load<T>(n0, a, row + 2 * stride, c0);
-    if (row + 3 * stride < a.M) ln_row_load<T>(n1, a, row + 3 * stride, c0);
-    row_bwd(r0, row);
-    if (row + stride < a.M) row_bwd(r1, row + stride);
-    r0 = n0;
-    r1 = n1;
+    cur = nxt;
   }
   // 8 waves -> 4 rows of LDS partials -> 1
   if (w >= 4) {
@@ -402,23 +391,15 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   if (rl < nrl) {
-    // 4 rows' loads in flight per thread, then the rows in their order (the sums as one row
-    // at a time: one row of loads per thread left the HBM queue mostly empty)
-    for (int r = r0 + rl; r < r1; r += 4 * nrl) {
-      float v[4][8];
+    for (int r = r0 + rl; r < r1; r += nrl) {
+      float v[8];
+      ld8(y + (int64_t)r * a.C + cg * 8, v);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (r + u * nrl < r1) ld8(y + (int64_t)(r + u * nrl) * a.C + cg * 8, v[u]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (r + u * nrl < r1) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float d = v[u][j] - k[j];
-            s1[j] += d;
-            s2[j] += d * d;
-          }
-        }
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[j] - k[j];
+        s1[j] += d;
+        s2[j] += d * d;
+      }
     }
   }
 #pragma unroll
@@ -630,30 +611,19 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   col8(a.mean, c0, mu); col8(a.rstd, c0, rs); col8(a.gamma, c0, g); col8(a.beta, c0, b);
   if (rl < nrl) {
-    // 4 rows' loads in flight per thread, then the rows in their order (as bn_stats_kernel)
-    for (int r = r0 + rl; r < r1; r += 4 * nrl) {
-      float v[4][8], d[4][8];
+    for (int r = r0 + rl; r < r1; r += nrl) {
+      const int64_t i0 = (int64_t)r * a.C + c0;
+      float v[8], d[8], kp[8];
+      ld8(y + i0, v);
+      ld8(dout + i0, d);
+      bn_keep8(a, seed, i0, kp);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (r + u * nrl < r1) {
-          const int64_t i0 = (int64_t)(r + u * nrl) * a.C + c0;
-          ld8(y + i0, v[u]);
-          ld8(dout + i0, d[u]);
-        }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (r + u * nrl < r1) {
-          const int64_t i0 = (int64_t)(r + u * nrl) * a.C + c0;
-          float kp[8];
-          bn_keep8(a, seed, i0, kp);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float xh = (v[u][j] - mu[j]) * rs[j];
-            const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[u][j]);
-            s1[j] += dp;
-            s2[j] += dp * xh;
-          }
-        }
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (v[j] - mu[j]) * rs[j];
+        const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[j]);
+        s1[j] += dp;
+        s2[j] += dp * xh;
+      }
     }
   }
 #pragma unroll
