@@ -315,6 +315,10 @@ int tt2_decode_reset(const tt2_decode_desc* d, uint32_t seed0, hipStream_t strea
 /* one step as eager launches */
 int tt2_decode_step(const tt2_decode_desc* d, hipStream_t stream);
 int tt2_decode_graph_create(const tt2_decode_desc* d, hipStream_t stream, tt2_decode_graph_t* out);
+/* also captures `steps` (1..64) consecutive steps as a second graph: a launch of n steps then
+ * replays it n / steps times (one graph boundary per `steps` frames) and the one-step graph for
+ * the rest.  tt2_decode_graph_create == steps 1. */
+int tt2_decode_graph_create_n(const tt2_decode_desc* d, int32_t steps, hipStream_t stream, tt2_decode_graph_t* out);
 /* n_steps replays.  The device step counter saturates at t_max: replays past it write no
  * KV-cache row, emit no frame and leave every output unchanged. */
 int tt2_decode_graph_launch(tt2_decode_graph_t g, int32_t n_steps, hipStream_t stream);

@@ -303,3 +303,24 @@ def test_replay_past_t_max_leaves_buffers_unchanged():
         cache_bytes = c.n_dec * 3 * T * 2 * c.d_model * 2
         assert cache_bytes % 256 == 0
         assert torch.equal(dec.ws[-cache_bytes:], ws0[-cache_bytes:])
+
+
+@pytest.mark.parametrize("steps", [4, 8])
+def test_multi_step_graph_equals_one_step(steps, monkeypatch):
+    """tt2_decode_graph_create_n: `steps` frames per graph launch (the rest by the one-step
+    graph) decode the same frames, stop positions and device counters bit for bit as one
+    frame per launch, with prenet dropout and a stop threshold (23 frames: not a multiple)."""
+    _, model, text, tl = setup(torch.bfloat16)
+    T = 23
+    outs = []
+    for gs in (1, steps):
+        monkeypatch.setenv("TT2_DEC_GRAPH_STEPS", str(gs))
+        dec = Decoder(model.engine, 3, 17, T, seed=11)
+        assert dec.graph_steps == gs
+        after, out_len = dec.run(text.cuda(), tl.cuda(), T, stop_threshold=0.5)
+        torch.cuda.synchronize()
+        outs.append((after.clone(), out_len.clone(), dec.mel_seq.clone(), dec.stop_seq.clone(), dec.t.clone(),
+                     dec.seed.clone(), dec.stop_len.clone()))
+        dec.close()
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)

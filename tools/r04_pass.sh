@@ -59,6 +59,15 @@ for s in $STEPS; do
                 run "normab $lib" 60 120 env TT2_LIB=$lib python -u tools/norm_ab.py >> "$OUT/normab.txt" 2>&1
               done
             done ;;
+    decg) for i in 1 2; do
+            for gs in 1 8 16; do
+              run "decg $gs" 90 200 env TT2_DEC_GRAPH_STEPS=$gs python3 -u tools/decode_bench_only.py \
+                > "$OUT/dec_run.json" 2> "$OUT/dec_run.err"
+              echo "steps=$gs $(python -c "import json,sys;d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]);print(d['decode']['value'], d.get('decode_longform',{}).get('value'))" "$OUT/dec_run.json" 2>&1 | tail -1)" >> "$OUT/decg.txt"
+            done
+          done ;;
+    dect) run dect 60 300 python -u -m pytest tests/test_gpu_decode.py -x -q --timeout 200 --timeout-method thread \
+            > "$OUT/dec_tests.log" 2>&1 ;;
     otl) run otl 90 200 python -u tools/overlap_timeline.py > "$OUT/otl.txt" 2>&1 ;;
     otlp) run otlp 90 200 python -u tools/overlap_timeline.py --pipeline > "$OUT/otlp.txt" 2>&1 ;;
     prof) run prof 150 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \

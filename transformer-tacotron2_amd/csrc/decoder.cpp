@@ -294,9 +294,44 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
 }  // namespace
 
 struct tt2_decode_graph {
-  hipGraph_t graph = nullptr;
+  hipGraph_t graph = nullptr;     // one step
   hipGraphExec_t exec = nullptr;
+  hipGraph_t graph_n = nullptr;   // `steps` consecutive steps (steps > 1), or none
+  hipGraphExec_t exec_n = nullptr;
+  int steps = 1;
 };
+
+// capture `n` consecutive steps (every per-step value lives on the device: the step counter,
+// the seed, the previous frame) as one graph on a private stream ordered after s
+static int capture_steps(const tt2_decode_desc* d, int n, hipStream_t s, hipGraph_t* graph, hipGraphExec_t* exec) {
+  // capture on a private stream (the caller's may be the legacy default stream, which
+  // cannot capture), ordered after the caller's pending work.  Thread-local mode: another
+  // thread's HIP calls (e.g. RCCL's watchdog) must not invalidate the capture.
+  hipStream_t cs = nullptr;
+  hipEvent_t ev = nullptr;
+  *graph = nullptr;
+  *exec = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(ev, s);
+  if (e == hipSuccess) e = hipStreamWaitEvent(cs, ev, 0);
+  if (e == hipSuccess) e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+  int rc = tt2_check_launch(e, "tt2_decode_graph_create");
+  if (rc == TT2_OK) {
+    for (int i = 0; i < n && rc == TT2_OK; ++i) rc = step_launches(d, cs);
+    const hipError_t ee = hipStreamEndCapture(cs, graph);   // always end a begun capture
+    if (rc == TT2_OK) rc = tt2_check_launch(ee, "tt2_decode_graph_create: end capture");
+  }
+  if (rc == TT2_OK) rc = tt2_check_launch(hipGraphInstantiate(exec, *graph, nullptr, nullptr, 0),
+                                          "tt2_decode_graph_create: instantiate");
+  if (ev) hipEventDestroy(ev);
+  if (cs) hipStreamDestroy(cs);
+  if (rc != TT2_OK && *graph) {
+    hipGraphDestroy(*graph);
+    *graph = nullptr;
+  }
+  return rc;
+}
 
 extern "C" size_t tt2_decode_workspace_size(const tt2_decode_desc* d) {
   if (!d) return 0;
@@ -319,51 +354,40 @@ extern "C" int tt2_decode_step(const tt2_decode_desc* d, hipStream_t s) {
   return step_launches(d, s);
 }
 
-extern "C" int tt2_decode_graph_create(const tt2_decode_desc* d, hipStream_t s, tt2_decode_graph_t* out) {
+extern "C" int tt2_decode_graph_create_n(const tt2_decode_desc* d, int32_t steps, hipStream_t s,
+                                         tt2_decode_graph_t* out) {
   if (!out) return tt2_set_error(TT2_E_INVALID, "tt2_decode_graph_create: null output");
   *out = nullptr;
+  if (steps < 1 || steps > 64) return tt2_set_error(TT2_E_INVALID, "tt2_decode_graph_create_n: steps in [1, 64]");
   TT2_TRY(validate(d));
-  // capture on a private stream (the caller's may be the legacy default stream, which
-  // cannot capture), ordered after the caller's pending work.  Thread-local mode: another
-  // thread's HIP calls (e.g. RCCL's watchdog) must not invalidate the capture.
-  hipStream_t cs = nullptr;
-  hipEvent_t ev = nullptr;
-  hipError_t e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventRecord(ev, s);
-  if (e == hipSuccess) e = hipStreamWaitEvent(cs, ev, 0);
-  if (e == hipSuccess) e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
-  int rc = tt2_check_launch(e, "tt2_decode_graph_create");
-  hipGraph_t graph = nullptr;
-  if (rc == TT2_OK) {
-    rc = step_launches(d, cs);
-    const hipError_t ee = hipStreamEndCapture(cs, &graph);   // always end a begun capture
-    if (rc == TT2_OK) rc = tt2_check_launch(ee, "tt2_decode_graph_create: end capture");
+  tt2_decode_graph* g = new (std::nothrow) tt2_decode_graph;
+  if (!g) return tt2_set_error(TT2_E_HIP, "tt2_decode_graph_create: out of host memory");
+  int rc = capture_steps(d, 1, s, &g->graph, &g->exec);
+  if (rc == TT2_OK && steps > 1) {
+    rc = capture_steps(d, steps, s, &g->graph_n, &g->exec_n);
+    g->steps = steps;
   }
-  hipGraphExec_t exec = nullptr;
-  if (rc == TT2_OK) rc = tt2_check_launch(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0),
-                                          "tt2_decode_graph_create: instantiate");
-  if (ev) hipEventDestroy(ev);
-  if (cs) hipStreamDestroy(cs);
   if (rc != TT2_OK) {
-    if (graph) hipGraphDestroy(graph);
+    tt2_decode_graph_destroy(g);
     return rc;
   }
-  tt2_decode_graph* g = new (std::nothrow) tt2_decode_graph;
-  if (!g) {
-    hipGraphExecDestroy(exec);
-    hipGraphDestroy(graph);
-    return tt2_set_error(TT2_E_HIP, "tt2_decode_graph_create: out of host memory");
-  }
-  g->graph = graph;
-  g->exec = exec;
   *out = g;
   return TT2_OK;
 }
 
+extern "C" int tt2_decode_graph_create(const tt2_decode_desc* d, hipStream_t s, tt2_decode_graph_t* out) {
+  return tt2_decode_graph_create_n(d, 1, s, out);
+}
+
 extern "C" int tt2_decode_graph_launch(tt2_decode_graph_t g, int32_t n_steps, hipStream_t s) {
   if (!g || !g->exec) return tt2_set_error(TT2_E_INVALID, "tt2_decode_graph_launch: null graph");
-  for (int i = 0; i < n_steps; ++i) {
+  int i = 0;
+  if (g->exec_n)
+    for (; i + g->steps <= n_steps; i += g->steps) {
+      const hipError_t e = hipGraphLaunch(g->exec_n, s);
+      if (e != hipSuccess) return tt2_check_launch(e, "tt2_decode_graph_launch");
+    }
+  for (; i < n_steps; ++i) {
     const hipError_t e = hipGraphLaunch(g->exec, s);
     if (e != hipSuccess) return tt2_check_launch(e, "tt2_decode_graph_launch");
   }
@@ -373,7 +397,9 @@ extern "C" int tt2_decode_graph_launch(tt2_decode_graph_t g, int32_t n_steps, hi
 extern "C" int tt2_decode_graph_destroy(tt2_decode_graph_t g) {
   if (!g) return TT2_OK;
   hipError_t e = hipSuccess;
-  if (g->exec) e = hipGraphExecDestroy(g->exec);
+  if (g->exec_n) e = hipGraphExecDestroy(g->exec_n);
+  if (g->graph_n && e == hipSuccess) e = hipGraphDestroy(g->graph_n);
+  if (g->exec && e == hipSuccess) e = hipGraphExecDestroy(g->exec);
   if (g->graph && e == hipSuccess) e = hipGraphDestroy(g->graph);
   delete g;
   return tt2_check_launch(e, "tt2_decode_graph_destroy");

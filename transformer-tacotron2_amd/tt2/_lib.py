@@ -300,6 +300,7 @@ SIGNATURES.update({
     "tt2_decode_reset": ([C.POINTER(DecodeDesc), u32, vp], C.c_int),
     "tt2_decode_step": ([C.POINTER(DecodeDesc), vp], C.c_int),
     "tt2_decode_graph_create": ([C.POINTER(DecodeDesc), vp, C.POINTER(vp)], C.c_int),
+    "tt2_decode_graph_create_n": ([C.POINTER(DecodeDesc), i32, vp, C.POINTER(vp)], C.c_int),
     "tt2_decode_graph_launch": ([vp, i32, vp], C.c_int),
     "tt2_decode_graph_destroy": ([vp], C.c_int),
 })

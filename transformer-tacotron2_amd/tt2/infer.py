@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 
 import torch
 
@@ -70,6 +71,9 @@ class Decoder:
         if cd == torch.float16 and (e.cd != torch.bfloat16 or batch > 64):
             raise ValueError("f16 decode needs a bf16 engine and batch <= 64 (the skinny decode kernels)")
         self.schedule = schedule
+        # steps per decode graph launch (tt2_decode_graph_create_n; dev knob TT2_DEC_GRAPH_STEPS):
+        # one graph boundary per that many frames
+        self.graph_steps = int(os.environ.get("TT2_DEC_GRAPH_STEPS", "1"))
         self.A = e.arena(batch, text_len, t_max)   # encoder + post-net buffers (lazy)
         B = batch
         self.mel_seq = torch.zeros(B, t_max, c.n_mels, dtype=torch.float32, device=dev)
@@ -175,8 +179,8 @@ class Decoder:
         logit = stop_logit(stop_threshold)
         if logit not in self._graphs:
             h = C.c_void_p()
-            check(lib().tt2_decode_graph_create(C.byref(self.desc(logit)), stream_ptr(), C.byref(h)),
-                  "tt2_decode_graph_create")
+            check(lib().tt2_decode_graph_create_n(C.byref(self.desc(logit)), self.graph_steps, stream_ptr(),
+                                                  C.byref(h)), "tt2_decode_graph_create_n")
             self._graphs[logit] = h.value
         return self._graphs[logit]
 
