@@ -68,6 +68,8 @@ for s in $STEPS; do
           done ;;
     dect) run dect 60 300 python -u -m pytest tests/test_gpu_decode.py -x -q --timeout 200 --timeout-method thread \
             > "$OUT/dec_tests.log" 2>&1 ;;
+    distt) run distt 60 300 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_syncbn.py -v --timeout 200 \
+             --timeout-method thread > "$OUT/dist_tests.log" 2>&1 ;;
     otl) run otl 90 200 python -u tools/overlap_timeline.py > "$OUT/otl.txt" 2>&1 ;;
     otlp) run otlp 90 200 python -u tools/overlap_timeline.py --pipeline > "$OUT/otlp.txt" 2>&1 ;;
     prof) run prof 150 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
