@@ -51,6 +51,19 @@ for s in $STEPS; do
     attn) for v in ${ATTN_VARIANTS:-3 4 5 3 4 5}; do
             run "attn $v" 60 120 env TT2_ATTN_VARIANT=$v python -u tools/attn_bench.py >> "$OUT/attn_v$v.txt" 2>&1
           done ;;
+    attnab) for i in 1 2; do
+              for lib in abl/attn0.so transformer-tacotron2_amd/tt2/libtt2.so; do
+                echo "== $lib" >> "$OUT/attnab.txt"
+                run "attnab $lib" 60 120 env TT2_LIB=$lib python -u tools/attn_bench.py >> "$OUT/attnab.txt" 2>&1
+              done
+            done ;;
+    stepab) for i in 1 2; do
+              for lib in abl/attn0.so transformer-tacotron2_amd/tt2/libtt2.so; do
+                run "stepab $lib" 90 200 env TT2_LIB=$lib python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline \
+                  --no-decode > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
+                echo "$lib $(lastms "$OUT/ab_run.json")" >> "$OUT/stepab.txt"
+              done
+            done ;;
     attnt) run attnt 60 300 python -u -m pytest tests/test_gpu_attention.py -x -q --timeout 120 --timeout-method thread \
              > "$OUT/attn_tests.log" 2>&1 ;;
     encg) run encg 60 200 python -u tools/enc_gemm_ab.py > "$OUT/enc_gemm.txt" 2>&1 ;;

@@ -576,6 +576,13 @@ TT2_DEV void zero16(f32x16& x) {
   for (int i = 0; i < 16; ++i) x[i] = 0.f;
 }
 
+// s_waitcnt vmcnt(0) as the builtin (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15), which the
+// compiler's wait-count pass sees: registers loaded before a tile loop are then known complete.
+// Without it the pass carried those loads' pending state around the loop and made each MFMA that
+// reads them wait for the NEXT tile's prefetch loads issued just before (vmcnt(3)..vmcnt(0)),
+// which put the prefetch's whole memory latency in front of every tile's first MFMAs.
+#define TT2_VMCNT0() __builtin_amdgcn_s_waitcnt(0x0F70)
+
 // in-kernel timeline hooks of the v3 forward (tools/attn_stamps.hip defines them; empty here)
 #ifndef ATTN_STAMP
 #define ATTN_STAMP(slot)
@@ -599,6 +606,7 @@ __global__ __launch_bounds__(NW * 64) void attn_fwd3_kernel(AttnArgs a) {
 
   bf16x8 fq[4];
   own_frags(fq, Q, qv, hi);
+  TT2_VMCNT0();   // the Q fragments are final before the tile loop (see TT2_VMCNT0)
   const float c = a.scale * LOG2E;
   float m_r = -INFINITY, l_r = 0.f;
   f32x16 o[2];
@@ -731,6 +739,7 @@ TT2_DEV void attn_bwd_dq3_body(const AttnArgs& a, int bx, int by, int ny, char* 
   const RowBuf Ob = row_buf(reinterpret_cast<const bf16*>(a.o) + (int64_t)b * a.Tq * a.o_ld + h * D, a.o_ld, a.Tq);
   own_frags(fo, Ob, qv, hi);
   const float lse = qok ? a.lse[(int64_t)bh * a.Tq + qv] : INFINITY;
+  TT2_VMCNT0();   // Q / dO / O fragments and the LSE are final before the tile loop
   float dsum = 0.f;
 #pragma unroll
   for (int st = 0; st < 4; ++st)
@@ -838,6 +847,7 @@ TT2_DEV void attn_bwd_dkdv3_body(const AttnArgs& a, int bx, int by, char* smem, 
   bf16x8 fk[4], fv[4];
   own_frags(fk, K, kv, hi);
   own_frags(fv, V, kv, hi);
+  TT2_VMCNT0();   // the K / V fragments are final before the tile loop (see TT2_VMCNT0)
   const float c = a.scale * LOG2E;
   f32x16 dk[2], dv[2];
 #pragma unroll
