@@ -58,7 +58,7 @@ for s in $STEPS; do
               done
             done ;;
     stepab) for i in 1 2; do
-              for lib in abl/attn0.so transformer-tacotron2_amd/tt2/libtt2.so; do
+              for lib in abl/${STEPAB_OLD:-attn0}.so transformer-tacotron2_amd/tt2/libtt2.so; do
                 run "stepab $lib" 90 200 env TT2_LIB=$lib python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline \
                   --no-decode > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
                 echo "$lib $(lastms "$OUT/ab_run.json")" >> "$OUT/stepab.txt"
@@ -81,6 +81,8 @@ for s in $STEPS; do
           done ;;
     dect) run dect 60 300 python -u -m pytest tests/test_gpu_decode.py -x -q --timeout 200 --timeout-method thread \
             > "$OUT/dec_tests.log" 2>&1 ;;
+    normt) run normt 60 300 python -u -m pytest tests/test_gpu_norm.py tests/test_gpu_syncbn.py tests/test_gpu_fullsize.py \
+             -x -q --timeout 200 --timeout-method thread > "$OUT/norm_tests.log" 2>&1 ;;
     distt) run distt 60 300 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_syncbn.py -v --timeout 200 \
              --timeout-method thread > "$OUT/dist_tests.log" 2>&1 ;;
     otl) run otl 90 200 python -u tools/overlap_timeline.py > "$OUT/otl.txt" 2>&1 ;;

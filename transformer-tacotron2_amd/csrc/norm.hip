@@ -241,7 +241,10 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
   LnRow<T> cur, nxt;
   if (row < a.M) ln_row_load<T>(cur, a, row, c0);
   for (; row < a.M; row += stride) {
-    if (row + stride < a.M) ln_row_load<T>(nxt, a, row + stride, c0);
+    // the next row's loads unconditionally (clamped to the last row: a spare load past the
+    // end): a conditional prefetch let the compiler's wait-count pass assume a path with no
+    // newer loads in flight, so it waited for the prefetch itself (vmcnt(0)) before this row
+    ln_row_load<T>(nxt, a, min(row + stride, a.M - 1), c0);
     const int64_t off = (int64_t)row * a.C + c0;
     float s[8], dy[8], keep[8];
     unpack8<T>(cur.x, s);
@@ -391,14 +394,31 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   if (rl < nrl) {
-    for (int r = r0 + rl; r < r1; r += nrl) {
-      float v[8];
-      ld8(y + (int64_t)r * a.C + cg * 8, v);
+    // 4 rows' raw loads in flight per thread, unconditional (rows clamped; a row past the
+    // chunk is loaded and not summed), converted only where they are summed: with a
+    // conditional or converted-on-load prefetch the compiler's wait-count pass waited for each
+    // load before the next was issued.  Rows are summed in order (the sums as one at a time).
+    for (int r = r0 + rl; r < r1; r += 4 * nrl) {
+      uint4 raw[4][sizeof(T) / 2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = v[j] - k[j];
-        s1[j] += d;
-        s2[j] += d * d;
+      for (int u = 0; u < 4; ++u) {
+        const uint4* q = reinterpret_cast<const uint4*>(y + (int64_t)min(r + u * nrl, r1 - 1) * a.C + cg * 8);
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(T) / 2); ++i) raw[u][i] = q[i];
+      }
+      // rows past the chunk count with weight 0 (a branch here let the compiler sink their
+      // loads into it, one round trip each): d * 1 = d exactly, fma(0, d, s) = s
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float w = r + u * nrl < r1 ? 1.f : 0.f;
+        float v[8];
+        unpack8<T>(raw[u], v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[j] - k[j], dw = d * w;
+          s1[j] += dw;
+          s2[j] = fmaf(dw, d, s2[j]);
+        }
       }
     }
   }
@@ -611,19 +631,35 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   col8(a.mean, c0, mu); col8(a.rstd, c0, rs); col8(a.gamma, c0, g); col8(a.beta, c0, b);
   if (rl < nrl) {
-    for (int r = r0 + rl; r < r1; r += nrl) {
-      const int64_t i0 = (int64_t)r * a.C + c0;
-      float v[8], d[8], kp[8];
-      ld8(y + i0, v);
-      ld8(dout + i0, d);
-      bn_keep8(a, seed, i0, kp);
+    // 4 rows' raw loads in flight per thread (as bn_stats_kernel), rows summed in order
+    for (int r = r0 + rl; r < r1; r += 4 * nrl) {
+      uint4 ry[4][sizeof(T) / 2], rd[4][sizeof(TD) / 2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xh = (v[j] - mu[j]) * rs[j];
-        const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[j]);
-        s1[j] += dp;
-        s2[j] += dp * xh;
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i0 = (int64_t)min(r + u * nrl, r1 - 1) * a.C + c0;
+        const uint4* qy = reinterpret_cast<const uint4*>(y + i0);
+        const uint4* qd = reinterpret_cast<const uint4*>(dout + i0);
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(T) / 2); ++i) ry[u][i] = qy[i];
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(TD) / 2); ++i) rd[u][i] = qd[i];
       }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (r + u * nrl < r1) {
+          const int64_t i0 = (int64_t)(r + u * nrl) * a.C + c0;
+          float v[8], d[8], kp[8];
+          unpack8<T>(ry[u], v);
+          unpack8<TD>(rd[u], d);
+          bn_keep8(a, seed, i0, kp);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xh = (v[j] - mu[j]) * rs[j];
+            const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[j]);
+            s1[j] += dp;
+            s2[j] += dp * xh;
+          }
+        }
     }
   }
 #pragma unroll
