@@ -92,7 +92,7 @@ for s in $STEPS; do
     phases) run phases 120 300 env TT2_LIB=abl/phase.so python -u tools/g7_phases.py --json "$OUT/phases.json" \
               > "$OUT/phases.txt" 2>&1 ;;
     decab) for i in 1 2; do
-             for lib in abl/dec0.so transformer-tacotron2_amd/tt2/libtt2.so; do
+             for lib in abl/${DECAB_OLD:-dec0}.so transformer-tacotron2_amd/tt2/libtt2.so; do
                run "decab $lib" 90 200 env TT2_LIB=$lib python3 -u tools/decode_bench_only.py --no-longform \
                  > "$OUT/dec_run.json" 2> "$OUT/dec_run.err"
                echo "$lib $(python -c "import json,sys;print(json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])['decode']['value'])" "$OUT/dec_run.json" 2>&1 | tail -1)" >> "$OUT/decab.txt"
