@@ -237,15 +237,11 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
   for (int j = 0; j < 8; ++j) pg[j] = pb[j] = pd[j] = 0.f;
   const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
   const int stride = gridDim.x * 8;
-  int row = blockIdx.x * 8 + w;
-  LnRow<T> cur, nxt;
-  if (row < a.M) ln_row_load<T>(cur, a, row, c0);
-  for (; row < a.M; row += stride) {
-    // the next row's loads unconditionally (clamped to the last row: a spare load past the
-    // end): a conditional prefetch let the compiler's wait-count pass assume a path with no
-    // newer loads in flight, so it waited for the prefetch itself (vmcnt(0)) before this row
-    ln_row_load<T>(nxt, a, min(row + stride, a.M - 1), c0);
-    const int64_t off = (int64_t)row * a.C + c0;
+  // one row of the wave (row_c: the clamped row whose data `cur` holds; wt 0 for a row past
+  // the end, which is then a copy of the last row: its stores rewrite that row's values and
+  // its column partials are weighted out -- x * 1 = x exactly, fma(0, y, s) = s)
+  auto row_bwd = [&](const LnRow<T>& cur, int row_c, float wt) {
+    const int64_t off = (int64_t)row_c * a.C + c0;
     float s[8], dy[8], keep[8];
     unpack8<T>(cur.x, s);
     unpack8<T>(cur.dy, dy);
@@ -268,8 +264,9 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
       gd[j] = g[j] * dy[j];
       c1 += gd[j];
       c2 += gd[j] * xh[j];
-      pg[j] += dy[j] * xh[j];
-      pb[j] += dy[j];
+      const float dyw = dy[j] * wt;
+      pg[j] = fmaf(dyw, xh[j], pg[j]);
+      pb[j] += dyw;
     }
     c1 = wave_sum(c1) / a.C;
     c2 = wave_sum(c2) / a.C;
@@ -278,11 +275,33 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
     for (int j = 0; j < 8; ++j) {
       ds[j] = cur.rstd * (gd[j] - c1 - xh[j] * c2);
       db[j] = ds[j] * keep[j];
-      pd[j] += db[j];
+      pd[j] += db[j] * wt;
     }
     st8nt(reinterpret_cast<T*>(a.dx) + off, ds);
     if (a.dbranch) st8nt(reinterpret_cast<T*>(a.dbranch) + off, db);
-    cur = nxt;
+  };
+  // two rows per iteration with the next two rows' loads in flight, every load and store
+  // unconditional (rows clamped): a branch around a prefetch let the compiler's wait-count
+  // pass assume a path without it and wait for it before the current rows
+  const int last = a.M - 1;
+  int row = blockIdx.x * 8 + w;
+  if (row < a.M) {
+    LnRow<T> r0, r1, n0, n1;
+    ln_row_load<T>(r0, a, row, c0);
+    ln_row_load<T>(r1, a, min(row + stride, last), c0);
+    auto wt = [&](int r) { return r < a.M ? 1.f : 0.f; };
+    // unrolled by two with the buffers' roles swapped (no register copies, whose waits would
+    // drain the prefetch at the end of every iteration)
+    for (; row < a.M; row += 4 * stride) {
+      ln_row_load<T>(n0, a, min(row + 2 * stride, last), c0);
+      ln_row_load<T>(n1, a, min(row + 3 * stride, last), c0);
+      row_bwd(r0, row, 1.f);
+      row_bwd(r1, min(row + stride, last), wt(row + stride));
+      ln_row_load<T>(r0, a, min(row + 4 * stride, last), c0);
+      ln_row_load<T>(r1, a, min(row + 5 * stride, last), c0);
+      row_bwd(n0, min(row + 2 * stride, last), wt(row + 2 * stride));
+      row_bwd(n1, min(row + 3 * stride, last), wt(row + 3 * stride));
+    }
   }
   // 8 waves -> 4 rows of LDS partials -> 1
   if (w >= 4) {
