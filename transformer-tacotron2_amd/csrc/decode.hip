@@ -229,11 +229,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
   // one iteration on register buffer BUF (compile-time, so the buffers stay in registers)
   auto iter = [&](auto BUFC, int kb) {
     constexpr int BUF = decltype(BUFC)::value;
-    // unconditional (clamped keys; the last iteration loads spares): behind a branch the
-    // compiler's wait-count pass assumed a path without these loads and so waited for them
-    // before this iteration's arithmetic, which made every iteration a full round trip
-    load_keys(kb + 8 * U, BUF ^ 1);
-    __builtin_amdgcn_sched_barrier(0);   // issued before this iteration's arithmetic, not sunk below it
+    if (kb + 8 * U < k1) load_keys(kb + 8 * U, BUF ^ 1);
     float kv[U][8], vv[U][8];
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -272,12 +268,9 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
     }
     m = mn;
   };
-  // both halves unconditionally: an iteration past k1 has only masked keys (alpha 1, p 0:
-  // no change to m, l, o), and a branch around the second let the compiler sink the first's
-  // prefetch of its buffer into it, after the first half's arithmetic
   for (int kb = k0; kb < k1; kb += 16 * U) {
     iter(std::integral_constant<int, 0>{}, kb);
-    iter(std::integral_constant<int, 1>{}, kb + 8 * U);
+    if (kb + 8 * U < k1) iter(std::integral_constant<int, 1>{}, kb + 8 * U);
   }
   // combine the 8 key slots (same m across the wave)
 #pragma unroll

@@ -237,11 +237,12 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
   for (int j = 0; j < 8; ++j) pg[j] = pb[j] = pd[j] = 0.f;
   const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
   const int stride = gridDim.x * 8;
-  // one row of the wave (row_c: the clamped row whose data `cur` holds; wt 0 for a row past
-  // the end, which is then a copy of the last row: its stores rewrite that row's values and
-  // its column partials are weighted out -- x * 1 = x exactly, fma(0, y, s) = s)
-  auto row_bwd = [&](const LnRow<T>& cur, int row_c, float wt) {
-    const int64_t off = (int64_t)row_c * a.C + c0;
+  int row = blockIdx.x * 8 + w;
+  LnRow<T> cur, nxt;
+  if (row < a.M) ln_row_load<T>(cur, a, row, c0);
+  for (; row < a.M; row += stride) {
+    if (row + stride < a.M) ln_row_load<T>(nxt, a, row + stride, c0);
+    const int64_t off = (int64_t)row * a.C + c0;
     float s[8], dy[8], keep[8];
     unpack8<T>(cur.x, s);
     unpack8<T>(cur.dy, dy);
@@ -264,9 +265,8 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
       gd[j] = g[j] * dy[j];
       c1 += gd[j];
       c2 += gd[j] * xh[j];
-      const float dyw = dy[j] * wt;
-      pg[j] = fmaf(dyw, xh[j], pg[j]);
-      pb[j] += dyw;
+      pg[j] += dy[j] * xh[j];
+      pb[j] += dy[j];
     }
     c1 = wave_sum(c1) / a.C;
     c2 = wave_sum(c2) / a.C;
@@ -275,33 +275,11 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
     for (int j = 0; j < 8; ++j) {
       ds[j] = cur.rstd * (gd[j] - c1 - xh[j] * c2);
       db[j] = ds[j] * keep[j];
-      pd[j] += db[j] * wt;
+      pd[j] += db[j];
     }
     st8nt(reinterpret_cast<T*>(a.dx) + off, ds);
     if (a.dbranch) st8nt(reinterpret_cast<T*>(a.dbranch) + off, db);
-  };
-  // two rows per iteration with the next two rows' loads in flight, every load and store
-  // unconditional (rows clamped): a branch around a prefetch let the compiler's wait-count
-  // pass assume a path without it and wait for it before the current rows
-  const int last = a.M - 1;
-  int row = blockIdx.x * 8 + w;
-  if (row < a.M) {
-    LnRow<T> r0, r1, n0, n1;
-    ln_row_load<T>(r0, a, row, c0);
-    ln_row_load<T>(r1, a, min(row + stride, last), c0);
-    auto wt = [&](int r) { return r < a.M ? 1.f : 0.f; };
-    // unrolled by two with the buffers' roles swapped (no register copies, whose waits would
-    // drain the prefetch at the end of every iteration)
-    for (; row < a.M; row += 4 * stride) {
-      ln_row_load<T>(n0, a, min(row + 2 * stride, last), c0);
-      ln_row_load<T>(n1, a, min(row + 3 * stride, last), c0);
-      row_bwd(r0, row, 1.f);
-      row_bwd(r1, min(row + stride, last), wt(row + stride));
-      ln_row_load<T>(r0, a, min(row + 4 * stride, last), c0);
-      ln_row_load<T>(r1, a, min(row + 5 * stride, last), c0);
-      row_bwd(n0, min(row + 2 * stride, last), wt(row + 2 * stride));
-      row_bwd(n1, min(row + 3 * stride, last), wt(row + 3 * stride));
-    }
+    cur = nxt;
   }
   // 8 waves -> 4 rows of LDS partials -> 1
   if (w >= 4) {
@@ -413,31 +391,14 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   if (rl < nrl) {
-    // 4 rows' raw loads in flight per thread, unconditional (rows clamped; a row past the
-    // chunk is loaded and not summed), converted only where they are summed: with a
-    // conditional or converted-on-load prefetch the compiler's wait-count pass waited for each
-    // load before the next was issued.  Rows are summed in order (the sums as one at a time).
-    for (int r = r0 + rl; r < r1; r += 4 * nrl) {
-      uint4 raw[4][sizeof(T) / 2];
+    for (int r = r0 + rl; r < r1; r += nrl) {
+      float v[8];
+      ld8(y + (int64_t)r * a.C + cg * 8, v);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint4* q = reinterpret_cast<const uint4*>(y + (int64_t)min(r + u * nrl, r1 - 1) * a.C + cg * 8);
-#pragma unroll
-        for (int i = 0; i < (int)(sizeof(T) / 2); ++i) raw[u][i] = q[i];
-      }
-      // rows past the chunk count with weight 0 (a branch here let the compiler sink their
-      // loads into it, one round trip each): d * 1 = d exactly, fma(0, d, s) = s
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float w = r + u * nrl < r1 ? 1.f : 0.f;
-        float v[8];
-        unpack8<T>(raw[u], v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = v[j] - k[j], dw = d * w;
-          s1[j] += dw;
-          s2[j] = fmaf(dw, d, s2[j]);
-        }
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[j] - k[j];
+        s1[j] += d;
+        s2[j] += d * d;
       }
     }
   }
@@ -650,35 +611,19 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   col8(a.mean, c0, mu); col8(a.rstd, c0, rs); col8(a.gamma, c0, g); col8(a.beta, c0, b);
   if (rl < nrl) {
-    // 4 rows' raw loads in flight per thread (as bn_stats_kernel), rows summed in order
-    for (int r = r0 + rl; r < r1; r += 4 * nrl) {
-      uint4 ry[4][sizeof(T) / 2], rd[4][sizeof(TD) / 2];
+    for (int r = r0 + rl; r < r1; r += nrl) {
+      const int64_t i0 = (int64_t)r * a.C + c0;
+      float v[8], d[8], kp[8];
+      ld8(y + i0, v);
+      ld8(dout + i0, d);
+      bn_keep8(a, seed, i0, kp);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t i0 = (int64_t)min(r + u * nrl, r1 - 1) * a.C + c0;
-        const uint4* qy = reinterpret_cast<const uint4*>(y + i0);
-        const uint4* qd = reinterpret_cast<const uint4*>(dout + i0);
-#pragma unroll
-        for (int i = 0; i < (int)(sizeof(T) / 2); ++i) ry[u][i] = qy[i];
-#pragma unroll
-        for (int i = 0; i < (int)(sizeof(TD) / 2); ++i) rd[u][i] = qd[i];
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (v[j] - mu[j]) * rs[j];
+        const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[j]);
+        s1[j] += dp;
+        s2[j] += dp * xh;
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (r + u * nrl < r1) {
-          const int64_t i0 = (int64_t)(r + u * nrl) * a.C + c0;
-          float v[8], d[8], kp[8];
-          unpack8<T>(ry[u], v);
-          unpack8<TD>(rd[u], d);
-          bn_keep8(a, seed, i0, kp);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float xh = (v[j] - mu[j]) * rs[j];
-            const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[j]);
-            s1[j] += dp;
-            s2[j] += dp * xh;
-          }
-        }
     }
   }
 #pragma unroll
