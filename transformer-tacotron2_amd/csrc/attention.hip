@@ -859,11 +859,21 @@ TT2_DEV void attn_bwd_dkdv3_body(const AttnArgs& a, int bx, int by, char* smem, 
   const int qstart = a.causal ? (k0 / 64) * 64 : 0;
   const int ntile = k0 < klim && a.Tq > qstart ? (a.Tq - qstart + 63) / 64 : 0;
   uint4 rq[PER], rd[PER], ro[PER];
-  auto stats = [&](int buf, int qb) {
+  // the next tile's LSE / delta are loaded with its Q / dO rows (stats_load) and stored to LDS
+  // with them (stats): loaded at the store, they cost a memory round trip at every tile's end
+  float lse_n = INFINITY, dl_n = 0.f;
+  auto stats_load = [&](int qb) {
     if (tid < 64) {
       const int q = qb + tid;
-      sL[buf][tid] = q < a.Tq ? LSE[q] : INFINITY;
-      if (!self_delta) sDl[buf][tid] = q < a.Tq ? DL[q] : 0.f;
+      lse_n = q < a.Tq ? LSE[q] : INFINITY;
+      if (!self_delta) dl_n = q < a.Tq ? DL[q] : 0.f;
+    }
+  };
+  auto stats = [&](int buf, int qb) {
+    (void)qb;
+    if (tid < 64) {
+      sL[buf][tid] = lse_n;
+      if (!self_delta) sDl[buf][tid] = dl_n;
     }
     if (self_delta) {   // chunk c = tid + NTH i is row c >> 3, 8 columns; the row's 8 chunks sit in 8 lanes
 #pragma unroll
@@ -885,6 +895,7 @@ TT2_DEV void attn_bwd_dkdv3_body(const AttnArgs& a, int bx, int by, char* smem, 
     g2r3<NTH>(rq, Q, qstart, tid);
     g2r3<NTH>(rd, dO, qstart, tid);
     if (self_delta) g2r3<NTH>(ro, Ob, qstart, tid);
+    stats_load(qstart);
     r2s3<NTH>(rq, sQ[0], tid);
     r2s3<NTH>(rd, sdO[0], tid);
     stats(0, qstart);
@@ -898,6 +909,7 @@ TT2_DEV void attn_bwd_dkdv3_body(const AttnArgs& a, int bx, int by, char* smem, 
       g2r3<NTH>(rq, Q, q0 + 64, tid);
       g2r3<NTH>(rd, dO, q0 + 64, tid);
       if (self_delta) g2r3<NTH>(ro, Ob, q0 + 64, tid);
+      stats_load(q0 + 64);
     }
     const bf16* cQ = sQ[BUF];
     const bf16* cD = sdO[BUF];
