@@ -52,7 +52,7 @@ for s in $STEPS; do
             run "attn $v" 60 120 env TT2_ATTN_VARIANT=$v python -u tools/attn_bench.py >> "$OUT/attn_v$v.txt" 2>&1
           done ;;
     attnab) for i in 1 2; do
-              for lib in abl/attn0.so transformer-tacotron2_amd/tt2/libtt2.so; do
+              for lib in abl/${ATTNAB_OLD:-attn0}.so transformer-tacotron2_amd/tt2/libtt2.so; do
                 echo "== $lib" >> "$OUT/attnab.txt"
                 run "attnab $lib" 60 120 env TT2_LIB=$lib python -u tools/attn_bench.py >> "$OUT/attnab.txt" 2>&1
               done
