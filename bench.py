@@ -610,7 +610,10 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-            "config": {"workload": "train step (fwd+loss+bwd+grad all-reduce+Adam), LJSpeech-shape synthetic batch",
+            "config": {"workload": ("train step (fwd+loss+bwd+grad all-reduce+Adam), LJSpeech-shape synthetic batch"
+                                    if sync is not None else
+                                    "train step (fwd+loss+bwd+Adam; one rank: no gradient exchange), "
+                                    "LJSpeech-shape synthetic batch"),
                        "global_batch": world * B_PER_GPU, "per_gpu_batch": B_PER_GPU, "seq_len": TY,
                        "text_len": TX, "n_mels": NMEL, "params": model.n_params(), "parallelism": f"dp{world}",
                        "graph": not args.no_graph,

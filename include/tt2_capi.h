@@ -516,6 +516,11 @@ typedef struct tt2_adam_args {
    * in place of the step's own pass over the gradients */
   const float* norm_parts;
   int32_t norm_nparts;
+  /* gate != NULL: the update runs only while *gate != 0 (the pipelined optimizer's deferred
+   * Adam: armed by tt2_adam_gate(op 1) when a step's gradients are final, consumed by
+   * tt2_adam_gate(op 0) once the deferred update has run), so a captured step replays a
+   * deferred update exactly once however often it was flushed eagerly in between */
+  const int32_t* gate;
 } tt2_adam_args;
 size_t tt2_adam_workspace_size(void);
 int tt2_adam_step(const tt2_adam_args* a, hipStream_t stream);
@@ -524,6 +529,16 @@ int tt2_sumsq_parts(const float* g, int64_t n, float* parts, int32_t nparts, hip
 /* step += 1; seed += 1 (either may be NULL: the pipelined optimizer bumps the dropout seed at the
  * end of a step and the step counter once the deferred Adam has run) */
 int tt2_step_bump(int32_t* step, uint32_t* seed, hipStream_t stream);
+/* op 1 (arm): *gate = 1.  op 0 (consume): if *gate != 0 { *step += 1 (when step != NULL); *gate = 0 } */
+int tt2_adam_gate(int32_t* gate, int32_t* step, int32_t op, hipStream_t stream);
+
+/* ---------------------------------------------------------- capture hygiene
+ * For each of n streams, status[i] = 0: not part of the origin's capture, 1: part of it and
+ * joined (the origin depends on all its captured work), 2: part of it with captured work the
+ * origin does not depend on (ending the capture now would leave it unjoined), 3: its capture
+ * was invalidated.  The origin stream must be capturing.  Host-only (reads the graph being
+ * captured; enqueues nothing). */
+int tt2_capture_joined(hipStream_t origin, const hipStream_t* streams, int32_t n, int32_t* status);
 
 /* ---------------------------------------------------------- block-level entry points
  * One call per block of the path: each is a fixed sequence of the kernels

@@ -130,3 +130,40 @@ def _bnsync_case(rank, world):
 def test_syncbn_exchange_gloo():
     out = run_world(_bnsync_case)
     assert all(v < 1e-6 for v in out.values()), out
+
+
+def _issue_order_case(rank, world):
+    """Each rank derives its bucket issue sequence from the same ready() offsets (rank 1 also
+    from a reordered copy), the sequences travel by all_gather_object, and compare_issue_logs
+    must accept the identical ones and flag the reordered one at its first difference."""
+    from tt2.dist import GradSync, compare_issue_logs
+    sync = GradSync(torch.zeros(10007), bucket_bytes=4 * 1000)
+    offs = [9000, 8500, 5000, 4999, 100]
+    good = []
+    for off in offs:
+        good += [("bucket",) + sync.buckets[i] + ("side",) for i in sync.take_ready(off)]
+    good += [("bucket",) + b + ("side",) for b in sync.buckets[sync.next:]]
+    bad = list(good)
+    if rank == 1:
+        bad[2], bad[3] = bad[3], bad[2]   # one bucket hook fired late on rank 1
+    logs_good, logs_bad = [None] * world, [None] * world
+    dist.all_gather_object(logs_good, good)
+    dist.all_gather_object(logs_bad, bad)
+    return compare_issue_logs(logs_good), compare_issue_logs(logs_bad), good[2], good[3]
+
+
+def test_compare_issue_logs_two_ranks():
+    out = run_world(_issue_order_case)
+    for r in range(2):
+        ok, bad, b2, b3 = out[r]
+        assert ok == []
+        assert bad == [(1, 2, b2, b3)]
+
+
+def test_compare_issue_logs_lengths():
+    from tt2.dist import compare_issue_logs
+    a = [("bucket", 0, 10, "side"), ("bn", 4104, "main")]
+    assert compare_issue_logs([a, list(a), list(a)]) == []
+    assert compare_issue_logs([a, a[:1]]) == [(1, 1, ("bn", 4104, "main"), None)]
+    assert compare_issue_logs([a, a + [("bn", 1, "main")]]) == [(1, 2, None, ("bn", 1, "main"))]
+    assert compare_issue_logs([a, [("bucket", 0, 10, "main"), a[1]]]) == [(1, 0, a[0], ("bucket", 0, 10, "main"))]

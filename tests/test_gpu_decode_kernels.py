@@ -168,13 +168,14 @@ def test_attn_decode_cross_ragged():
     assert out[2].float().abs().sum().item() == 0   # no keys -> zeros, never NaN
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_attn_decode_fused_oproj(dtype):
+@pytest.mark.parametrize("dtype,H", [(torch.bfloat16, 8), (torch.float16, 8), (torch.bfloat16, 4)])
+def test_attn_decode_fused_oproj(dtype, H):
     """The output projection fused into the decode attention launch: one f32 slab per
     head, slab[h, b] = o[b, h] W_o[:, h]^T; the sum over heads is o W_o^T (float64 ref).
-    A finished utterance (stop_len) writes zero slabs."""
+    A finished utterance (stop_len) writes zero slabs.  H = 4 (W_o is [256, 256]): the waves
+    past the 4 row blocks prefetch nothing (no read past the end of W_o)."""
     g = torch.Generator().manual_seed(11)
-    B, H, d, Tm, t = 6, 8, 512, 300, 140
+    B, d, Tm, t = 6, 64 * H, 300, 140
     mk = (lambda sh: _bf(sh, g)) if dtype == torch.bfloat16 else (lambda sh: _h(sh, g))
     qkv, cache = mk((B, 3 * d)), mk((B, Tm, 2 * d))
     wo = (torch.randn(d, d, generator=g) / math.sqrt(d)).to(dtype).cuda()

@@ -33,6 +33,8 @@ def test_metrics_jsonl(tmp_path):
     assert [r["step"] for r in lines] == [0, 1, 2, 3]
     for r, lv in zip(lines, losses):
         assert r["ms"] > 0 and r["frames_per_s"] > 0 and r["tflops"] > 0
-        assert r["allreduce_ms"] is None and r["batch"] == B and r["frames"] == Ty
+        assert r["allreduce_ms"] is None and r["batch"] == B and r["frames"] == Ty and r["world"] == 1
+        # frames_per_s counts padded frames (B x Ty), valid_frames_per_s the mel_len frames
+        assert r["valid_frames_per_s"] / r["frames_per_s"] == pytest.approx((48 + 30) / (B * Ty), rel=1e-3)
         got = [r["loss"][k] for k in ("total", "mse_before", "mse_after", "bce_stop")]
         assert got == pytest.approx(lv.float().cpu().tolist(), rel=1e-6)

@@ -1,10 +1,10 @@
 #!/bin/bash
-# One round-4 GPU pass in priority order, inside one gpurun call (run from the repo root):
-#   tools/r04_pass.sh <tag> [budget_s] [steps...]
+# One GPU pass in priority order, inside one gpurun call (run from the repo root):
+#   tools/gpu_pass.sh <tag> [budget_s] [steps...]
 # steps (default: dpt bench ab prof phases decab tests): each GPU step runs under its own
 # timeout; a step starts only while the call's time budget allows it; a timeout, abort or
 # segfault (124/137/134/139) ends the pass, a failing test run (rc 1) does not.
-TAG=${1:-r04x}; BUDGET=${2:-1100}; shift 2 || true
+TAG=${1:-r05x}; BUDGET=${2:-1100}; shift 2 || true
 STEPS=${*:-dpt bench ab prof phases decab tests}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -41,13 +41,6 @@ for s in $STEPS; do
                > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
              echo "$e $(lastms "$OUT/ab_run.json")" >> "$OUT/knobs.txt"
            done ;;
-    pipe) for i in 1 2; do
-            for f in --pipeline ""; do
-              run "pipe $f" 90 200 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-decode $f \
-                > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
-              echo "pipe${f:- off} $(lastms "$OUT/ab_run.json")" >> "$OUT/pipe.txt"
-            done
-          done ;;
     attn) for v in ${ATTN_VARIANTS:-3 4 5 3 4 5}; do
             run "attn $v" 60 120 env TT2_ATTN_VARIANT=$v python -u tools/attn_bench.py >> "$OUT/attn_v$v.txt" 2>&1
           done ;;
@@ -86,7 +79,6 @@ for s in $STEPS; do
     distt) run distt 60 300 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_syncbn.py -v --timeout 200 \
              --timeout-method thread > "$OUT/dist_tests.log" 2>&1 ;;
     otl) run otl 90 200 python -u tools/overlap_timeline.py > "$OUT/otl.txt" 2>&1 ;;
-    otlp) run otlp 90 200 python -u tools/overlap_timeline.py --pipeline > "$OUT/otlp.txt" 2>&1 ;;
     prof) run prof 150 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
             python3 bench.py --profile-run --steps 10 --warmup 2 > "$OUT/bench_step.json" 2> "$OUT/bench_step.err" ;;
     phases) run phases 120 300 env TT2_LIB=abl/phase.so python -u tools/g7_phases.py --json "$OUT/phases.json" \
@@ -116,6 +108,15 @@ for s in $STEPS; do
     tests) run tests 300 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
              > "$OUT/gpu_tests.log" 2>&1
            run smoke 60 120 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
+    probe) # SyncBN + encoder overlap capture probes, least to most likely to crash (tools/capture_probe.py)
+           for args in "--kind record --shape cfg2 --snap" "--kind rccl --shape small" "--kind rccl --shape cfg2" \
+                       "--kind rccl --shape cfg2 --snap"; do
+             run "probe $args" 60 180 python -u tools/capture_probe.py $args >> "$OUT/probe.txt" 2>&1
+           done ;;
+    newt) run newt 120 600 python -u -m pytest ${NEWT:-tests/test_gpu_capture.py tests/test_gpu_dp_order.py} -x -v \
+            --timeout 600 --timeout-method thread > "$OUT/new_tests.log" 2>&1 ;;
+    decprof) run decprof 120 300 rocprofv3 --kernel-trace --stats -d "$OUT/dk" -o run --output-format csv -- \
+               python3 tools/decode_prof.py > "$OUT/decprof.log" 2>&1 ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -208,7 +208,9 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
   if (k0 < k1) load_keys(k0, 0);
   T8<T> wpre[8];   // 16-bit types only: the f32 (parity-mode) kernel has no registers to spare
   if constexpr (sizeof(T) == 2) {
-    if (a.wo) oproj_prefetch<T, NW>(a, h, wpre);
+    // only waves that own a row block (w * 64 < H * 64): with fewer heads than waves the
+    // rows past N do not exist (oproj_slab's loop then skips the wave too)
+    if (a.wo && (int)(threadIdx.x >> 6) * 64 < a.H * D) oproj_prefetch<T, NW>(a, h, wpre);
   }
   float qv[8];
   if (a.wq) {

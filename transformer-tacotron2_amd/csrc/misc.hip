@@ -475,6 +475,7 @@ struct AdamArgs {
   int64_t n;
   const float* sumsq;   // clip: global squared gradient norm (device scalar) or null
   int32_t* step;        // device step counter (read; bumped by tt2_step_bump)
+  const int32_t* gate;  // null, or: update only while *gate != 0 (tt2_adam_gate)
   float lr, beta1, beta2, eps, wd, clip, warmup, d_model_rsqrt;
   int noam;
 };
@@ -493,6 +494,7 @@ TT2_DEV void adam_one(const AdamArgs& a, int64_t i, float g, float lr, float ste
 
 // one thread updates 4 consecutive parameters (n is a multiple of 16: slots are 16-aligned)
 __global__ __launch_bounds__(NT) void adam_kernel(AdamArgs a) {
+  if (a.gate && *a.gate == 0) return;   // a deferred update that already ran (or none pending)
   const int step = *a.step + 1;
   float scale = 1.f;
   if (a.clip > 0.f && a.sumsq) {
@@ -543,6 +545,17 @@ __global__ void step_bump_kernel(int32_t* step, uint32_t* seed) {
   if (threadIdx.x == 0) {
     if (step) step[0] += 1;
     if (seed) seed[0] += 1u;
+  }
+}
+
+__global__ void adam_gate_kernel(int32_t* gate, int32_t* step, int op) {
+  if (threadIdx.x == 0) {
+    if (op == 1) {
+      gate[0] = 1;
+    } else if (gate[0] != 0) {
+      if (step) step[0] += 1;
+      gate[0] = 0;
+    }
   }
 }
 
@@ -740,7 +753,7 @@ extern "C" size_t tt2_adam_workspace_size(void) { return (TT2_ADAM_NORM_BLOCKS +
 extern "C" int tt2_adam_step(const tt2_adam_args* p, hipStream_t s) {
   AdamArgs a{};
   a.p = p->params; a.g = p->grads; a.m = p->exp_avg; a.v = p->exp_avg_sq; a.shadow = (bf16*)p->shadow_bf16;
-  a.n = p->n; a.step = p->step;
+  a.n = p->n; a.step = p->step; a.gate = p->gate;
   a.lr = p->lr; a.beta1 = p->beta1; a.beta2 = p->beta2; a.eps = p->eps; a.wd = p->weight_decay;
   a.clip = p->clip_norm; a.warmup = p->warmup; a.noam = p->noam;
   a.d_model_rsqrt = p->d_model > 0 ? 1.f / sqrtf((float)p->d_model) : 1.f;
@@ -769,6 +782,12 @@ extern "C" int tt2_sumsq_parts(const float* g, int64_t n, float* parts, int32_t 
     return tt2_set_error(TT2_E_INVALID, "tt2_sumsq_parts: g 16-B aligned, parts, nparts > 0");
   hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(NT), 0, s, g, n, parts);
   return tt2_check_launch(hipGetLastError(), "tt2_sumsq_parts");
+}
+
+extern "C" int tt2_adam_gate(int32_t* gate, int32_t* step, int32_t op, hipStream_t s) {
+  if (!gate || (op != 0 && op != 1)) return tt2_set_error(TT2_E_INVALID, "tt2_adam_gate: gate, op 0 or 1");
+  hipLaunchKernelGGL(adam_gate_kernel, dim3(1), dim3(64), 0, s, gate, step, (int)op);
+  return tt2_check_launch(hipGetLastError(), "tt2_adam_gate");
 }
 
 extern "C" int tt2_step_bump(int32_t* step, uint32_t* seed, hipStream_t s) {

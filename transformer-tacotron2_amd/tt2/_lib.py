@@ -208,7 +208,7 @@ class AdamArgs(C.Structure):
         ("params", vp), ("grads", vp), ("exp_avg", vp), ("exp_avg_sq", vp), ("shadow_bf16", vp), ("step", vp),
         ("workspace", vp), ("ws_bytes", sz), ("n", i64),
         ("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32), ("weight_decay", f32), ("clip_norm", f32),
-        ("warmup", f32), ("noam", i32), ("d_model", i32), ("norm_parts", vp), ("norm_nparts", i32),
+        ("warmup", f32), ("noam", i32), ("d_model", i32), ("norm_parts", vp), ("norm_nparts", i32), ("gate", vp),
     ]
 
 
@@ -251,6 +251,8 @@ SIGNATURES.update({
     "tt2_adam_workspace_size": ([], sz),
     "tt2_adam_step": ([P_(AdamArgs), vp], C.c_int),
     "tt2_step_bump": ([vp, vp, vp], C.c_int),
+    "tt2_adam_gate": ([vp, vp, C.c_int32, vp], C.c_int),
+    "tt2_capture_joined": ([vp, C.POINTER(vp), C.c_int32, C.POINTER(C.c_int32)], C.c_int),
 })
 
 

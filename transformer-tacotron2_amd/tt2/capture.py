@@ -1,0 +1,108 @@
+"""hipGraph capture of a training step, with the fork/join discipline checked.
+
+A captured step forks work onto other streams (the overlapped backward's side stream, the
+RCCL comm stream, the encoder's stream) by stream waits; every such stream must be joined
+back into the capture's origin stream before the capture ends.  ``StepCapture`` wraps
+``torch.cuda.CUDAGraph.capture_begin`` / ``capture_end``:
+
+* before ending a capture it asks libtt2 (``tt2_capture_joined``: the streams' current capture
+  dependencies against the origin's ancestors in the graph being captured) whether every
+  registered stream is joined, and raises ``CaptureError`` naming the stream that is not,
+  instead of letting ``hipStreamEndCapture`` meet an unjoined fork;
+* on any exception inside the captured region it joins every registered stream that takes part
+  in the capture, ends the capture and drops the graph, then re-raises: the process survives
+  and no stream is left in capture mode (a capture left open made ``~CUDAGraph`` abort the
+  process).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+
+JOIN_NAMES = {0: "not captured", 1: "joined", 2: "UNJOINED", 3: "invalidated"}
+
+
+class CaptureError(RuntimeError):
+    pass
+
+
+def joined_status(origin: torch.cuda.Stream, streams: dict) -> dict:
+    """{name: 0 not in the capture / 1 joined / 2 unjoined / 3 invalidated} for each stream,
+    relative to the capturing origin stream (tt2_capture_joined)."""
+    names = list(streams)
+    if not names:
+        return {}
+    arr = (C.c_void_p * len(names))(*[streams[k].cuda_stream for k in names])
+    st = (C.c_int32 * len(names))()
+    _lib.check(_lib.lib().tt2_capture_joined(C.c_void_p(origin.cuda_stream), arr, len(names), st),
+               "tt2_capture_joined")
+    return {k: int(st[i]) for i, k in enumerate(names)}
+
+
+class StepCapture:
+    """``with StepCapture(graph, origin, streams_fn):`` captures the body into `graph` on
+    `origin` (made current).  streams_fn() -> {name: stream} lists the streams the body may
+    fork into the capture (evaluated at the end, so streams created lazily inside count)."""
+
+    def __init__(self, graph, origin: torch.cuda.Stream, streams_fn=None, capture_error_mode: str = "global"):
+        self.graph, self.origin = graph, origin
+        self.streams_fn = streams_fn or (lambda: {})
+        self.mode = capture_error_mode
+        self._ctx = None
+
+    def begin(self):
+        self.graph.capture_begin(capture_error_mode=self.mode)
+
+    def _streams(self) -> dict:
+        return {k: s for k, s in self.streams_fn().items() if s is not None and s != self.origin}
+
+    def end(self):
+        """End the capture after checking every registered stream is joined."""
+        st = joined_status(self.origin, self._streams())
+        bad = {k: JOIN_NAMES[v] for k, v in st.items() if v >= 2}
+        if bad:
+            self.abort()
+            raise CaptureError(f"graph capture: streams not joined into the origin before capture end: {bad}")
+        self.graph.capture_end()
+
+    def abort(self):
+        """Join whatever takes part in the capture, end it and discard the graph (errors of the
+        teardown itself are swallowed: the caller re-raises the original one)."""
+        try:
+            st = joined_status(self.origin, self._streams())
+            for k, s in self._streams().items():
+                if st.get(k) in (1, 2):
+                    self.origin.wait_stream(s)
+        except Exception:   # noqa: BLE001 - best effort: the capture must still be ended
+            pass
+        try:
+            self.graph.capture_end()
+        except Exception:   # noqa: BLE001
+            pass
+        try:
+            self.graph.reset()
+        except Exception:   # noqa: BLE001
+            pass
+
+    def __enter__(self):
+        self._ctx = torch.cuda.stream(self.origin)
+        self._ctx.__enter__()
+        try:
+            self.begin()
+        except BaseException:
+            self._ctx.__exit__(None, None, None)
+            raise
+        return self
+
+    def __exit__(self, et, ev, tb):
+        try:
+            if et is None:
+                self.end()
+            else:
+                self.abort()
+        finally:
+            self._ctx.__exit__(None, None, None)
+        return False

@@ -303,23 +303,46 @@ def sync_kind(group=None) -> str:
 
 
 def attach(model, group=None, bucket_bytes: int = 25 << 20, kind: str | None = None,
-           sync_bn: bool = False) -> GradSync:
+           sync_bn: bool = False, sync_cls=None, bn_cls=None) -> GradSync:
     """Wire a TransformerTTS for data parallelism: gradient pre-scaling and the
     bucket hook.  Returns the sync object whose finish() goes between backward and
     the optimizer step (pass it as train_step(..., sync_grads=sync.finish)).
     sync_bn: SyncBatchNorm (the encoder pre-net's and post-net's BatchNorms take their
-    training statistics over every rank's rows; BnSync)."""
+    training statistics over every rank's rows; BnSync).
+    sync_cls / bn_cls: the exchange classes (default RcclGradSync or GradSync by `kind`, and
+    BnSync); a subclass may swap the transport, as the issue-order test's recording syncs do."""
     eng = model.engine
     kind = kind or sync_kind(group)
-    cls = RcclGradSync if kind == "rccl" else GradSync
+    cls = sync_cls or (RcclGradSync if kind == "rccl" else GradSync)
     sync = cls(eng.grads, bucket_bytes, group)
     eng.grad_scale = 1.0 / sync.world
     eng.grad_ready_hook = sync.ready
     sync.engine = eng
     if sync_bn:
         rank = dist.get_rank(group) if dist.is_initialized() else 0
-        eng.bn_sync = BnSync(sync.world, rank, group, grad_sync=sync if kind == "rccl" else None, device=eng.dev)
+        eng.bn_sync = (bn_cls or BnSync)(sync.world, rank, group, grad_sync=sync if sync.in_graph else None,
+                                         device=eng.dev)
     return sync
+
+
+def compare_issue_logs(logs: list) -> list:
+    """Every rank must issue the same collectives on a communicator in the same order (one
+    stream per communicator; a rank that issues bucket k+1 before bucket k, or a BatchNorm
+    exchange between other buckets, deadlocks an N-rank replay).  logs[r] is rank r's
+    sequence of (kind, ...) records; returns [(rank, index, rank-0 record, this rank's
+    record)] for every rank whose sequence differs from rank 0's (first difference only;
+    None past the end of the shorter sequence)."""
+    out = []
+    ref = logs[0]
+    for r, lg in enumerate(logs[1:], 1):
+        n = max(len(ref), len(lg))
+        for i in range(n):
+            a = tuple(ref[i]) if i < len(ref) else None
+            b = tuple(lg[i]) if i < len(lg) else None
+            if a != b:
+                out.append((r, i, a, b))
+                break
+    return out
 
 
 def broadcast_params(model, src: int = 0, group=None):

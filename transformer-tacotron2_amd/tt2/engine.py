@@ -235,14 +235,18 @@ class TTSEngine:
         self.side_groups = int(os.environ.get("TT2_SIDE_WG", "0"))
         self.side_start = int(os.environ.get("TT2_SIDE_START", "-1"))   # decoder layer whose backward starts it
         self.enc_overlap = int(os.environ.get("TT2_ENC_OVERLAP", "1"))   # see forward()
+        # ... also with SyncBatchNorm (the encoder pre-net's exchanges then fork the comm stream
+        # from the side stream); TT2_ENC_OVERLAP_SYNCBN=0 keeps the encoder on the main stream there
+        self.enc_overlap_syncbn = os.environ.get("TT2_ENC_OVERLAP_SYNCBN", "1") != "0"
         # pipelined optimizer (opt-in: TransformerTTS.pipeline_optimizer): a step's Adam is
         # deferred to the start of the next forward, where the encoder's share runs on the side
         # stream ahead of the encoder and the rest on the main stream ahead of the decoder,
-        # beside the encoder's forward (the same updates in the same order: identical results)
+        # beside the encoder's forward (the same updates in the same order: identical results).
+        # Whether an update is pending lives on the device (adam_gate: armed by optimizer_step,
+        # consumed by the deferred Adam or by flush_optimizer), so a captured step never applies
+        # an update twice after an eager flush, nor a stale one after load_state_dict
         self.pipeline_opt = False
-        self._adam_pending = None
-        # overlapped backward, dev knob: each decoder layer's cross-attention dK / dV on the side
-        self.xattn_split = int(os.environ.get("TT2_XATTN_SPLIT", "0"))
+        self._adam_parts = None   # the clip-norm partials the deferred Adam reads (a fixed buffer)
         self.cd = dtype
         self.dev = torch.device(device)
         self.lay = Layout(build_slots(c))
@@ -258,6 +262,7 @@ class TTSEngine:
         self.pe = sinusoid_table(c.max_len, c.d_model).to(self.dev)
         self.seed = torch.tensor([seed], dtype=torch.int32, device=self.dev)   # per-step dropout seed (uint32)
         self.step_t = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.adam_gate = torch.zeros(1, dtype=torch.int32, device=self.dev)   # pipelined Adam pending
         self.ws = ops.Workspace()
         self.arenas: dict[tuple, Arena] = {}
         self.training = True
@@ -522,11 +527,8 @@ class TTSEngine:
         pre-net and layer 0's self-attention block, which do not need the memory (the step
         6.94 vs 7.03 ms measured; 1 issues the encoder first, 2 the decoder's part first: the
         same; 0 off)."""
-        parts, self._adam_pending = self._adam_pending, None   # pipelined optimizer: last step's Adam
-        # not with SyncBatchNorm: its statistics exchange forked onto the comm stream from the side
-        # stream made the captured step's hipStreamEndCapture segfault (ROCm 7.2, RCCL in-graph,
-        # tests/test_gpu_dist.py cfg2 sync_bn); the encoder then runs on the main stream
-        if self.enc_overlap and self.cd == torch.bfloat16 and self.bn_sync is None:
+        parts = self._adam_parts if self.pipeline_opt else None   # pipelined: last step's Adam (gated)
+        if self.enc_overlap and self.cd == torch.bfloat16 and (self.bn_sync is None or self.enc_overlap_syncbn):
             if self._side is None:
                 self._side = torch.cuda.Stream()
                 self._side_ws = ops.Workspace()
@@ -541,7 +543,7 @@ class TTSEngine:
                 try:
                     with torch.cuda.stream(side):
                         for lo, hi in enc_r:   # the encoder's parameters first
-                            self._adam(lo, hi, parts)
+                            self._adam(lo, hi, parts, gated=True)
                         self.forward_encoder(A)
                 finally:
                     self.ws = ws
@@ -552,7 +554,7 @@ class TTSEngine:
                 lo = 0
                 for a, b in enc_r + [(self.lay.numel, self.lay.numel)]:
                     if a > lo:
-                        self._adam(lo, a, parts)
+                        self._adam(lo, a, parts, gated=True)
                     lo = b
             if self.enc_overlap == 1:
                 encoder()
@@ -564,13 +566,13 @@ class TTSEngine:
                 encoder()
             main.wait_stream(side)   # the memory K/V, before layer 0's cross-attention
             if parts is not None:
-                ops.step_bump(self.step_t, None)   # both halves of the deferred Adam have read it
+                ops.adam_gate(self.adam_gate, self.step_t)   # both halves of the deferred Adam have read it
             for _ in dec:
                 pass
         else:
             if parts is not None:
-                self._adam(0, self.lay.numel, parts)
-                ops.step_bump(self.step_t, None)
+                self._adam(0, self.lay.numel, parts, gated=True)
+                ops.adam_gate(self.adam_gate, self.step_t)
             self.forward_encoder(A)
             for _ in self._decoder_steps(A):
                 pass
@@ -802,7 +804,6 @@ class TTSEngine:
         mkv = A["mkv"]
         kvld = c.n_dec * 2 * d
         g_mkv = A["g_mkv"]
-        xsplit = ov and self.xattn_split and not self._side_live
         for l in reversed(range(c.n_dec)):
             p, base = f"dec{l}.", SITE_DEC_LAYER + 4 * l
             if ov and l == self.side_start and not self._side_live:
@@ -839,17 +840,7 @@ class TTSEngine:
             xargs = (A[f"dcq{l}"], mkv[:, ko:], mkv[:, ko + d:], A[f"dcatt{l}"], A["g_att"], A[f"dclse{l}"],
                      A["delta"], g_cq, g_mkv[:, ko:], g_mkv[:, ko + d:], d, kvld, kvld, d, d, d, kvld, kvld,
                      B, H, Ty, Tx, A["text_len"], False, scale)
-            if xsplit:
-                # the memory's dK / dV (needed only by the memory gradient after the decoder
-                # backward) on the side stream; dQ (the critical chain) here
-                ev = torch.cuda.Event()
-                ev.record()
-                self._side.wait_event(ev)
-                with torch.cuda.stream(self._side):
-                    ops.attn_bwd(*xargs, parts=2)
-                ops.attn_bwd(*xargs, parts=1)
-            else:
-                ops.attn_bwd(*xargs)
+            ops.attn_bwd(*xargs)
             self._wgrad(g_cq, h1, self.G(p + "cq.w"), d, d, Md, gb=self.G(p + "cq.b"))
             self._dgrad(g_cq, self.W(p + "cq.w"), gx2, Md, d, d, res=A["g_res"])
             gx, gx2 = gx2, gx
@@ -897,8 +888,6 @@ class TTSEngine:
         gf1 = A["g_f1"].view(-1)[:Me * F].view(Me, F)
         gatt = A["g_att"].view(-1)[:Me * d].view(Me, d)
         gq = A["g_qkv"].view(-1)[:Me * 3 * d].view(Me, 3 * d)
-        if xsplit:   # the side stream's dK / dV of every layer's memory are in g_mkv
-            torch.cuda.current_stream().wait_stream(self._side)
         self._dgrad(g_mkv, self.W("dec.kv.w"), gxe, Me, d, kvld)
         if ov and not self._side_live:   # the weight gradients queued so far run beside the encoder backward
             self._start_side()
@@ -1017,30 +1006,38 @@ class TTSEngine:
                     ops.sumsq_parts(self.grads[lo:hi], self._norm_buf[at:], nb)
             parts = self._norm_buf[:used]
         if self.pipeline_opt:
-            # pipelined: this step's Adam runs at the start of the next forward (pending), beside
-            # the encoder; only the dropout seed advances now
+            # pipelined: this step's Adam runs at the start of the next forward (armed on the
+            # device), beside the encoder; only the dropout seed advances now
             if parts is None:
                 raise RuntimeError("pipelined optimizer: no clip-norm partial sums (optimizer_step without backward)")
-            self._adam_pending = parts
+            if self._adam_parts is not None and self._adam_parts.data_ptr() != parts.data_ptr():
+                raise RuntimeError("pipelined optimizer: the clip-norm partials moved")
+            self._adam_parts = parts
+            ops.adam_gate(self.adam_gate, arm=True)
             ops.step_bump(None, self.seed)
             return
         self._adam(0, self.lay.numel, parts)
         ops.step_bump(self.step_t, self.seed)
 
-    def _adam(self, lo, hi, parts):
+    def _adam(self, lo, hi, parts, gated: bool = False):
         o = self.opt
         sl = lambda t: t[lo:hi] if t is not None else None   # noqa: E731
         ops.adam_step(sl(self.params), sl(self.grads), sl(self.exp_avg), sl(self.exp_avg_sq), sl(self.shadow),
                       self.step_t, hi - lo, o["lr"], o["beta1"], o["beta2"], o["eps"], o["weight_decay"],
-                      o["clip_norm"], o["warmup"], o["noam"], self.cfg.d_model, ws=self.ws, norm_parts=parts)
+                      o["clip_norm"], o["warmup"], o["noam"], self.cfg.d_model, ws=self.ws, norm_parts=parts,
+                      gate=self.adam_gate if gated else None)
 
     def flush_optimizer(self):
         """Pipelined optimizer: run the pending Adam now (before parameters are read, saved or
-        evaluated, or pipelining is switched off)."""
-        if self._adam_pending is not None:
-            parts, self._adam_pending = self._adam_pending, None
-            self._adam(0, self.lay.numel, parts)
-            ops.step_bump(self.step_t, None)
+        evaluated, or pipelining is switched off).  Gated on the device: with nothing pending
+        (never armed, already flushed, or consumed by a replay) the launches change nothing."""
+        if self._adam_parts is not None:
+            self._adam(0, self.lay.numel, self._adam_parts, gated=True)
+            ops.adam_gate(self.adam_gate, self.step_t)
+
+    def drop_pending_update(self):
+        """Forget a pending pipelined update (its gradients belong to replaced weights)."""
+        self.adam_gate.zero_()
 
     def _enc_param_ranges(self):
         """Flat ranges the encoder forward reads: the encoder's slots, and the memory K/V

@@ -5,7 +5,8 @@
         model.train_step(*batch, sync_grads=sync.finish)   # or a captured run(...)
 
 One JSON object per training step: wall time of the step on the device (HIP events on
-the compute stream around it), mel frames/s, the loss terms, the span of the gradient
+the compute stream around it), mel frames/s (padded frames, B x Ty per rank, times the world size; valid_frames_per_s counts
+the mel_len frames of this rank's batch times the world size), the loss terms, the span of the gradient
 all-reduce on the comm stream (RcclGradSync; null without data parallelism) and the
 achieved useful TFLOP/s against the dense bf16 MFMA peak.  Nothing blocks the step: a
 step's events and loss are read back once the NEXT step has been issued (and at close()),
@@ -47,7 +48,10 @@ class StepMetrics:
 
     LOSS_KEYS = ("total", "mse_before", "mse_after", "bce_stop")
 
-    def __init__(self, path: str, cfg, world: int = 1):
+    def __init__(self, path: str, cfg, world: int | None = None):
+        """world: ranks whose frames count in frames/s; None: torch.distributed's world size,
+        looked up when the first line is written (after init_process_group, wherever the
+        model was built)."""
         self.path, self.cfg, self.world = path, cfg, world
         d = os.path.dirname(os.path.abspath(path))
         os.makedirs(d, exist_ok=True)
@@ -61,11 +65,18 @@ class StepMetrics:
         ev.record()
         self._open = ev
 
-    def end(self, loss: torch.Tensor, B: int, Tx: int, Ty: int, sync=None):
+    def _world(self) -> int:
+        if self.world is None:
+            import torch.distributed as dist
+            self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        return self.world
+
+    def end(self, loss: torch.Tensor, B: int, Tx: int, Ty: int, sync=None, mel_len: torch.Tensor | None = None):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         ar = sync.pop_span() if sync is not None and hasattr(sync, "pop_span") else None
-        cur = (self._open, ev, loss.detach().clone(), (B, Tx, Ty), ar, time.time())
+        valid = mel_len.detach().to(torch.int64).sum() if mel_len is not None else None   # device scalar, no sync
+        cur = (self._open, ev, loss.detach().clone(), (B, Tx, Ty), ar, time.time(), valid)
         self._open = None
         self.flush()
         self._pending = cur
@@ -73,19 +84,21 @@ class StepMetrics:
     def flush(self):
         if self._pending is None:
             return
-        t0, t1, loss, (B, Tx, Ty), ar, wall = self._pending
+        t0, t1, loss, (B, Tx, Ty), ar, wall, valid = self._pending
         self._pending = None
         t1.synchronize()
         ms = t0.elapsed_time(t1)
         vals = loss.float().cpu().tolist()
         fl = step_flops(self.cfg, B, Tx, Ty)
+        world = self._world()
         rec = {"step": self.step, "time": round(wall, 3), "ms": round(ms, 4),
-               "frames_per_s": round(self.world * B * Ty / (ms / 1e3), 1),
+               "frames_per_s": round(world * B * Ty / (ms / 1e3), 1),
+               "valid_frames_per_s": round(world * int(valid.item()) / (ms / 1e3), 1) if valid is not None else None,
                "loss": {k: v for k, v in zip(self.LOSS_KEYS, vals)},
                "allreduce_ms": round(ar[0].elapsed_time(ar[1]), 4) if ar is not None else None,
                "tflops": round(fl / (ms / 1e3) / 1e12, 2),
                "frac_of_peak": round(fl / (ms / 1e3) / 1e12 / PEAK_BF16_TFLOPS, 4),
-               "batch": B, "text_len": Tx, "frames": Ty, "world": self.world}
+               "batch": B, "text_len": Tx, "frames": Ty, "world": world}
         self._f.write(json.dumps(rec) + "\n")
         self.step += 1
 

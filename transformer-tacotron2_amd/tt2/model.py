@@ -35,6 +35,7 @@ import torch.nn as nn
 from torch.autograd.function import once_differentiable
 
 from . import ops
+from .capture import StepCapture
 from .config import TTSConfig
 from .engine import Arena, TTSEngine
 from .params import from_state_dict, grads_to_state_dict_names, to_state_dict
@@ -136,7 +137,9 @@ class TransformerTTS(nn.Module):
         the same as without it, in the same order, so the trajectory is identical; the
         parameters lag one Adam behind until flush_optimizer() (which state_dict(),
         save_checkpoint() and infer() call).  A captured step must be taken after at least one
-        pipelined eager step (its graph then holds the deferred Adam)."""
+        pipelined eager step (its graph then holds the deferred Adam).  Whether an update is
+        pending is a device flag the deferred Adam checks, so flushing between replays (a
+        checkpoint, an eval) never applies an update twice."""
         if not on:
             self.engine.flush_optimizer()
         self.engine.pipeline_opt = on
@@ -153,7 +156,7 @@ class TransformerTTS(nn.Module):
 
     def load_state_dict(self, sd, strict: bool = True):
         P, S, nbt = from_state_dict(self.cfg, sd)
-        self.engine._adam_pending = None   # a pending pipelined Adam belongs to the replaced weights
+        self.engine.drop_pending_update()   # a pending pipelined Adam belongs to the replaced weights
         self.engine.load_slots(P, S, nbt)
         self._shadow_version = self.engine.params._version
 
@@ -372,19 +375,18 @@ class TransformerTTS(nn.Module):
 
     def enable_metrics(self, path: str | None, world: int | None = None):
         """Per-step JSONL metrics (tt2/metrics.py) appended to `path`; None turns them off.
-        world: ranks whose frames count in frames/s (default: torch.distributed's world)."""
+        world: ranks whose frames count in frames/s (default: torch.distributed's world size,
+        looked up when the first line is written, so a model built before
+        init_process_group still reports the whole job)."""
         from .metrics import StepMetrics
         if self.metrics is not None:
             self.metrics.close()
             self.metrics = None
         if path:
-            if world is None:
-                import torch.distributed as dist
-                world = dist.get_world_size() if dist.is_initialized() else 1
             self.metrics = StepMetrics(path, self.cfg, world)
 
     def _metrics_end(self, A: Arena, sync_grads):
-        self.metrics.end(A["loss"], A.B, A.Tx, A.Ty, sync=getattr(sync_grads, "__self__", None))
+        self.metrics.end(A["loss"], A.B, A.Tx, A.Ty, sync=getattr(sync_grads, "__self__", None), mel_len=A["mel_len"])
 
     def train_step(self, text, text_len, mel, mel_len, sync_grads=None):
         """One optimisation step, eagerly.  Returns the device loss vector
@@ -412,7 +414,7 @@ class TransformerTTS(nn.Module):
                                "the nccl backend (RCCL, captured)")
         if e.exp_avg is None:
             e.init_optimizer()
-        if e.pipeline_opt and e._adam_pending is None:
+        if e.pipeline_opt and e._adam_parts is None:
             raise RuntimeError("capture_train_step: with the pipelined optimizer, capture after an eager step "
                                "(the graph holds that step's deferred Adam)")
         A = e.arena(B, Tx, Ty)
@@ -430,45 +432,63 @@ class TransformerTTS(nn.Module):
         g2 = torch.cuda.CUDAGraph() if sync_grads is not None else None
         # the segmented capture ends graphs inside the backward, where the overlapped weight
         # gradients' side stream (engine.wgrad_overlap) would still be forked: off for it
+        # (only the gloo / TT2_DP_SYNC=segmented path takes this branch;
+        # the nccl path at N > 1 is the one-graph capture below, with the side stream)
         ov_saved = e.wgrad_overlap
         if sync is not None and hasattr(sync, "take_ready"):
             e.wgrad_overlap = False
         segs = []   # [(graph, bucket indices launched right after its replay)]
+        streams = lambda: self._capture_streams(sync)   # noqa: E731
         # captures are thread-local: RCCL's watchdog thread polls its work events during
         # capture, which a global-mode capture treats as a prohibited call (capture invalidated)
         torch.cuda.synchronize()
-        with torch.cuda.stream(s):
-            cur = [torch.cuda.CUDAGraph()]
-            cur[0].capture_begin(capture_error_mode=ops.CAPTURE_MODE)
-            if sync is not None and hasattr(sync, "take_ready"):
-                # cut the forward+backward graph wherever a gradient bucket becomes final,
-                # so the replay can start that bucket's all-reduce while the rest of the
-                # backward runs (RCCL stays outside the graphs, on its own stream)
-                sync.reset()
+        cur = [StepCapture(torch.cuda.CUDAGraph(), s, streams, ops.CAPTURE_MODE)]
+        try:
+            with torch.cuda.stream(s):
+                cur[0].begin()
+                if sync is not None and hasattr(sync, "take_ready"):
+                    # cut the forward+backward graph wherever a gradient bucket becomes final,
+                    # so the replay can start that bucket's all-reduce while the rest of the
+                    # backward runs (RCCL stays outside the graphs, on its own stream)
+                    sync.reset()
 
-                def cut(offset):
-                    if offset <= 0:       # the last buckets go to finish(): no empty tail graph
-                        return
-                    idx = sync.take_ready(offset)
-                    if idx:
-                        cur[0].capture_end()
-                        segs.append((cur[0], idx))
-                        cur[0] = torch.cuda.CUDAGraph()
-                        cur[0].capture_begin(capture_error_mode=ops.CAPTURE_MODE)
-                e.grad_ready_hook = cut
-            e.forward(A)
-            e.loss(A)
-            e.backward(A)
-            e.grad_ready_hook = None
-            if g2 is None:
-                e.optimizer_step()
-            cur[0].capture_end()
-            segs.append((cur[0], []))
-            if sync is not None and hasattr(sync, "take_ready"):
-                sync.reset()
-            if g2 is not None:
-                with torch.cuda.graph(g2, stream=s, capture_error_mode=ops.CAPTURE_MODE):
+                    def cut(offset):
+                        if offset <= 0:       # the last buckets go to finish(): no empty tail graph
+                            return
+                        idx = sync.take_ready(offset)
+                        if idx:
+                            c, cur[0] = cur[0], None
+                            c.end()
+                            segs.append((c.graph, idx))
+                            cur[0] = StepCapture(torch.cuda.CUDAGraph(), s, streams, ops.CAPTURE_MODE)
+                            cur[0].begin()
+                    e.grad_ready_hook = cut
+                e.forward(A)
+                e.loss(A)
+                e.backward(A)
+                e.grad_ready_hook = None
+                if g2 is None:
                     e.optimizer_step()
+                c, cur[0] = cur[0], None
+                c.end()
+                segs.append((c.graph, []))
+                if sync is not None and hasattr(sync, "take_ready"):
+                    sync.reset()
+                if g2 is not None:
+                    with StepCapture(g2, s, streams, ops.CAPTURE_MODE):
+                        e.optimizer_step()
+        except BaseException:
+            # a capture left open aborts the process at teardown (~CUDAGraph): end it, drop the
+            # graphs, restore the engine, re-raise
+            if cur[0] is not None:
+                cur[0].abort()
+            e.grad_ready_hook = hook
+            e.wgrad_overlap = ov_saved
+            e.nbt = nbt_saved
+            if sync is not None and hasattr(sync, "reset"):
+                sync.reset()
+            torch.cuda.current_stream().wait_stream(s)
+            raise
         torch.cuda.current_stream().wait_stream(s)
         e.grad_ready_hook = hook
         e.wgrad_overlap = ov_saved
@@ -495,6 +515,17 @@ class TransformerTTS(nn.Module):
 
         return run
 
+    def _capture_streams(self, sync=None) -> dict:
+        """The streams a captured step may fork into the capture, by role."""
+        e = self.engine
+        out = {"side": e._side}
+        if sync is not None and getattr(sync, "stream", None) is not None:
+            out["comm"] = sync.stream
+        bn = e.bn_sync
+        if bn is not None and getattr(bn, "grad_sync", None) is not None:
+            out["bn_comm"] = bn.grad_sync.stream
+        return out
+
     def _capture_in_graph(self, A: Arena, sync, hook, nbt_saved):
         """The data-parallel step as ONE hipGraph: the bucket all-reduces (RcclGradSync)
         fork onto the comm stream inside the capture as each bucket's gradients become
@@ -506,13 +537,19 @@ class TransformerTTS(nn.Module):
         torch.cuda.synchronize()
         sync.reset()
         try:
-            with torch.cuda.graph(g, stream=s, capture_error_mode=ops.CAPTURE_MODE):
+            # every stream the step forks (side, comm) is checked joined before the capture
+            # ends; an exception ends the capture and re-raises (tt2/capture.py)
+            with StepCapture(g, s, lambda: self._capture_streams(sync), ops.CAPTURE_MODE):
                 e.grad_ready_hook = sync.ready
                 e.forward(A)
                 e.loss(A)
                 e.backward(A)
                 sync.finish()
                 e.optimizer_step()
+        except BaseException:
+            e.nbt = nbt_saved
+            torch.cuda.current_stream().wait_stream(s)
+            raise
         finally:
             e.grad_ready_hook = hook
             sync.reset()
@@ -529,7 +566,7 @@ class TransformerTTS(nn.Module):
                 e.nbt[k] += 1
             self._last = A
             if self.metrics is not None:
-                self.metrics.end(A["loss"], A.B, A.Tx, A.Ty)   # the all-reduce span is inside the graph
+                self.metrics.end(A["loss"], A.B, A.Tx, A.Ty, mel_len=A["mel_len"])   # all-reduce span: inside the graph
             return A["loss"]
 
         return run

@@ -502,9 +502,10 @@ def sumsq_parts(g: torch.Tensor, parts: torch.Tensor, nparts: int):
 
 def adam_step(params, grads, m, v, shadow, step, n, lr, beta1=0.9, beta2=0.98, eps=1e-9, weight_decay=0.0,
               clip_norm=1.0, warmup=4000.0, noam=True, d_model=512, ws: Workspace | None = None,
-              norm_parts: torch.Tensor | None = None):
+              norm_parts: torch.Tensor | None = None, gate: torch.Tensor | None = None):
     """norm_parts: the squared-norm partial sums of every gradient (sumsq_parts over ranges
-    covering grads), so the clip needs no pass of its own over the gradients."""
+    covering grads), so the clip needs no pass of its own over the gradients.
+    gate: int32 device flag; the update runs only while it is non-zero (adam_gate)."""
     L = lib()
     a = _lib.AdamArgs()
     if norm_parts is not None:
@@ -513,6 +514,7 @@ def adam_step(params, grads, m, v, shadow, step, n, lr, beta1=0.9, beta2=0.98, e
     a.shadow_bf16, a.step, a.n = ptr(shadow), step.data_ptr(), n
     a.lr, a.beta1, a.beta2, a.eps, a.weight_decay = lr, beta1, beta2, eps, weight_decay
     a.clip_norm, a.warmup, a.noam, a.d_model = clip_norm, warmup, int(noam), d_model
+    a.gate = ptr(gate)
     buf = (ws or _WS).get(L.tt2_adam_workspace_size())
     a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
     check(L.tt2_adam_step(C.byref(a), stream_ptr()), "tt2_adam_step")
@@ -520,6 +522,11 @@ def adam_step(params, grads, m, v, shadow, step, n, lr, beta1=0.9, beta2=0.98, e
 
 def step_bump(step, seed=None):
     check(lib().tt2_step_bump(ptr(step), ptr(seed), stream_ptr()), "tt2_step_bump")
+
+
+def adam_gate(gate, step=None, arm: bool = False):
+    """arm: gate = 1.  Otherwise (consume): if gate != 0, step += 1 and gate = 0."""
+    check(lib().tt2_adam_gate(gate.data_ptr(), ptr(step), 1 if arm else 0, stream_ptr()), "tt2_adam_gate")
 
 
 def attn_decode(q, k, v, out, q_ld, k_bstride, k_ld, v_bstride, v_ld, o_ld, batch, heads, tk, key_len=None,
