@@ -442,7 +442,8 @@ int tt2_batchnorm_bwd_apply(const tt2_bn_args* a, hipStream_t stream);
 /* -------------------------------------------------- embedding / pos. enc. */
 int tt2_embedding_fwd(const int64_t* ids, const void* table, void* out, int m, int c, int vocab, int dtype,
                       hipStream_t stream);
-/* dtable (f32) is zeroed then scatter-added; rows == pad_idx get no gradient */
+/* dtable (f32) row v = sum of dout rows with ids == v, added in increasing row order (gathered per
+ * table row: deterministic, no atomics); every row is written; rows == pad_idx get zero */
 int tt2_embedding_bwd(const int64_t* ids, const void* dout, float* dtable, int m, int c, int vocab, int pad_idx,
                       int dtype, hipStream_t stream);
 

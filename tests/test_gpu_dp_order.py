@@ -16,8 +16,8 @@ without SyncBatchNorm:
   sequence, and rank 1's sequences equal rank 0's (tt2.dist.compare_issue_logs over
   all_gather_object);
 * every bucket is handed over from the side stream, once, in reverse layout order; with
-  SyncBatchNorm 16 exchanges per step, the encoder's issued from the side stream (the encoder
-  forward overlap is on under SyncBatchNorm too);
+  SyncBatchNorm 16 exchanges per step, all issued from the main stream (the capture's origin:
+  the encoder pre-net runs there, its layers on the side stream, engine.forward);
 * without SyncBatchNorm the eager overlapped step's reduced gradient equals the mean of the two
   shards' standalone gradients (<= 1e-6 relative) and is bitwise equal on both ranks;
 * negative control: rank 1 holding one bucket's hand-off back behind the next one is flagged.
@@ -180,7 +180,7 @@ def test_production_schedule_issue_order_two_ranks():
             bns = [x for x in seq if x[0] == "bn"]
             if bn:
                 assert len(bns) == 16, len(bns)
-                assert sum(x[2] == "side" for x in bns) == 3      # encoder pre-net forward, overlapped
+                assert all(x[2] == "main" for x in bns)           # the comm stream forks from the origin only
             else:
                 assert bns == []
             assert len(mism["held"]) == 1 and mism["held"][0][0] == 1, mism["held"]   # the control is caught

@@ -69,6 +69,51 @@ def test_overlapped_backward_gradients_bitwise(knobs):
         assert ((got - ref).norm() / ref.norm()).item() < 1e-5
 
 
+def test_overlapped_backward_bitwise_cfg2():
+    """The production bf16 schedule at the cfg2 shape (B = 16, 128 phonemes, 800 frames, ragged
+    lengths, dropout on, default side-grid caps and split factors): the overlapped backward with
+    the encoder forward on the side stream writes the same gradients as the in-place schedule
+    (which test_gpu_bf16_parity pins to the oracle), bit for bit, and a captured step of each
+    schedule leaves the same parameters."""
+    g = torch.Generator().manual_seed(12)
+    B, Tx, Ty = 16, 128, 800
+    text = torch.randint(1, 80, (B, Tx), generator=g)
+    tl = torch.randint(Tx // 2, Tx + 1, (B,), generator=g)
+    mel = torch.randn(B, Ty, 80, generator=g)
+    ml = torch.randint(Ty // 2, Ty + 1, (B,), generator=g)
+    tl[3], ml[5] = Tx, Ty
+    for i in range(B):
+        text[i, tl[i]:] = 0
+        mel[i, ml[i]:] = 0
+    b = [t.cuda() for t in (text, tl, mel, ml)]
+    ref_m, ov_m = _model(False, enc_overlap=0), _model(True)
+    assert ov_m.engine.enc_overlap and ov_m.engine.side_groups == 0 and ov_m.engine.side_split == 1
+    ref, got = _grads(ref_m, b), _grads(ov_m, b)
+    wo = _grads(_model(True, enc_overlap=0), b)     # the weight-gradient overlap alone
+    twice = _grads(_model(False, enc_overlap=0), b)   # the in-place schedule against itself
+    lay = ref_m.engine.lay
+
+    def diff(x):
+        out = []
+        for name in lay.slots:
+            u, v = lay.view(ref, name), lay.view(x, name)
+            if not torch.equal(u, v):
+                out.append((name, float((u - v).abs().max()), float(u.abs().max())))
+        return out
+    assert diff(twice) == [], ("in-place schedule not reproducible", diff(twice)[:8])
+    assert diff(wo) == [], ("overlapped backward", diff(wo)[:8])
+    assert diff(got) == [], ("overlapped backward + encoder forward overlap", diff(got)[:8])
+    for m in (ref_m, ov_m):
+        m.train_step(*b)
+    runs = [m.capture_train_step(B, Tx, Ty) for m in (ref_m, ov_m)]
+    for _ in range(2):
+        la, lb = (r(*b).clone() for r in runs)
+        assert torch.equal(la, lb)
+    torch.cuda.synchronize()
+    assert torch.equal(ref_m.engine.params, ov_m.engine.params)
+    assert torch.equal(ref_m.engine.exp_avg_sq, ov_m.engine.exp_avg_sq)
+
+
 def test_overlapped_step_clip_norm_and_graph():
     """A train step with the overlap: the clip norm's partial sums are taken over the same
     gradient ranges as in the in-place schedule (on the side stream as each range becomes final,

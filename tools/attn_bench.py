@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import torch  # noqa: E402
 
-from v9_ab import graph_of, time_graph, ops  # noqa: E402
+from gemm_ab import graph_of, time_graph, ops  # noqa: E402
 
 B, H, D = 16, 8, 64
 CASES = [("dec self causal", 800, 800, True), ("cross", 800, 128, False), ("enc self", 128, 128, False)]

@@ -8,7 +8,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import torch  # noqa: E402
 
-from v9_ab import graph_of, time_graph, ops  # noqa: E402
+from gemm_ab import graph_of, time_graph, ops  # noqa: E402
 
 SHAPES = [(12800, 2048, 512), (12800, 1536, 512), (12800, 512, 512), (12800, 512, 2048), (2048, 6144, 512),
           (2048, 2048, 512), (2048, 512, 2048), (4096, 4096, 4096), (8192, 8192, 8192)]

@@ -10,6 +10,7 @@ bucket and BatchNorm exchange final, as in the test)."""
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import os
 import socket
 import sys
@@ -24,6 +25,8 @@ import torch.distributed as dist  # noqa: E402
 
 
 def main():
+    faulthandler.enable()
+    os.environ.setdefault("TT2_CAPTURE_TRACE", "1")
     ap = argparse.ArgumentParser()
     ap.add_argument("--kind", default="rccl", choices=["rccl", "record"])
     ap.add_argument("--shape", default="cfg2", choices=["small", "cfg2"])

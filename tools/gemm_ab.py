@@ -2,7 +2,7 @@
 variant, each timed as 10 launches replayed from a hipGraph (no host gaps), interleaved rounds,
 and the forced variant's output checked against the auto plan's.
 
-    python tools/v9_ab.py [variant=16]
+    python tools/gemm_ab.py [variant=16]  (also the graph_of / time_graph helpers of the other A/B tools)
 """
 import os
 import sys

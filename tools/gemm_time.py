@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import torch  # noqa: E402
 
-from v9_ab import SHAPES, graph_of, time_graph, ops, ACT_RELU  # noqa: E402
+from gemm_ab import SHAPES, graph_of, time_graph, ops, ACT_RELU  # noqa: E402
 
 
 def main():

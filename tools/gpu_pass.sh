@@ -109,10 +109,13 @@ for s in $STEPS; do
              > "$OUT/gpu_tests.log" 2>&1
            run smoke 60 120 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     probe) # SyncBN + encoder overlap capture probes, least to most likely to crash (tools/capture_probe.py)
-           for args in "--kind record --shape cfg2 --snap" "--kind rccl --shape small" "--kind rccl --shape cfg2" \
-                       "--kind rccl --shape cfg2 --snap"; do
-             run "probe $args" 60 180 python -u tools/capture_probe.py $args >> "$OUT/probe.txt" 2>&1
+           for args in ${PROBES:-"--kind record --shape cfg2 --snap"}; do
+             run "probe ${args//,/ }" 60 180 python -u tools/capture_probe.py ${args//,/ } >> "$OUT/probe.txt" 2>&1
            done ;;
+    topo) for t in ${TOPOS:-simple nested2o nested2s refork reforks}; do
+            run "topo $t" 30 60 python -u tools/capture_topo.py $t >> "$OUT/topo.txt" 2>&1
+          done ;;
+    det) run det 60 200 python -u tools/det_check.py > "$OUT/det.txt" 2>&1 ;;
     newt) run newt 120 600 python -u -m pytest ${NEWT:-tests/test_gpu_capture.py tests/test_gpu_dp_order.py} -x -v \
             --timeout 600 --timeout-method thread > "$OUT/new_tests.log" 2>&1 ;;
     decprof) run decprof 120 300 rocprofv3 --kernel-trace --stats -d "$OUT/dk" -o run --output-format csv -- \

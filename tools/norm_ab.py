@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import torch  # noqa: E402
 
-from v9_ab import graph_of, time_graph, ops  # noqa: E402
+from gemm_ab import graph_of, time_graph, ops  # noqa: E402
 from tt2._lib import ACT_TANH  # noqa: E402
 
 

@@ -128,13 +128,36 @@ __global__ void embed_fwd_kernel(const int64_t* ids, const T* table, T* out, int
     out[i] = (id >= 0 && id < V) ? table[id * C + c] : from_f32<T>(0.f);
   }
 }
+
+// Gather form, deterministic (no atomics): workgroup (v, column block) writes table row v's
+// gradient = sum over the rows m with ids[m] == v of dout[m], added in increasing m (the same
+// bits every run, whatever the collisions).  Each wave walks the ids 64 at a time; a ballot
+// gives the matching rows of the slice in order; every lane adds its column pair of each.
+// Rows == pad_idx (and out-of-range ids) get no gradient; the row is written, not accumulated.
 template <typename T>
-__global__ void embed_bwd_kernel(const int64_t* ids, const T* dout, float* dtable, int M, int C, int V, int pad_idx) {
-  const int64_t total = (int64_t)M * C;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < total; i += (int64_t)gridDim.x * NT) {
-    const int m = (int)(i / C), c = (int)(i % C);
-    const int64_t id = ids[m];
-    if (id >= 0 && id < V && id != pad_idx) atomicAdd(&dtable[id * C + c], to_f32(dout[i]));
+__global__ __launch_bounds__(NT) void embed_bwd_kernel(const int64_t* ids, const T* dout, float* dtable, int M,
+                                                       int C, int V, int pad_idx) {
+  const int v = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.y * (2 * NT) + 2 * (w * 64 + lane);   // this lane's column pair
+  float a0 = 0.f, a1 = 0.f;
+  if (v != pad_idx) {
+    for (int base = 0; base < M; base += 64) {
+      const int m = base + lane;
+      const bool hit = m < M && ids[m] == (int64_t)v;
+      uint64_t mask = __ballot(hit);
+      while (mask) {
+        const int r = base + __builtin_ctzll(mask);
+        mask &= mask - 1;
+        if (c < C) {
+          a0 += to_f32(dout[(int64_t)r * C + c]);
+          if (c + 1 < C) a1 += to_f32(dout[(int64_t)r * C + c + 1]);
+        }
+      }
+    }
+  }
+  if (c < C) {
+    dtable[(int64_t)v * C + c] = a0;
+    if (c + 1 < C) dtable[(int64_t)v * C + c + 1] = a1;
   }
 }
 
@@ -608,14 +631,13 @@ extern "C" int tt2_embedding_fwd(const int64_t* ids, const void* table, void* ou
 
 extern "C" int tt2_embedding_bwd(const int64_t* ids, const void* dout, float* dtable, int m, int c, int vocab,
                                  int pad_idx, int dtype, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(dtable, 0, (size_t)vocab * c * sizeof(float), s);
-  if (e != hipSuccess) return tt2_check_launch(e, "tt2_embedding_bwd memset");
-  const int g = grid_for((int64_t)m * c);
+  if (vocab <= 0 || c <= 0) return TT2_OK;
+  const dim3 g(vocab, (c + 2 * NT - 1) / (2 * NT));   // every table row written: no memset
   if (dtype == TT2_DT_BF16)
-    hipLaunchKernelGGL(embed_bwd_kernel<bf16>, dim3(g), dim3(NT), 0, s, ids, (const bf16*)dout, dtable, m, c, vocab,
+    hipLaunchKernelGGL(embed_bwd_kernel<bf16>, g, dim3(NT), 0, s, ids, (const bf16*)dout, dtable, m, c, vocab,
                        pad_idx);
   else
-    hipLaunchKernelGGL(embed_bwd_kernel<float>, dim3(g), dim3(NT), 0, s, ids, (const float*)dout, dtable, m, c,
+    hipLaunchKernelGGL(embed_bwd_kernel<float>, g, dim3(NT), 0, s, ids, (const float*)dout, dtable, m, c,
                        vocab, pad_idx);
   return tt2_check_launch(hipGetLastError(), "tt2_embedding_bwd");
 }

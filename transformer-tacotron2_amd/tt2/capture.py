@@ -17,12 +17,20 @@ back into the capture's origin stream before the capture ends.  ``StepCapture`` 
 from __future__ import annotations
 
 import ctypes as C
+import os
+import sys
 
 import torch
 
 from . import _lib
 
 JOIN_NAMES = {0: "not captured", 1: "joined", 2: "UNJOINED", 3: "invalidated"}
+_TRACE = os.environ.get("TT2_CAPTURE_TRACE") == "1"   # dev: print each stage of a capture's end
+
+
+def _trace(*a):
+    if _TRACE:
+        print("[capture]", *a, file=sys.stderr, flush=True)
 
 
 class CaptureError(RuntimeError):
@@ -61,31 +69,39 @@ class StepCapture:
 
     def end(self):
         """End the capture after checking every registered stream is joined."""
+        _trace("join check", {k: str(v) for k, v in self._streams().items()})
         st = joined_status(self.origin, self._streams())
+        _trace("join status", st)
         bad = {k: JOIN_NAMES[v] for k, v in st.items() if v >= 2}
         if bad:
             self.abort()
             raise CaptureError(f"graph capture: streams not joined into the origin before capture end: {bad}")
-        self.graph.capture_end()
+        _trace("capture_end")
+        with torch.cuda.stream(self.origin):
+            self.graph.capture_end()
+        _trace("capture ended")
 
     def abort(self):
         """Join whatever takes part in the capture, end it and discard the graph (errors of the
         teardown itself are swallowed: the caller re-raises the original one)."""
-        try:
-            st = joined_status(self.origin, self._streams())
-            for k, s in self._streams().items():
-                if st.get(k) in (1, 2):
-                    self.origin.wait_stream(s)
-        except Exception:   # noqa: BLE001 - best effort: the capture must still be ended
-            pass
-        try:
-            self.graph.capture_end()
-        except Exception:   # noqa: BLE001
-            pass
-        try:
-            self.graph.reset()
-        except Exception:   # noqa: BLE001
-            pass
+        # torch ends a capture only on the stream it began on: make the origin current (the
+        # caller may already have left its stream context)
+        with torch.cuda.stream(self.origin):
+            try:
+                st = joined_status(self.origin, self._streams())
+                for k, s in self._streams().items():
+                    if st.get(k) in (1, 2):
+                        self.origin.wait_stream(s)
+            except Exception:   # noqa: BLE001 - best effort: the capture must still be ended
+                pass
+            try:
+                self.graph.capture_end()
+            except Exception:   # noqa: BLE001
+                pass
+            try:
+                self.graph.reset()
+            except Exception:   # noqa: BLE001
+                pass
 
     def __enter__(self):
         self._ctx = torch.cuda.stream(self.origin)

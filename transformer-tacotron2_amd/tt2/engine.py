@@ -216,6 +216,7 @@ class TTSEngine:
         # ... and each layer's last one in the layer's grouped weight-gradient reduce launch
         self.ln_fin_in_reduce = os.environ.get("TT2_LN_FIN_REDUCE", "1") != "0"
         self._wq = None   # weight-gradient requests queued for one grouped launch (see _defer_wgrads)
+        self._in_scope = False   # between _defer_wgrads and _flush_wgrads (a layer's group)
         self.wflip_batch = os.environ.get("TT2_WFLIP_BATCH", "1") != "0"
         # bf16 backward: every weight-gradient GEMM (and the DP hook of its bucket) runs on a side
         # stream that starts with the encoder backward, whose small latency-bound launches leave
@@ -233,6 +234,10 @@ class TTSEngine:
         self._norm_pending = None   # (ranges, computed on the side stream) of the last overlapped backward
         self.side_split = int(os.environ.get("TT2_SIDE_SPLIT", "1"))
         self.side_groups = int(os.environ.get("TT2_SIDE_WG", "0"))
+        # ... for the jobs issued while the decoder backward runs (side_start >= 0): the 200-tile
+        # N = 512 dgrads there leave 56 CUs idle, which a capped side grid can fill
+        self.side_groups_dec = int(os.environ.get("TT2_SIDE_WG_DEC", "0"))
+        self._side_cap = 0
         self.side_start = int(os.environ.get("TT2_SIDE_START", "-1"))   # decoder layer whose backward starts it
         self.enc_overlap = int(os.environ.get("TT2_ENC_OVERLAP", "1"))   # see forward()
         # ... also with SyncBatchNorm (the encoder pre-net's exchanges then fork the comm stream
@@ -347,10 +352,19 @@ class TTSEngine:
         backward every v7-eligible request is queued for the side stream (now=True: not)."""
         if (self._wq is not None or (self._jobs is not None and not now)) and _wide(dy.dtype, b_conv, n_out, n_out,
                                                                                      n_in):
-            if self._wq is None:
-                self._wq = []
-            self._wq.append(dict(a=dy, b=x, c=gw, m=n_out, n=n_in, k=m, lda=ldy or n_out, ldb=ldx or n_in, ldc=n_in,
-                                 trans_a=True, trans_b=True, b_conv=b_conv, a_ksum=gb))
+            if not self._in_scope:
+                # a request the in-place schedule launches on its own (outside a layer's group):
+                # queued as that same launch (same plan, same split-K factor), so the overlapped
+                # schedule sums every weight gradient in the same order (bit-identical)
+                req = {"direct": dict(a=dy, b=x, c=gw, m=n_out, n=n_in, k=m, lda=ldy or n_out, ldb=ldx or n_in,
+                                      ldc=n_in, trans_a=True, trans_b=True, b_conv=b_conv, a_ksum=gb,
+                                      splits=auto_splits(n_out, n_in, m, True))}
+                if self._wq is None:
+                    self._wq = []
+            else:
+                req = dict(a=dy, b=x, c=gw, m=n_out, n=n_in, k=m, lda=ldy or n_out, ldb=ldx or n_in, ldc=n_in,
+                           trans_a=True, trans_b=True, b_conv=b_conv, a_ksum=gb)
+            self._wq.append(req)
             return
         # the fused path rides on the LDS-DMA kernel: bf16 with 8-aligned M and N
         fused = gb is not None and dy.dtype == torch.bfloat16 and n_out % 8 == 0 and n_in % 8 == 0
@@ -397,6 +411,7 @@ class TTSEngine:
         if self._wq and self._jobs is not None:   # overlapped: earlier queued requests keep their order
             self._push_job(self._wq)
         self._wq = []
+        self._in_scope = True
 
     def _flush_wgrads(self, fin=None):
         """Launch the queued weight gradients as grouped v7 GEMMs (<= 8 per launch), one
@@ -404,6 +419,7 @@ class TTSEngine:
         layer's last (deferred) LayerNorm backward, finalized in the first group's reduce
         launch instead of a launch of its own."""
         q, self._wq = self._wq or [], None
+        self._in_scope = False
         if self._jobs is not None:
             self._push_job(q, fin)
             return
@@ -412,6 +428,10 @@ class TTSEngine:
     def _launch_wgrads(self, q, fin, ws, side=False):
         if not q and fin is not None:
             ops.layernorm_bwd_finalize(fin)
+        for p in q:
+            if "direct" in p:
+                ops.gemm(p["direct"].pop("a"), p["direct"].pop("b"), p["direct"].pop("c"), ws=ws, **p["direct"])
+        q = [p for p in q if "direct" not in p]
         for i in range(0, len(q), 8):
             grp = q[i:i + 8]
             tiles = sum(((p["m"] + 255) // 256) * ((p["n"] + 127) // 128) for p in grp)
@@ -420,7 +440,7 @@ class TTSEngine:
             if side:   # beside the encoder backward: shorter items, a capped grid
                 sp = max(1, min(16 * self.side_split, sp * self.side_split, kmin // 256))
             ops.gemm_grouped([dict(p, splits=sp) for p in grp], ws=ws, fin=fin if i == 0 else None,
-                             max_groups=self.side_groups if side else 0)
+                             max_groups=self._side_cap if side else 0)
 
     # ------------------------------------------------------------ overlapped weight gradients
     # A job = queued weight-gradient requests (+ a deferred LayerNorm finalize, + the DP hooks
@@ -538,13 +558,24 @@ class TTSEngine:
             dec = self._decoder_steps(A)
             enc_r = self._enc_param_ranges() if parts is not None else []
 
+            # SyncBatchNorm: the pre-net's exchanges stay on the main stream (the capture's
+            # origin).  Forked from the side stream, the comm stream would have to be joined
+            # back into the side stream, and hipStreamEndCapture (ROCm 7.0 runtime in torch)
+            # segfaults on any stream joined into a stream other than the origin
+            # (tools/capture_topo.py nested2s).  The decoder's first block
+            # then overlaps the encoder layers instead of the pre-net: the chain is the same.
+            pre_main = self.bn_sync is not None
+            enc_r_side = [] if pre_main else enc_r   # with the pre-net on main, its update goes there
+
             def encoder():
                 ws, self.ws = self.ws, self._side_ws
                 try:
                     with torch.cuda.stream(side):
-                        for lo, hi in enc_r:   # the encoder's parameters first
+                        for lo, hi in enc_r_side:   # the encoder's parameters first
                             self._adam(lo, hi, parts, gated=True)
-                        self.forward_encoder(A)
+                        if not pre_main:
+                            self.forward_encoder_prenet(A)
+                        self.forward_encoder_layers(A)
                 finally:
                     self.ws = ws
 
@@ -556,6 +587,11 @@ class TTSEngine:
                     if a > lo:
                         self._adam(lo, a, parts, gated=True)
                     lo = b
+            if pre_main:
+                for lo, hi in enc_r:   # the encoder's deferred update before the pre-net reads it
+                    self._adam(lo, hi, parts, gated=True)
+                self.forward_encoder_prenet(A)
+                side.wait_stream(main)
             if self.enc_overlap == 1:
                 encoder()
                 rest_adam()
@@ -587,6 +623,11 @@ class TTSEngine:
     def forward_encoder(self, A: Arena):
         """Encoder pre-net + layers, then the K/V projection of the memory for
         all decoder layers (A["mkv"])."""
+        self.forward_encoder_prenet(A)
+        self.forward_encoder_layers(A)
+
+    def forward_encoder_prenet(self, A: Arena):
+        """Embedding, 3 x (conv + BatchNorm + ReLU + dropout), projection, scaled PE -> A["ex0"]."""
         c = self.cfg
         B, Tx, Me = A.B, A.Tx, A.Me
         d, F, H, K = c.d_model, c.d_ffn, c.n_heads, c.enc_conv_kernel
@@ -608,6 +649,13 @@ class TTSEngine:
         self._lin(x, self.W("enc.proj.w"), A["eproj"], Me, d, d, bias=self.P("enc.proj.b"))
         ops.posenc_fwd(A["eproj"], self.P("enc.alpha"), self.pe, A["ex0"], Me, Tx,
                        drop=self.drop(SITE_ENC_PE, c.dropout))
+
+    def forward_encoder_layers(self, A: Arena):
+        """The encoder layers on A["ex0"], then the memory's K/V projection (A["mkv"])."""
+        c = self.cfg
+        B, Tx, Me = A.B, A.Tx, A.Me
+        d, F, H = c.d_model, c.d_ffn, c.n_heads
+        scale = 1.0 / math.sqrt(c.head_dim)
         x = A["ex0"]
         # ---------------- encoder layers
         for l in range(c.n_enc):
@@ -744,6 +792,7 @@ class TTSEngine:
         ov = self.wgrad_overlap and cd == torch.bfloat16
         self._norm_pending = None
         self._jobs = self._wq = None   # (a backward that raised leaves no queue behind)
+        self._in_scope = False
         self._norm_begin(side=ov and self.grad_ready_hook is None)
         if ov:
             self._ov_begin()
@@ -804,6 +853,7 @@ class TTSEngine:
         mkv = A["mkv"]
         kvld = c.n_dec * 2 * d
         g_mkv = A["g_mkv"]
+        self._side_cap = self.side_groups_dec or self.side_groups   # jobs pumped beside the decoder backward
         for l in reversed(range(c.n_dec)):
             p, base = f"dec{l}.", SITE_DEC_LAYER + 4 * l
             if ov and l == self.side_start and not self._side_live:
@@ -891,6 +941,7 @@ class TTSEngine:
         self._dgrad(g_mkv, self.W("dec.kv.w"), gxe, Me, d, kvld)
         if ov and not self._side_live:   # the weight gradients queued so far run beside the encoder backward
             self._start_side()
+        self._side_cap = self.side_groups
         # ---------------- encoder layers
         for l in reversed(range(c.n_enc)):
             p, base = f"enc{l}.", SITE_ENC_LAYER + 4 * l

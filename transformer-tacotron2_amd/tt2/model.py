@@ -208,13 +208,33 @@ class TransformerTTS(nn.Module):
         return self.engine.lay.n_params()
 
     # ------------------------------------------------------------ forward / loss / backward
+    def input_buffers(self, B: int, Tx: int, Ty: int):
+        """The step's own input tensors for shape (B, Tx, Ty): text [B, Tx] int64, text_len [B]
+        int32, mel [B, Ty, 80] f32, mel_len [B] int32 (the arena's, which the kernels read).  A
+        train_step / captured run handed exactly these tensors reads them in place, with no staging
+        copies in front of the step (the static-input pattern of graph replay: a data loader
+        writes the next batch into them, e.g. by non_blocking copies on a side stream)."""
+        A = self.engine.arena(B, Tx, Ty)
+        return A["text"].view(B, Tx), A["text_len"], A["mel"], A["mel_len"]
+
+    @staticmethod
+    def _is_arena_input(A: Arena, text, text_len, mel, mel_len) -> bool:
+        return (text.data_ptr() == A["text"].data_ptr() and text_len.data_ptr() == A["text_len"].data_ptr()
+                and mel.data_ptr() == A["mel"].data_ptr() and mel_len.data_ptr() == A["mel_len"].data_ptr()
+                and text.dtype == torch.int64 and text_len.dtype == mel_len.dtype == torch.int32
+                and mel.dtype == torch.float32)
+
+    def _stage_into(self, A: Arena, text, text_len, mel, mel_len):
+        if not self._is_arena_input(A, text, text_len, mel, mel_len):
+            dev = self.engine.dev
+            self.engine.stage_inputs(A, text.to(dev), text_len.to(dev, torch.int32), mel.to(dev, torch.float32),
+                                     mel_len.to(dev, torch.int32))
+
     def _stage(self, text, text_len, mel, mel_len) -> Arena:
         B, Tx = text.shape
         Ty = mel.shape[1]
         A = self.engine.arena(B, Tx, Ty)
-        dev = self.engine.dev
-        self.engine.stage_inputs(A, text.to(dev), text_len.to(dev, torch.int32), mel.to(dev, torch.float32),
-                                 mel_len.to(dev, torch.int32))
+        self._stage_into(A, text, text_len, mel, mel_len)
         return A
 
     def _run_forward(self, text, text_len, mel, mel_len) -> Arena:
@@ -498,7 +518,7 @@ class TransformerTTS(nn.Module):
         def run(text, text_len, mel, mel_len):
             if self.metrics is not None:
                 self.metrics.begin()
-            e.stage_inputs(A, text, text_len.to(torch.int32), mel, mel_len.to(torch.int32))
+            self._stage_into(A, text, text_len, mel, mel_len)
             for g, idx in segs:
                 g.replay()
                 if idx:
@@ -560,7 +580,7 @@ class TransformerTTS(nn.Module):
         def run(text, text_len, mel, mel_len):
             if self.metrics is not None:
                 self.metrics.begin()
-            e.stage_inputs(A, text, text_len.to(torch.int32), mel, mel_len.to(torch.int32))
+            self._stage_into(A, text, text_len, mel, mel_len)
             g.replay()
             for k in e.nbt:
                 e.nbt[k] += 1
