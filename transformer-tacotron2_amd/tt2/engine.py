@@ -236,9 +236,12 @@ class TTSEngine:
         self.side_groups = int(os.environ.get("TT2_SIDE_WG", "0"))
         # ... for the jobs issued while the decoder backward runs (side_start >= 0): the 200-tile
         # N = 512 dgrads there leave 56 CUs idle, which a capped side grid can fill
-        self.side_groups_dec = int(os.environ.get("TT2_SIDE_WG_DEC", "0"))
+        self.side_groups_dec = int(os.environ.get("TT2_SIDE_WG_DEC", "128"))
         self._side_cap = 0
-        self.side_start = int(os.environ.get("TT2_SIDE_START", "-1"))   # decoder layer whose backward starts it
+        # the decoder layer whose backward starts the side stream (-1: the encoder backward).  Default:
+        # the first one (5), with the side grid capped at 128 work groups while the decoder backward
+        # runs (side_groups_dec): -0.8 % step time, same box, interleaved (gpurun_out/r05j, r05m)
+        self.side_start = int(os.environ.get("TT2_SIDE_START", "5"))
         self.enc_overlap = int(os.environ.get("TT2_ENC_OVERLAP", "1"))   # see forward()
         # ... also with SyncBatchNorm (the encoder pre-net's exchanges then fork the comm stream
         # from the side stream); TT2_ENC_OVERLAP_SYNCBN=0 keeps the encoder on the main stream there
