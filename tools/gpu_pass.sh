@@ -85,9 +85,9 @@ for s in $STEPS; do
               > "$OUT/phases.txt" 2>&1 ;;
     decab) for i in 1 2; do
              for lib in abl/${DECAB_OLD:-dec0}.so transformer-tacotron2_amd/tt2/libtt2.so; do
-               run "decab $lib" 90 200 env TT2_LIB=$lib python3 -u tools/decode_bench_only.py --no-longform \
+               run "decab $lib" 90 240 env TT2_LIB=$lib python3 -u tools/decode_bench_only.py \
                  > "$OUT/dec_run.json" 2> "$OUT/dec_run.err"
-               echo "$lib $(python -c "import json,sys;print(json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])['decode']['value'])" "$OUT/dec_run.json" 2>&1 | tail -1)" >> "$OUT/decab.txt"
+               echo "$lib $(python -c "import json,sys;d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1]);print(d['decode']['value'], d['longform']['value'])" "$OUT/dec_run.json" 2>&1 | tail -1)" >> "$OUT/decab.txt"
              done
            done ;;
     pmc) run pmc_f 120 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \

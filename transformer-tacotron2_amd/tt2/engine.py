@@ -431,9 +431,12 @@ class TTSEngine:
     def _launch_wgrads(self, q, fin, ws, side=False):
         if not q and fin is not None:
             ops.layernorm_bwd_finalize(fin)
-        for p in q:
-            if "direct" in p:
-                ops.gemm(p["direct"].pop("a"), p["direct"].pop("b"), p["direct"].pop("c"), ws=ws, **p["direct"])
+        # requests the in-place schedule launches one by one (v7, each with its own split-K factor):
+        # grouped launches with per-problem splits, which compute every problem's tiles and its
+        # split-K reduce the same way (bit-identical to the single launches), in fewer launches
+        direct = [p["direct"] for p in q if "direct" in p]
+        for i in range(0, len(direct), 8):
+            ops.gemm_grouped(direct[i:i + 8], ws=ws, max_groups=self._side_cap if side else 0)
         q = [p for p in q if "direct" not in p]
         for i in range(0, len(q), 8):
             grp = q[i:i + 8]
