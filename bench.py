@@ -33,7 +33,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(ROOT, "transformer-tacotron2_amd"))
+# TT2_PKG (dev): the directory holding the tt2 host package, for A/B of host-schedule versions
+sys.path.insert(0, os.environ.get("TT2_PKG") or os.path.join(ROOT, "transformer-tacotron2_amd"))
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402

@@ -115,6 +115,13 @@ for s in $STEPS; do
     topo) for t in ${TOPOS:-simple nested2o nested2s refork reforks}; do
             run "topo $t" 30 60 python -u tools/capture_topo.py $t >> "$OUT/topo.txt" 2>&1
           done ;;
+    pkgab) for i in 1 2 3; do   # host-schedule A/B: abl/pkg_<name>/tt2 (a copy of the package at an older commit)
+             for pk in abl/pkg_${PKGAB_OLD:-head} ""; do
+               run "pkgab $pk" 90 200 env TT2_PKG=$pk TT2_LIB=$PWD/transformer-tacotron2_amd/tt2/libtt2.so python -u \
+                 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-decode > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
+               echo "${pk:-current} $(lastms "$OUT/ab_run.json")" >> "$OUT/pkgab.txt"
+             done
+           done ;;
     det) run det 60 200 python -u tools/det_check.py > "$OUT/det.txt" 2>&1 ;;
     newt) run newt 120 600 python -u -m pytest ${NEWT:-tests/test_gpu_capture.py tests/test_gpu_dp_order.py} -x -v \
             --timeout 600 --timeout-method thread > "$OUT/new_tests.log" 2>&1 ;;

@@ -581,7 +581,7 @@ class TTSEngine:
                             self._adam(lo, hi, parts, gated=True)
                         if not pre_main:
                             self.forward_encoder_prenet(A)
-                        self.forward_encoder_layers(A)
+                        self.forward_encoder_layers(A, rest_kv_later=True)
                 finally:
                     self.ws = ws
 
@@ -606,9 +606,22 @@ class TTSEngine:
                 rest_adam()
                 next(dec)
                 encoder()
-            main.wait_stream(side)   # the memory K/V, before layer 0's cross-attention
+            if self.training and self.wflip_batch:
+                # the dgrad conv weights (tap-flipped) for the backward, on the main stream while it
+                # waits for the encoder (they depend on the weights only)
+                self._flip_conv_weights()
+                self._wflip_ready = True
+            main.wait_stream(side)   # layer 0's memory K/V, before layer 0's cross-attention
             if parts is not None:
                 ops.adam_gate(self.adam_gate, self.step_t)   # both halves of the deferred Adam have read it
+            ws, self.ws = self.ws, self._side_ws
+            try:
+                with torch.cuda.stream(side):   # layers 1..'s memory K/V beside decoder layer 0
+                    self.forward_memory_kv(A, 1)
+            finally:
+                self.ws = ws
+            next(dec)                # decoder layer 0 and layer 1's self-attention block
+            main.wait_stream(side)
             for _ in dec:
                 pass
         else:
@@ -656,8 +669,9 @@ class TTSEngine:
         ops.posenc_fwd(A["eproj"], self.P("enc.alpha"), self.pe, A["ex0"], Me, Tx,
                        drop=self.drop(SITE_ENC_PE, c.dropout))
 
-    def forward_encoder_layers(self, A: Arena):
-        """The encoder layers on A["ex0"], then the memory's K/V projection (A["mkv"])."""
+    def forward_encoder_layers(self, A: Arena, rest_kv_later: bool = False):
+        """The encoder layers on A["ex0"], then the memory's K/V projection (A["mkv"]); with
+        rest_kv_later only layer 0's part (the caller issues forward_memory_kv(A, 1))."""
         c = self.cfg
         B, Tx, Me = A.B, A.Tx, A.Me
         d, F, H = c.d_model, c.d_ffn, c.n_heads
@@ -680,9 +694,20 @@ class TTSEngine:
             ops.layernorm_fwd(h1, A[f"ef2{l}"], self.P(p + "ln2.g"), self.P(p + "ln2.b"), A[f"ex{l + 1}"],
                               A[f"eln2m{l}"], A[f"eln2r{l}"], Me, c.ln_eps, drop=self.drop(base + 2, c.dropout))
             x = A[f"ex{l + 1}"]
-        mem = x
-        # one GEMM projects the memory to K/V for all decoder layers
-        self._lin(mem, self.W("dec.kv.w"), A["mkv"], Me, c.n_dec * 2 * d, d, bias=self.P("dec.kv.b"))
+        self.forward_memory_kv(A, 0)
+        if not rest_kv_later:
+            self.forward_memory_kv(A, 1)
+
+    def forward_memory_kv(self, A: Arena, part: int):
+        """The memory's K/V projection for the decoder layers' cross-attention, as two GEMMs into
+        A["mkv"] [Me, n_dec * 1024]: part 0 = layer 0's K/V, which decoder layer 0 waits for;
+        part 1 = layers 1.., which the overlapped forward issues after layer 0 can start (it runs
+        beside the decoder's layer 0).  Every schedule uses the same two GEMMs (identical bits)."""
+        c = self.cfg
+        d, Me = c.d_model, A.Me
+        kvld, w, b = c.n_dec * 2 * d, self.W("dec.kv.w"), self.P("dec.kv.b")
+        lo, hi = (0, 2 * d) if part == 0 else (2 * d, kvld)
+        self._lin(A[f"ex{c.n_enc}"], w[lo:hi], A["mkv"][:, lo:], Me, hi - lo, d, bias=b[lo:hi], ldo=kvld)
 
     @ranged("tt2.decoder")
     def forward_decoder(self, A: Arena):
@@ -723,7 +748,7 @@ class TTSEngine:
             h1 = A[f"dh1{l}"]
             self._lin(h1, self.W(p + "cq.w"), A[f"dcq{l}"], Md, d, d, bias=self.P(p + "cq.b"))
             ko = 2 * d * l
-            if l == 0:
+            if l <= 1:
                 yield
             ops.attn_fwd(A[f"dcq{l}"], mkv[:, ko:], mkv[:, ko + d:], A[f"dcatt{l}"], A[f"dclse{l}"], d, kvld, kvld,
                          d, B, H, Ty, Tx, A["text_len"], False, scale)
@@ -805,7 +830,9 @@ class TTSEngine:
         # a weight-gradient dY buffer: per layer (`key`) when the side stream reads it later
         gbuf = (lambda name, key, shape=None: A.layer_buf(name, key, shape)) if ov else \
             (lambda name, key, shape=None: A[name] if shape is None else A[name].view(-1)[:math.prod(shape)].view(shape))
-        self._flip_conv_weights()
+        if not getattr(self, "_wflip_ready", False):   # (the overlapped forward flipped them)
+            self._flip_conv_weights()
+        self._wflip_ready = False
         # ---------------- post-net
         chans = postnet_channels(c)
         nl = c.postnet_layers
