@@ -129,36 +129,64 @@ __global__ void embed_fwd_kernel(const int64_t* ids, const T* table, T* out, int
   }
 }
 
-// Gather form, deterministic (no atomics): workgroup (v, column block) writes table row v's
-// gradient = sum over the rows m with ids[m] == v of dout[m], added in increasing m (the same
-// bits every run, whatever the collisions).  Each wave walks the ids 64 at a time; a ballot
-// gives the matching rows of the slice in order; every lane adds its column pair of each.
-// Rows == pad_idx (and out-of-range ids) get no gradient; the row is written, not accumulated.
+// Gather form, deterministic (no atomics): workgroup (v, column block of 512) writes table row
+// v's gradient = sum over the rows m with ids[m] == v of dout[m], added in increasing m (the same
+// bits every run, whatever the collisions).  The ids are taken in chunks of EB_CHUNK rows: each
+// of the 8 waves ballots its slice of the chunk, the matching rows are compacted into an LDS
+// list in row order (wave offsets from the per-wave counts), then every thread adds its column of
+// those rows with EB_UNROLL loads in flight.  Rows == pad_idx (and out-of-range ids) get no
+// gradient; every table row is written, not accumulated.
+constexpr int EB_NT = 512, EB_CHUNK = 4096, EB_UNROLL = 8;
 template <typename T>
-__global__ __launch_bounds__(NT) void embed_bwd_kernel(const int64_t* ids, const T* dout, float* dtable, int M,
-                                                       int C, int V, int pad_idx) {
+__global__ __launch_bounds__(EB_NT) void embed_bwd_kernel(const int64_t* ids, const T* dout, float* dtable, int M,
+                                                          int C, int V, int pad_idx) {
+  __shared__ int list[EB_CHUNK];
+  __shared__ int wcnt[EB_NT / 64];
   const int v = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.y * (2 * NT) + 2 * (w * 64 + lane);   // this lane's column pair
-  float a0 = 0.f, a1 = 0.f;
+  const int c = blockIdx.y * EB_NT + threadIdx.x;
+  constexpr int PERW = EB_CHUNK / (EB_NT / 64);   // rows per wave per chunk
+  float acc = 0.f;
   if (v != pad_idx) {
-    for (int base = 0; base < M; base += 64) {
-      const int m = base + lane;
-      const bool hit = m < M && ids[m] == (int64_t)v;
-      uint64_t mask = __ballot(hit);
-      while (mask) {
-        const int r = base + __builtin_ctzll(mask);
-        mask &= mask - 1;
-        if (c < C) {
-          a0 += to_f32(dout[(int64_t)r * C + c]);
-          if (c + 1 < C) a1 += to_f32(dout[(int64_t)r * C + c + 1]);
-        }
+    for (int base = 0; base < M; base += EB_CHUNK) {
+      const int r0 = base + w * PERW;
+      uint64_t masks[PERW / 64];
+      int n = 0;
+#pragma unroll
+      for (int i = 0; i < PERW / 64; ++i) {
+        const int m = r0 + 64 * i + lane;
+        masks[i] = __ballot(m < M && ids[m] == (int64_t)v);
+        n += __builtin_popcountll(masks[i]);
       }
+      if (lane == 0) wcnt[w] = n;
+      __syncthreads();
+      int off = 0, total = 0;
+#pragma unroll
+      for (int k = 0; k < EB_NT / 64; ++k) {
+        off += k < w ? wcnt[k] : 0;
+        total += wcnt[k];
+      }
+#pragma unroll
+      for (int i = 0; i < PERW / 64; ++i) {
+        const uint64_t below = lane ? (masks[i] & (~0ull >> (64 - lane))) : 0ull;
+        if ((masks[i] >> lane) & 1ull) list[off + __builtin_popcountll(below)] = r0 + 64 * i + lane;
+        off += __builtin_popcountll(masks[i]);
+      }
+      __syncthreads();
+      if (c < C) {
+        int i = 0;
+        for (; i + EB_UNROLL <= total; i += EB_UNROLL) {
+          float x[EB_UNROLL];
+#pragma unroll
+          for (int u = 0; u < EB_UNROLL; ++u) x[u] = to_f32(dout[(int64_t)list[i + u] * C + c]);
+#pragma unroll
+          for (int u = 0; u < EB_UNROLL; ++u) acc += x[u];
+        }
+        for (; i < total; ++i) acc += to_f32(dout[(int64_t)list[i] * C + c]);
+      }
+      __syncthreads();   // the list is rebuilt for the next chunk
     }
   }
-  if (c < C) {
-    dtable[(int64_t)v * C + c] = a0;
-    if (c + 1 < C) dtable[(int64_t)v * C + c + 1] = a1;
-  }
+  if (c < C) dtable[(int64_t)v * C + c] = acc;
 }
 
 // ------------------------------------------------------ positional encoding
@@ -632,12 +660,12 @@ extern "C" int tt2_embedding_fwd(const int64_t* ids, const void* table, void* ou
 extern "C" int tt2_embedding_bwd(const int64_t* ids, const void* dout, float* dtable, int m, int c, int vocab,
                                  int pad_idx, int dtype, hipStream_t s) {
   if (vocab <= 0 || c <= 0) return TT2_OK;
-  const dim3 g(vocab, (c + 2 * NT - 1) / (2 * NT));   // every table row written: no memset
+  const dim3 g(vocab, (c + EB_NT - 1) / EB_NT);   // every table row written: no memset
   if (dtype == TT2_DT_BF16)
-    hipLaunchKernelGGL(embed_bwd_kernel<bf16>, g, dim3(NT), 0, s, ids, (const bf16*)dout, dtable, m, c, vocab,
+    hipLaunchKernelGGL(embed_bwd_kernel<bf16>, g, dim3(EB_NT), 0, s, ids, (const bf16*)dout, dtable, m, c, vocab,
                        pad_idx);
   else
-    hipLaunchKernelGGL(embed_bwd_kernel<float>, g, dim3(NT), 0, s, ids, (const float*)dout, dtable, m, c,
+    hipLaunchKernelGGL(embed_bwd_kernel<float>, g, dim3(EB_NT), 0, s, ids, (const float*)dout, dtable, m, c,
                        vocab, pad_idx);
   return tt2_check_launch(hipGetLastError(), "tt2_embedding_bwd");
 }
