@@ -364,6 +364,12 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
         "replay_avg_launch_us": round(replay / n * 1e6, 2) if replay is not None else None,
         "all_gemms": {"launches": round(sum(v[0] for v in allg.values())), "ms_per_step": round(tot_t * 1e3, 3),
                       "tflops": round(tot_f / tot_t / 1e12, 1)},
+        # the four GEMM variants with the most in-step device time, same timing as above
+        "top_gemms": [{"kernel": (gemm_kernel_name(*k[1:4]).replace("gemm7_kernel", "gemm7g_kernel")
+                                  if k[0] == "gemm_grouped" else gemm_kernel_name(*k[1:4])),
+                       "launches": round(v[0]), "avg_launch_us": round(v[2] / v[0] * 1e6, 2),
+                       "frac": round(v[1] / v[2] / 1e12 / PEAK_BF16_TFLOPS, 4)}
+                      for k, v in sorted(allg.items(), key=lambda kv: -kv[1][2])[:4]],
     }
 
 
