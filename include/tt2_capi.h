@@ -122,7 +122,16 @@ typedef struct tt2_gemm_args {
   const float* emit_stop_bias;
   int32_t* emit_stop_len;
   float emit_stop_thr;
+  /* fused BatchNorm statistics: when col_stats != NULL, each 256-row chunk r of the stored
+   * (bf16) output C also leaves its column moments, col_stats[(2 r) * n + j] = mean and
+   * col_stats[(2 r + 1) * n + j] = sum over the chunk's rows of (C - mean)^2 (rows < m only;
+   * the last chunk holds m - 256 r rows), in the chunk layout tt2_batchnorm_fwd reads with
+   * stats_rows = TT2_GEMM_STATS_ROWS.  Only on the 256 x 128 LDS-image path: bf16 C, no split-K,
+   * n % 128 == 0 (tt2_gemm_plan 13 with the default epilogue); other requests fail with
+   * TT2_E_INVALID. */
+  float* col_stats;
 } tt2_gemm_args;
+#define TT2_GEMM_STATS_ROWS 256
 
 size_t tt2_gemm_workspace_size(const tt2_gemm_args* a);
 int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream);
@@ -417,6 +426,11 @@ typedef struct tt2_bn_args {
   /* SyncBatchNorm (the *_stats / *_apply phases below; ignored by tt2_batchnorm_fwd/bwd) */
   float* sync_buf;               /* tt2_batchnorm_sync_size bytes, 16-B aligned */
   int32_t sync_world, sync_rank;
+  /* training forward (tt2_batchnorm_fwd / _fwd_stats): stats_rows > 0 says the workspace already
+   * holds the column moments of y in chunks of stats_rows rows (tt2_gemm col_stats, stats_rows =
+   * TT2_GEMM_STATS_ROWS), so the statistics pass over y is skipped; tt2_batchnorm_workspace_size
+   * then gives that layout's size.  0: the pass runs (its own chunking). */
+  int32_t stats_rows;
 } tt2_bn_args;
 size_t tt2_batchnorm_workspace_size(const tt2_bn_args* a);
 int tt2_batchnorm_fwd(const tt2_bn_args* a, hipStream_t stream);

@@ -1,0 +1,91 @@
+"""BatchNorm statistics fused into the producing conv GEMM (tt2_gemm col_stats + tt2_bn_args
+stats_rows, GPU): the chunk moments against float64 of the stored bf16 output, the BatchNorm
+forward from them against the BatchNorm's own statistics pass, and the requests the fusion
+refuses (tests/test_gpu_norm.py covers the BatchNorm kernels themselves)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from tt2 import ops  # noqa: E402
+from tt2._lib import ACT_TANH, GEMM_STATS_ROWS, TT2Error  # noqa: E402
+
+
+def _conv(m, cin, cout, T, g):
+    """a post-net conv as the engine issues it: implicit im2col over T-frame utterances"""
+    K, pad = 5, 2
+    x = torch.randn(m, cin, generator=g).bfloat16().cuda()
+    w = (torch.randn(cout, K * cin, generator=g) / (K * cin) ** 0.5).bfloat16().cuda()
+    b = (0.1 * torch.randn(cout, generator=g)).cuda()
+    return x, w, b, (T, cin, pad), K * cin
+
+
+@pytest.mark.parametrize("m,cin,cout,T", [(12800, 512, 512, 800), (12800, 80, 512, 800), (3 * 96, 512, 256, 96),
+                                          (1000, 512, 128, 125)])
+def test_gemm_col_stats(m, cin, cout, T):
+    g = torch.Generator().manual_seed(m + cin)
+    x, w, b, conv, k = _conv(m, cin, cout, T, g)
+    y = torch.empty(m, cout, dtype=torch.bfloat16, device="cuda")
+    R = (m + GEMM_STATS_ROWS - 1) // GEMM_STATS_ROWS
+    st = torch.full((2 * R * cout,), float("nan"), device="cuda")
+    ops.gemm(x, w, y, m, cout, k, cin, k, cout, bias=b, a_conv=conv, col_stats=st)
+    y_ref = torch.empty_like(y)   # the same kernel without the statistics (variant 14: v7, LDS image;
+    ops.gemm(x, w, y_ref, m, cout, k, cin, k, cout, bias=b, a_conv=conv, variant=14)   # auto may take v8)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)          # the statistics do not change what is stored
+    yd = y.double().cpu()
+    st = st.view(R, 2, cout).double().cpu()
+    for r in range(R):
+        blk = yd[r * GEMM_STATS_ROWS:(r + 1) * GEMM_STATS_ROWS]
+        mu = blk.mean(0)
+        m2 = ((blk - mu) ** 2).sum(0)
+        assert torch.allclose(st[r, 0], mu, rtol=1e-5, atol=1e-6), (r, (st[r, 0] - mu).abs().max())
+        assert torch.allclose(st[r, 1], m2, rtol=1e-4, atol=1e-4 * blk.shape[0]), (r, (st[r, 1] - m2).abs().max())
+
+
+@pytest.mark.parametrize("m,T", [(12800, 800), (1000, 125)])
+def test_batchnorm_fwd_from_gemm_stats(m, T):
+    cin = cout = 512
+    g = torch.Generator().manual_seed(7 + m)
+    x, w, b, conv, k = _conv(m, cin, cout, T, g)
+    y = torch.empty(m, cout, dtype=torch.bfloat16, device="cuda")
+    R = (m + GEMM_STATS_ROWS - 1) // GEMM_STATS_ROWS
+    st = torch.empty(2 * R * cout, device="cuda")
+    ops.gemm(x, w, y, m, cout, k, cin, k, cout, bias=b, a_conv=conv, col_stats=st)
+    gamma = (1 + 0.1 * torch.randn(cout, generator=g)).cuda()
+    beta = (0.1 * torch.randn(cout, generator=g)).cuda()
+    seed = torch.tensor([5], dtype=torch.int32, device="cuda")
+    drop = ops.Drop(seed, 40, 0.5)
+    outs = []
+    for stats in ((st, GEMM_STATS_ROWS), None):
+        mean, rstd = torch.empty(cout, device="cuda"), torch.empty(cout, device="cuda")
+        rm, rv = torch.zeros(cout, device="cuda"), torch.ones(cout, device="cuda")
+        out = torch.empty_like(y)
+        ops.batchnorm_fwd(y, gamma, beta, mean, rstd, rm, rv, out, m, cout, ACT_TANH, True, drop=drop,
+                          ws=ops.Workspace(), stats=stats)
+        outs.append((mean, rstd, rm, rv, out))
+    torch.cuda.synchronize()
+    (mf, rf, rmf, rvf, of), (ms, rs, rms, rvs, os_) = outs
+    yd = y.double()
+    assert torch.allclose(mf.double(), yd.mean(0), rtol=1e-6, atol=1e-6)
+    assert torch.allclose(rf.double(), 1 / torch.sqrt(yd.var(0, unbiased=False) + 1e-5), rtol=1e-5)
+    for a, b_ in ((mf, ms), (rf, rs), (rmf, rms), (rvf, rvs)):
+        assert torch.allclose(a, b_, rtol=1e-5, atol=1e-7), (a - b_).abs().max()
+    # the same statistics to f32 rounding: the outputs (|out| < 2 after tanh and the 1 / (1 - p)
+    # dropout scale) agree to a bf16 step or two
+    assert (of.float() - os_.float()).abs().max().item() <= 2 ** -6
+
+
+def test_col_stats_refused():
+    g = torch.Generator().manual_seed(3)
+    m, cin, cout, T = 12800, 512, 512, 800
+    x, w, b, conv, k = _conv(m, cin, cout, T, g)
+    st = torch.empty(2 * 50 * cout, device="cuda")
+    with pytest.raises(TT2Error):   # split-K
+        ops.gemm(x, w, torch.empty(m, cout, dtype=torch.bfloat16, device="cuda"), m, cout, k, cin, k, cout,
+                 a_conv=conv, splits=2, col_stats=st, ws=ops.Workspace())
+    with pytest.raises(TT2Error):   # f32 C
+        ops.gemm(x, w, torch.empty(m, cout, device="cuda"), m, cout, k, cin, k, cout, a_conv=conv, col_stats=st)
+    with pytest.raises(TT2Error):   # n % 128
+        ops.gemm(x, w[:80], torch.empty(m, 80, dtype=torch.bfloat16, device="cuda"), m, 80, k, cin, k, 80,
+                 a_conv=conv, col_stats=st)

@@ -133,6 +133,7 @@ struct EpiParams {
   int vec;    // every row of C/res/gate/bias is 16-B aligned at 8-column boundaries
   float* ksum; float ksum_beta;   // fused row sums of op(A) over k (v2, M-contiguous A)
   int main_only;                  // split-K: skip the reduce launch (measurement hook)
+  float* cstats;                  // v7 LDS-image path: 256-row chunk column moments (tt2_gemm_args col_stats)
 };
 
 // fixed-order split-K slab reduce + epilogue (defined after epi_store8) and its grid size
@@ -1142,18 +1143,82 @@ TT2_DEV int g7_img_row(int nkt, int r) {
   return r < 192 ? (nkt % 3) * G7_STAGE + r * 256 : ((nkt + 1) % 3) * G7_STAGE + (r - 192) * 256;
 }
 
+TT2_DEV void bf16x8_unpack(const u32x4& v, float (&f)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = __uint_as_float(v[j] << 16);
+    f[2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
+  }
+}
+
 // whole-row store of the LDS C image (all 768 threads; 4 rows x 256 B per wave instruction).
 // Nontemporal: C streams out during the epilogue instead of sitting dirty in L2 until the
 // end-of-kernel write-back (the consumer kernel reads it from the Infinity Cache either way).
-TT2_DEV void g7_store_c(const G7Prob& P, const char* smem, int m0, int n0, int nkt) {
+// With E.cstats (a BatchNorm's statistics fused into the producing GEMM), the stored values'
+// column moments over the tile's rows ride along: every thread keeps one 8-column chunk
+// (768 % 16 == 0) and sums (v - k), (v - k)^2 over its rows with k = the tile's row 0 (the
+// statistics kernel's shift), the 4 lanes of a chunk in a wave combine by shuffles, the 12 waves
+// through the free ring stage, and 128 threads write the chunk's mean and M2 per column.
+TT2_DEV void g7_store_c(const G7Prob& P, char* smem, int m0, int n0, int nkt) {
   bf16* C = reinterpret_cast<bf16*>(P.E.c);
+  const bool st = P.E.cstats != nullptr;
+  const int c = threadIdx.x & 15;
+  float k[8], s1[8], s2[8];
+  if (st) {
+    bf16x8_unpack(*reinterpret_cast<const u32x4*>(smem + g7_img_row(nkt, 0) + (c << 4)), k);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  }
   for (int id = threadIdx.x; id < 256 * 16; id += G7_NT) {
-    const int r = id >> 4, c = id & 15, m = m0 + r, n = n0 + 8 * c;
+    const int r = id >> 4, m = m0 + r, n = n0 + 8 * c;
     if (m < P.M && n < P.N) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(smem + g7_img_row(nkt, r) + ((c ^ (r & 15)) << 4));
       u32x4* dst = reinterpret_cast<u32x4*>(C + (int64_t)m * P.E.ldc + n);
       __builtin_nontemporal_store(v, dst);
+      if (st) {
+        float f[8];
+        bf16x8_unpack(v, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = f[j] - k[j];
+          s1[j] += d;
+          s2[j] += d * d;
+        }
+      }
     }
+  }
+  if (!st) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {   // lanes c, c + 16, c + 32, c + 48 of the wave hold the same chunk
+    s1[j] += __shfl_xor(s1[j], 16);
+    s2[j] += __shfl_xor(s2[j], 16);
+    s1[j] += __shfl_xor(s1[j], 32);
+    s2[j] += __shfl_xor(s2[j], 32);
+  }
+  // the ring stage neither image part occupies (every K step's copies have landed)
+  float* red = reinterpret_cast<float*>(smem + ((nkt + 2) % 3) * G7_STAGE);   // [12 waves][128 cols][2]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(wave * 128 + 8 * c + j) * 2 + 0] = s1[j];
+      red[(wave * 128 + 8 * c + j) * 2 + 1] = s2[j];
+    }
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < 128 && n0 + t < P.N) {
+    float S1 = 0.f, S2 = 0.f;
+    for (int w = 0; w < G7_NT / 64; ++w) {
+      S1 += red[(w * 128 + t) * 2 + 0];
+      S2 += red[(w * 128 + t) * 2 + 1];
+    }
+    const float kt = __uint_as_float((uint32_t)*reinterpret_cast<const uint16_t*>(smem + g7_img_row(nkt, 0) +
+                                                                                  2 * t) << 16);
+    const float nr = (float)min(256, P.M - m0);
+    float* out = P.E.cstats + (int64_t)(m0 / 256) * 2 * P.N + n0 + t;
+    out[0] = kt + S1 / nr;
+    out[P.N] = fmaxf(S2 - S1 * S1 / nr, 0.f);
   }
 }
 
@@ -2115,6 +2180,7 @@ static int gemm_prep(const tt2_gemm_args* a, OpDesc& A, OpDesc& B, EpiParams& ep
   ep.ksum = a->a_ksum;
   ep.ksum_beta = a->a_ksum_beta;
   ep.main_only = a->main_only;
+  ep.cstats = a->col_stats;
   {
     // vectorised epilogue: rows of C / res / gate start 16-B aligned at every 8th column
     auto ok = [](const void* p, int64_t ld, int dt) {
@@ -2153,6 +2219,15 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
     b.kernel_variant = 13;
     plan = gemm_plan(&b);
   }
+  if (ep.cstats && plan != 13) {   // the fused column statistics exist on v7's LDS-image path only
+    tt2_gemm_args b = *a;
+    b.kernel_variant = 14;
+    plan = gemm_plan(&b);
+  }
+  if (ep.cstats && !(plan == 13 && g7_lds_epi(a->kernel_variant) && sp == 1 && a->dtype_out == TT2_BF16 && ep.vec &&
+                     a->n % 128 == 0 && (reinterpret_cast<uintptr_t>(a->col_stats) & 3) == 0))
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: col_stats needs the v7 LDS-image path (bf16 C, 16-B aligned "
+                                        "rows, no split-K, n % 128 == 0)");
   if (plan == 3) {   // skinny-M weight-streaming path (decode step)
     SkinnyFuse F{reinterpret_cast<const bf16*>(a->a_ln_branch), a->a_ln_gamma, a->a_ln_beta,
                  reinterpret_cast<bf16*>(a->a_ln_out), a->a_ln_eps, a->kv_cache, a->kv_t,
@@ -2255,6 +2330,7 @@ extern "C" int tt2_gemm_grouped_ex(const tt2_gemm_args* probs, int n, const tt2_
     if (gemm_plan(a) != 13)
       return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: every problem must take the v7 kernel (bf16, "
                                           "8-aligned inner dims, conv T, C >= 64, no decode fusions)");
+    if (a->col_stats) return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: no col_stats");
     if (ta < 0) { ta = a->trans_a; tb = a->trans_b; }
     if (a->trans_a != ta || a->trans_b != tb)
       return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: problems must share trans_a / trans_b");

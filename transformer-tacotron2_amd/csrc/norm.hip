@@ -755,7 +755,9 @@ extern "C" int tt2_ln_combine(const void* x, const float* part, int32_t splits, 
 }
 
 static int ln_bwd_blocks(int m) {
-  return min(256, (m + 15) / 16);   // at most one workgroup per CU, 16+ rows each
+  // at most one workgroup per CU, 16+ rows each (512 / 1024 / 128 work groups: 19.0-19.3 / 23.6 /
+  // 21.5 us against 17.9-18.2 us at 12800 x 512, tools/norm_ab.py, gpurun_out/r05hp)
+  return min(256, (m + 15) / 16);
 }
 
 static LnFin ln_fin_of(const tt2_ln_args* q) {
@@ -826,7 +828,8 @@ static BnArgs bn_args(const tt2_bn_args* p) {
   a.res_ld = p->res_ld > 0 ? p->res_ld : p->c;
   a.training = p->training;
   a.eps = p->eps; a.momentum = p->momentum;
-  a.rows_per = bn_rows_per(p->m);
+  // stats_rows > 0: the workspace already holds the chunk moments (tt2_gemm col_stats)
+  a.rows_per = p->stats_rows > 0 ? p->stats_rows : bn_rows_per(p->m);
   a.R = (p->m + a.rows_per - 1) / a.rows_per;
   a.drop = DropDesc{p->drop_seed, p->drop_site, p->drop_thr, p->drop_scale};
   a.W = 1;
@@ -835,7 +838,7 @@ static BnArgs bn_args(const tt2_bn_args* p) {
 }
 
 extern "C" size_t tt2_batchnorm_workspace_size(const tt2_bn_args* p) {
-  const int rp = bn_rows_per(p->m);
+  const int rp = p->stats_rows > 0 ? p->stats_rows : bn_rows_per(p->m);
   const size_t R = (p->m + rp - 1) / rp;
   return R * 2 * p->c * sizeof(float);
 }
@@ -858,7 +861,7 @@ extern "C" int tt2_batchnorm_fwd(const tt2_bn_args* p, hipStream_t s) {
     return TT2_E_INVALID;
   BnArgs a = bn_args(p);
   const bool bf = p->dtype == TT2_DT_BF16;
-  if (p->training) {
+  if (p->training && p->stats_rows <= 0) {
     if (bf) hipLaunchKernelGGL(bn_stats_kernel<bf16>, dim3(a.R), dim3(NT), 0, s, a);
     else hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(a.R), dim3(NT), 0, s, a);
   }
@@ -923,8 +926,10 @@ extern "C" int tt2_batchnorm_fwd_stats(const tt2_bn_args* p, hipStream_t s) {
                        "16-B aligned sync_buf, workspace and the tt2_batchnorm_fwd layout rules required"))
     return TT2_E_INVALID;
   const BnArgs a = bn_sync_args(p);
-  if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(bn_stats_kernel<bf16>, dim3(a.R), dim3(NT), 0, s, a);
-  else hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(a.R), dim3(NT), 0, s, a);
+  if (p->stats_rows <= 0) {
+    if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(bn_stats_kernel<bf16>, dim3(a.R), dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(a.R), dim3(NT), 0, s, a);
+  }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
   return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_fwd_stats");
 }

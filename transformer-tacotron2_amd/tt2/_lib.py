@@ -47,6 +47,7 @@ class GemmArgs(C.Structure):
         ("emit_mel", vp), ("emit_stop", vp), ("emit_prev", vp), ("emit_t", vp), ("emit_seed", vp),
         ("emit_done", vp), ("emit_nmels", i32), ("emit_tmax", i32),
         ("emit_stop_bias", vp), ("emit_stop_len", vp), ("emit_stop_thr", f32),
+        ("col_stats", vp),
     ]
 
 
@@ -172,6 +173,9 @@ class LnArgs(C.Structure):
     ]
 
 
+GEMM_STATS_ROWS = 256   # TT2_GEMM_STATS_ROWS: rows per chunk of tt2_gemm's fused column moments
+
+
 class BnArgs(C.Structure):
     _fields_ = [
         ("y", vp), ("dout", vp), ("res", vp), ("out", vp), ("dy", vp),
@@ -181,7 +185,7 @@ class BnArgs(C.Structure):
         ("m", i32), ("c", i32), ("act", i32), ("dtype", i32), ("out_dtype", i32), ("res_dtype", i32),
         ("dout_dtype", i32), ("training", i32), ("eps", f32), ("momentum", f32),
         ("drop_site", u32), ("drop_thr", u32), ("drop_scale", f32),
-        ("sync_buf", vp), ("sync_world", i32), ("sync_rank", i32),
+        ("sync_buf", vp), ("sync_world", i32), ("sync_rank", i32), ("stats_rows", i32),
     ]
 
 

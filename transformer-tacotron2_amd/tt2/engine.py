@@ -20,7 +20,7 @@ import os
 import torch
 
 from . import ops
-from ._lib import ACT_NONE, ACT_RELU, ACT_TANH
+from ._lib import ACT_NONE, ACT_RELU, ACT_TANH, GEMM_STATS_ROWS
 from .trace import ranged
 from .config import (SITE_DEC_FC1, SITE_DEC_FC2, SITE_DEC_LAYER, SITE_DEC_PE, SITE_ENC_CONV, SITE_ENC_LAYER,
                      SITE_ENC_PE, SITE_POSTNET, TTSConfig)
@@ -148,6 +148,8 @@ class Arena:
                 mk(f"pcv_o{i}", (Md, chans[i + 1]))
             mk(f"pcv_mean{i}", (chans[i + 1],), f32)
             mk(f"pcv_rstd{i}", (chans[i + 1],), f32)
+            # the conv GEMM's fused BatchNorm statistics (256-row chunk moments, bf16 training)
+            mk(f"pcv_part{i}", (2 * ((Md + GEMM_STATS_ROWS - 1) // GEMM_STATS_ROWS) * chans[i + 1],), f32)
         mk("mel_after", (Md, c.n_mels), f32)
         mk("loss", (4,), f32)
         # ---- gradient scratch
@@ -207,7 +209,8 @@ class TTSEngine:
                  seed: int = 0):
         self.cfg = c = cfg or TTSConfig()
         assert c.d_model == 512 and c.head_dim == 64, "kernels are built for d_model 512, head_dim 64"
-        self._heads_pad = None   # bf16 backward: heads GEMMs padded to 88 rows (see backward)
+        self._heads_pad = None   # bf16: heads GEMMs padded to 88 rows (_pad_heads_weights)
+        self._heads_pad_fresh = False
         self.pad_heads = True
         # backward: a LayerNorm's column-sum finalize rides in the next LayerNorm's launch
         # (two dedicated partials buffers alternate; see _ln_defer)
@@ -246,6 +249,8 @@ class TTSEngine:
         # ... also with SyncBatchNorm (the encoder pre-net's exchanges then fork the comm stream
         # from the side stream); TT2_ENC_OVERLAP_SYNCBN=0 keeps the encoder on the main stream there
         self.enc_overlap_syncbn = os.environ.get("TT2_ENC_OVERLAP_SYNCBN", "1") != "0"
+        # the post-net BatchNorms' statistics from their conv GEMMs' epilogues (_postnet_fwd)
+        self.bn_gemm_stats = os.environ.get("TT2_BN_GEMM_STATS", "1") != "0"
         # pipelined optimizer (opt-in: TransformerTTS.pipeline_optimizer): a step's Adam is
         # deferred to the start of the next forward, where the encoder's share runs on the side
         # stream ahead of the encoder and the rest on the main stream ahead of the decoder,
@@ -304,6 +309,7 @@ class TTSEngine:
         return self.slay.view(self.stats, name)
 
     def sync_shadow(self):
+        self._heads_pad_fresh = False
         if self.shadow is not None:
             self.shadow.copy_(self.params)
 
@@ -331,9 +337,10 @@ class TTSEngine:
     # ------------------------------------------------------------ GEMM helpers
     def _lin(self, x, w, out, m, n, k, bias=None, act=ACT_NONE, drop=NO_DROP, res=None, ldx=None, ldo=None,
              a_conv=None, beta=0.0, **fuse):
+        # fused column statistics need the whole K in one tile (no split-K)
+        sp = 1 if "col_stats" in fuse else act_splits(m, n, k, _wide(x.dtype, a_conv, m, k) and not fuse)
         ops.gemm(x, w, out, m, n, k, ldx or k, k, ldo or n, bias=bias, res=res, ldr=ldo or n, act=act, drop=drop,
-                 a_conv=a_conv, beta=beta, ws=self.ws,
-                 splits=act_splits(m, n, k, _wide(x.dtype, a_conv, m, k) and not fuse), **fuse)
+                 a_conv=a_conv, beta=beta, ws=self.ws, splits=sp, **fuse)
 
     def _dgrad(self, dy, w, out, m, n_in, n_out, res=None, gate=None, gate_scale=1.0, ldy=None, ldo=None,
                a_conv=None, beta=0.0):
@@ -553,6 +560,7 @@ class TTSEngine:
         pre-net and layer 0's self-attention block, which do not need the memory (the step
         6.94 vs 7.03 ms measured; 1 issues the encoder first, 2 the decoder's part first: the
         same; 0 off)."""
+        self._heads_pad_fresh = False   # the padded head weights are copied again (_pad_heads_weights)
         parts = self._adam_parts if self.pipeline_opt else None   # pipelined: last step's Adam (gated)
         if self.enc_overlap and self.cd == torch.bfloat16 and (self.bn_sync is None or self.enc_overlap_syncbn):
             if self._side is None:
@@ -611,6 +619,7 @@ class TTSEngine:
                 # waits for the encoder (they depend on the weights only)
                 self._flip_conv_weights()
                 self._wflip_ready = True
+            self._pad_heads_weights()   # (also while the main stream waits for the encoder)
             main.wait_stream(side)   # layer 0's memory K/V, before layer 0's cross-attention
             if parts is not None:
                 ops.adam_gate(self.adam_gate, self.step_t)   # both halves of the deferred Adam have read it
@@ -764,7 +773,13 @@ class TTSEngine:
             x = A[f"dx{l + 1}"]
         # ---------------- heads (mel 80 + stop 1 in one GEMM, f32 out)
         nh = c.n_mels + 1
-        self._lin(x, self.W("heads.w"), A["heads"], Md, nh, d, bias=self.P("heads.b"), ldo=A.heads_ld)
+        if self._heads_padded():
+            # the head rows padded to 88 (zero rows and bias): 8-column chunks only, 14.0 vs 16.4 us
+            # (tools/heads_ab.py); output columns 81..87 are zero, the buffer's padding anyway
+            _, _, w_p, b_p = self._pad_heads_weights()
+            self._lin(x, w_p, A["heads"], Md, w_p.shape[0], d, bias=b_p, ldo=A.heads_ld)
+        else:
+            self._lin(x, self.W("heads.w"), A["heads"], Md, nh, d, bias=self.P("heads.b"), ldo=A.heads_ld)
         # ---------------- post-net
         ops.cast2d(A["heads"], A.heads_ld, A["pin"], c.n_mels, Md, c.n_mels)
         self._postnet_fwd(A, A["pin"], A["heads"], A.heads_ld, Md, Ty, tr)
@@ -780,8 +795,12 @@ class TTSEngine:
         for i in range(nl):
             cin, cout = chans[i], chans[i + 1]
             y = A[f"pcv_y{i}"]
+            # training in bf16: the conv GEMM leaves the BatchNorm's column moments from its output
+            # tiles (v7 LDS image), so the statistics pass over y is skipped (TT2_BN_GEMM_STATS=0: not)
+            st = A[f"pcv_part{i}"] if (tr and self.bn_gemm_stats and self.cd == torch.bfloat16 and cout % 128 == 0
+                                       and _wide(self.cd, (Ty, cin, pad), Md, K * cin)) else None
             self._lin(x, self.W(f"post.conv{i}.w"), y, Md, cout, K * cin, bias=self.P(f"post.conv{i}.b"), ldx=cin,
-                      a_conv=(Ty, cin, pad))
+                      a_conv=(Ty, cin, pad), **({"col_stats": st} if st is not None else {}))
             last = i == nl - 1
             out = A["mel_after"] if last else A[f"pcv_o{i}"]
             ops.batchnorm_fwd(y, self.P(f"post.bn{i}.g"), self.P(f"post.bn{i}.b"), A[f"pcv_mean{i}"],
@@ -789,7 +808,8 @@ class TTSEngine:
                               ACT_NONE if last else ACT_TANH, tr,
                               drop=self.drop(SITE_POSTNET + i, c.postnet_dropout),
                               res=res if last else None, res_ld=res_ld, eps=c.bn_eps, momentum=c.bn_momentum,
-                              ws=self.ws, sync=self.bn_sync)
+                              ws=self.ws, sync=self.bn_sync,
+                              stats=(st, GEMM_STATS_ROWS) if st is not None else None)
             x = out
 
     # ------------------------------------------------------------ loss
@@ -867,16 +887,11 @@ class TTSEngine:
         if cd == torch.bfloat16 and self.pad_heads:
             # the 81 head rows padded to 88 (gh_cd columns 81.. are zero) so both products take
             # the LDS-DMA kernels instead of the register-staged one (odd inner dimension)
-            nhp = 88
-            if self._heads_pad is None:
-                self._heads_pad = (torch.zeros(nhp, d, dtype=torch.float32, device=self.dev),
-                                   torch.zeros(nhp, dtype=torch.float32, device=self.dev),
-                                   torch.zeros(nhp, d, dtype=cd, device=self.dev))
-            gw_p, gb_p, w_p = self._heads_pad
+            gw_p, gb_p, w_p, _ = self._pad_heads_weights()   # (this step's forward padded w_p)
+            nhp = w_p.shape[0]
             self._wgrad(A["gh_cd"], x_top, gw_p, nhp, d, Md, ldy=A.heads_ld, gb=gb_p, now=True)
             ops.cast2d(gw_p, d, self.G("heads.w"), d, nh, d)
             ops.cast2d(gb_p, nhp, self.G("heads.b"), nh, 1, nh)
-            ops.cast2d(self.W("heads.w"), d, w_p, d, nh, d)
             self._dgrad(A["gh_cd"], w_p, gx, Md, d, nhp, ldy=A.heads_ld)
         else:
             self._wgrad(A["gh_cd"], x_top, self.G("heads.w"), nh, d, Md, ldy=A.heads_ld, gb=self.G("heads.b"))
@@ -1104,6 +1119,7 @@ class TTSEngine:
         ops.step_bump(self.step_t, self.seed)
 
     def _adam(self, lo, hi, parts, gated: bool = False):
+        self._heads_pad_fresh = False
         o = self.opt
         sl = lambda t: t[lo:hi] if t is not None else None   # noqa: E731
         ops.adam_step(sl(self.params), sl(self.grads), sl(self.exp_avg), sl(self.exp_avg_sq), sl(self.shadow),
@@ -1122,6 +1138,27 @@ class TTSEngine:
     def drop_pending_update(self):
         """Forget a pending pipelined update (its gradients belong to replaced weights)."""
         self.adam_gate.zero_()
+
+    def _heads_padded(self) -> bool:
+        return self.cd == torch.bfloat16 and self.pad_heads
+
+    def _pad_heads_weights(self):
+        """bf16 with pad_heads: the mel + stop head's 81 rows as an 88-row weight / bias (rows 81..
+        zero), copied from the parameters once per forward (the backward's products reuse it; the
+        weights do not change in between).  Returns (grad w, grad b, w, b) padded buffers."""
+        if not self._heads_padded():
+            return None
+        c, d = self.cfg, self.cfg.d_model
+        nh, nhp = c.n_mels + 1, 88
+        if self._heads_pad is None:
+            z = lambda *s_, dt=torch.float32: torch.zeros(*s_, dtype=dt, device=self.dev)   # noqa: E731
+            self._heads_pad = (z(nhp, d), z(nhp), z(nhp, d, dt=self.cd), z(nhp))
+        if not self._heads_pad_fresh:   # cleared by forward() and by every parameter update
+            _, _, w_p, b_p = self._heads_pad
+            ops.cast2d(self.W("heads.w"), d, w_p, d, nh, d)
+            ops.cast2d(self.P("heads.b"), nh, b_p, nhp, 1, nh)
+            self._heads_pad_fresh = True
+        return self._heads_pad
 
     def _enc_param_ranges(self):
         """Flat ranges the encoder forward reads: the encoder's slots, and the memory K/V

@@ -66,7 +66,7 @@ def gemm_args(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bia
               gate=None, ldg=0, gate_scale=1.0, alpha=1.0, beta=0.0, act=0, drop: Drop = NO_DROP, splits=1,
               a_conv=None, b_conv=None, ws: Workspace | None = None, variant: int = 0, a_ksum=None,
               a_ksum_beta=0.0, a_ln=None, kv=None, pe=None, emit=None, main_only=False,
-              defer_ws: bool = False) -> GemmArgs:
+              defer_ws: bool = False, col_stats=None) -> GemmArgs:
     """Build the tt2_gemm_args of one request (see tt2_capi.h).  defer_ws: only size the
     split-K workspace (ws_bytes); the caller places it."""
     L = lib()
@@ -92,6 +92,7 @@ def gemm_args(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bia
     if b_conv is not None:
         g.b_conv_t, g.b_conv_c, g.b_conv_pad = b_conv
     g.kernel_variant = variant
+    g.col_stats = ptr(col_stats)
     g.a_ksum, g.a_ksum_beta = ptr(a_ksum), a_ksum_beta
     if a_ln is not None:
         br, gam, bet, out, eps = a_ln
@@ -124,7 +125,9 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, **kw):
     kv = (cache, t_ptr, col0, bstride, ld): also store columns >= col0 to the KV cache at step *t_ptr.
     pe = (table, alpha, t_ptr): add alpha * table[*t_ptr] to every output row (skinny path).
     emit = (mel_seq, stop_seq, prev, t_ptr, seed, done, n_mels, t_max): the decode frame emit
-    (see tt2_capi.h), which also advances *t_ptr."""
+    (see tt2_capi.h), which also advances *t_ptr.
+    col_stats (f32, 2 * ceil(m / 256) * n): the stored C's column moments per 256-row chunk
+    (mean, M2), for batchnorm_fwd(stats=(col_stats, GEMM_STATS_ROWS)); v7 LDS-image path only."""
     L = lib()
     g = gemm_args(a, b, c, m, n, k, lda, ldb, ldc, **kw)
     if PROBE is not None:
@@ -386,16 +389,25 @@ def _bn_sync_into(L, a, sync):
 
 
 def batchnorm_fwd(y, gamma, beta, mean, rstd, run_mean, run_var, out, m, c, act, training, drop: Drop = NO_DROP,
-                  res=None, res_ld=0, eps=1e-5, momentum=0.1, ws: Workspace | None = None, sync=None):
+                  res=None, res_ld=0, eps=1e-5, momentum=0.1, ws: Workspace | None = None, sync=None, stats=None):
     """sync (training only): SyncBatchNorm over the data-parallel ranks -- the statistics of
-    all ranks' rows (tt2_batchnorm_fwd_stats, exchange, tt2_batchnorm_fwd_apply)."""
+    all ranks' rows (tt2_batchnorm_fwd_stats, exchange, tt2_batchnorm_fwd_apply).
+    stats = (buf, rows): y's column moments are already in buf, chunks of `rows` rows (the
+    producing GEMM's col_stats), so the statistics pass over y is skipped (training only)."""
     L = lib()
     a = _bn(y, gamma, beta, mean, rstd, m, c, act, training, drop, eps, momentum, ws)
     a.run_mean, a.run_var = ptr(run_mean), ptr(run_var)
     a.out, a.out_dtype = out.data_ptr(), dt(out)
     a.res, a.res_dtype, a.res_ld = ptr(res), (dt(res) if res is not None else 0), res_ld
-    buf = (ws or _WS).get(L.tt2_batchnorm_workspace_size(C.byref(a)))
-    a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
+    if stats is not None and training:
+        sbuf, a.stats_rows = stats
+        need = L.tt2_batchnorm_workspace_size(C.byref(a))
+        if sbuf.dtype != torch.float32 or sbuf.numel() * 4 < need:
+            raise _lib.TT2Error(f"batchnorm_fwd: stats buffer needs {need} bytes of f32")
+        a.workspace, a.ws_bytes = sbuf.data_ptr(), sbuf.numel() * 4
+    else:
+        buf = (ws or _WS).get(L.tt2_batchnorm_workspace_size(C.byref(a)))
+        a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
     if sync is None or not training:
         check(L.tt2_batchnorm_fwd(C.byref(a), stream_ptr()), "tt2_batchnorm_fwd")
         return
