@@ -130,6 +130,13 @@ typedef struct tt2_gemm_args {
    * n % 128 == 0 (tt2_gemm_plan 13 with the default epilogue); other requests fail with
    * TT2_E_INVALID. */
   float* col_stats;
+  /* fused BatchNorm backward sums: when bn_bwd != NULL, C is that BatchNorm's dout (the gradient
+   * of its output: bn_bwd->y is its input, mean / rstd / gamma / beta / act / dropout as for
+   * tt2_batchnorm_bwd, c == n, m == m), and each 256-row chunk r of the stored (bf16) C leaves the
+   * column sums of dpre = dout * keep * act'(z) and of dpre * xhat in bn_bwd->workspace
+   * ([r][2][n], the layout tt2_batchnorm_bwd reads with stats_rows = TT2_GEMM_STATS_ROWS).  The
+   * tt2_bn_args struct is read during the call only.  Same path restrictions as col_stats. */
+  const struct tt2_bn_args* bn_bwd;
 } tt2_gemm_args;
 #define TT2_GEMM_STATS_ROWS 256
 
@@ -426,10 +433,11 @@ typedef struct tt2_bn_args {
   /* SyncBatchNorm (the *_stats / *_apply phases below; ignored by tt2_batchnorm_fwd/bwd) */
   float* sync_buf;               /* tt2_batchnorm_sync_size bytes, 16-B aligned */
   int32_t sync_world, sync_rank;
-  /* training forward (tt2_batchnorm_fwd / _fwd_stats): stats_rows > 0 says the workspace already
-   * holds the column moments of y in chunks of stats_rows rows (tt2_gemm col_stats, stats_rows =
-   * TT2_GEMM_STATS_ROWS), so the statistics pass over y is skipped; tt2_batchnorm_workspace_size
-   * then gives that layout's size.  0: the pass runs (its own chunking). */
+  /* stats_rows > 0 says the workspace already holds this pass's per-chunk column statistics in
+   * chunks of stats_rows rows, so the statistics pass over the rows is skipped: the training
+   * forward's moments of y (tt2_gemm col_stats) or the backward's sums (tt2_gemm bn_bwd; both
+   * with stats_rows = TT2_GEMM_STATS_ROWS); tt2_batchnorm_workspace_size then gives that layout's
+   * size.  0: the pass runs (its own chunking). */
   int32_t stats_rows;
 } tt2_bn_args;
 size_t tt2_batchnorm_workspace_size(const tt2_bn_args* a);

@@ -89,3 +89,49 @@ def test_col_stats_refused():
     with pytest.raises(TT2Error):   # n % 128
         ops.gemm(x, w[:80], torch.empty(m, 80, dtype=torch.bfloat16, device="cuda"), m, 80, k, cin, k, 80,
                  a_conv=conv, col_stats=st)
+
+
+@pytest.mark.parametrize("m,T,p", [(12800, 800, 0.5), (1000, 125, 0.0)])
+def test_batchnorm_bwd_from_gemm_sums(m, T, p):
+    """the post-net backward's pairing: the conv dgrad that produces a BatchNorm's dout also
+    leaves its column sums (tt2_gemm bn_bwd), and the BatchNorm backward skips its own pass"""
+    c = 512
+    g = torch.Generator().manual_seed(11 + m)
+    dyn, wf, _, conv, k = _conv(m, c, c, T, g)          # the next layer's dy and flipped weights
+    y = (torch.randn(m, c, generator=g) * 2 + 0.3).bfloat16().cuda()   # this layer's conv output
+    gamma = (1 + 0.1 * torch.randn(c, generator=g)).cuda()
+    beta = (0.1 * torch.randn(c, generator=g)).cuda()
+    mean = y.float().mean(0)
+    rstd = 1 / torch.sqrt(y.float().var(0, unbiased=False) + 1e-5)
+    seed = torch.tensor([9], dtype=torch.int32, device="cuda")
+    drop = ops.Drop(seed, 41, p)
+    R = (m + GEMM_STATS_ROWS - 1) // GEMM_STATS_ROWS
+    sums = torch.full((2 * R * c,), float("nan"), device="cuda")
+    bnb = ops.bn_bwd_args(y, gamma, beta, mean, rstd, m, c, ACT_TANH, drop, (sums, GEMM_STATS_ROWS))
+    dout = torch.empty(m, c, dtype=torch.bfloat16, device="cuda")
+    ops.gemm(dyn, wf, dout, m, c, k, c, k, c, a_conv=conv, bn_bwd=bnb)
+    dout_ref = torch.empty_like(dout)
+    ops.gemm(dyn, wf, dout_ref, m, c, k, c, k, c, a_conv=conv, variant=14)
+    res = []
+    for stats in ((sums, GEMM_STATS_ROWS), None):
+        dy = torch.empty_like(y)
+        dg, db = torch.empty(c, device="cuda"), torch.empty(c, device="cuda")
+        ops.batchnorm_bwd(y, dout, gamma, beta, mean, rstd, dy, dg, db, m, c, ACT_TANH, drop=drop,
+                          ws=ops.Workspace(), stats=stats)
+        res.append((dy, dg, db))
+    torch.cuda.synchronize()
+    assert torch.equal(dout, dout_ref)
+    # float64 column sums of the same per-element terms
+    keep = torch.ones(m, c, dtype=torch.float64)
+    if p > 0:
+        from tt2_oracle import dropout_keep
+        keep = torch.from_numpy(dropout_keep(9, 41, m * c, p)).view(m, c).double() / (1 - p)
+    xh = (y.double().cpu() - mean.double().cpu()) * rstd.double().cpu()
+    z = torch.tanh(xh * gamma.double().cpu() + beta.double().cpu())
+    dp = dout.double().cpu() * keep * (1 - z * z)
+    s = sums.view(R, 2, c).double().cpu().sum(0)
+    assert torch.allclose(s[0], dp.sum(0), rtol=1e-4, atol=1e-3), (s[0] - dp.sum(0)).abs().max()
+    assert torch.allclose(s[1], (dp * xh).sum(0), rtol=1e-4, atol=1e-3), (s[1] - (dp * xh).sum(0)).abs().max()
+    (dyf, dgf, dbf), (dys, dgs, dbs) = res
+    assert torch.allclose(dgf, dgs, rtol=1e-4, atol=1e-3) and torch.allclose(dbf, dbs, rtol=1e-4, atol=1e-3)
+    assert (dyf.float() - dys.float()).abs().max().item() <= 2e-2 * dys.float().abs().max().item()

@@ -134,6 +134,14 @@ struct EpiParams {
   float* ksum; float ksum_beta;   // fused row sums of op(A) over k (v2, M-contiguous A)
   int main_only;                  // split-K: skip the reduce launch (measurement hook)
   float* cstats;                  // v7 LDS-image path: 256-row chunk column moments (tt2_gemm_args col_stats)
+  // v7 LDS-image path: C is a BatchNorm backward's dout; its chunk sums of dpre, dpre * xhat go
+  // to bnb.part (tt2_gemm_args bn_bwd)
+  struct {
+    const bf16* y; const float* mean; const float* rstd; const float* gamma; const float* beta;
+    float* part;
+    DropDesc drop;
+    int act;
+  } bnb;
 };
 
 // fixed-order split-K slab reduce + epilogue (defined after epi_store8) and its grid size
@@ -1159,23 +1167,56 @@ TT2_DEV void bf16x8_unpack(const u32x4& v, float (&f)[8]) {
 // (768 % 16 == 0) and sums (v - k), (v - k)^2 over its rows with k = the tile's row 0 (the
 // statistics kernel's shift), the 4 lanes of a chunk in a wave combine by shuffles, the 12 waves
 // through the free ring stage, and 128 threads write the chunk's mean and M2 per column.
+// With E.bnb.part (the BatchNorm backward's statistics pass fused into the GEMM that produces its
+// dout), each thread sums, over the same rows and chunk, dpre = dout * keep * act'(z) and
+// dpre * xhat exactly as bn_bwd_stats_kernel forms them per element (its y rows are loaded
+// before the store loop, all in flight), then the same reduction writes plain chunk sums.
+// SM (compile time, so the plain kernels carry none of it): 0 store only, 1 col_stats, 2 bn_bwd sums.
+template <int SM>
 TT2_DEV void g7_store_c(const G7Prob& P, char* smem, int m0, int n0, int nkt) {
   bf16* C = reinterpret_cast<bf16*>(P.E.c);
-  const bool st = P.E.cstats != nullptr;
+  constexpr bool st = SM == 1, sb = SM == 2;
   const int c = threadIdx.x & 15;
   float k[8], s1[8], s2[8];
-  if (st) {
-    bf16x8_unpack(*reinterpret_cast<const u32x4*>(smem + g7_img_row(nkt, 0) + (c << 4)), k);
+  if (st) bf16x8_unpack(*reinterpret_cast<const u32x4*>(smem + g7_img_row(nkt, 0) + (c << 4)), k);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  constexpr int NR = (256 * 16 + G7_NT - 1) / G7_NT;   // rows per thread (6; the last only for some)
+  constexpr int YB = NR / 2;   // y rows in flight per batch (two batches: register pressure)
+  u32x4 yv[YB];
+  float mu[8], rs[8], ga[8], be[8];
+  uint32_t seed = 0;
+  auto load_y = [&](int i0) {
+#pragma unroll
+    for (int i = 0; i < YB; ++i) {
+      const int r = (threadIdx.x >> 4) + (G7_NT / 16) * (i0 + i), m = min(m0 + r, P.M - 1);
+      yv[i] = r < 256 ? *reinterpret_cast<const u32x4*>(P.E.bnb.y + (int64_t)m * P.N + n0 + 8 * c)
+                      : u32x4{0, 0, 0, 0};
+    }
+  };
+  if constexpr (sb) {
+    const int n = n0 + 8 * c;
+    load_y(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mu[j] = P.E.bnb.mean[n + j]; rs[j] = P.E.bnb.rstd[n + j];
+      ga[j] = P.E.bnb.gamma[n + j]; be[j] = P.E.bnb.beta[n + j];
+    }
+    seed = P.E.bnb.drop.thr ? *P.E.bnb.drop.seed : 0u;
   }
-  for (int id = threadIdx.x; id < 256 * 16; id += G7_NT) {
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    if constexpr (sb) {
+      if (i == YB) load_y(YB);
+    }
+    const int id = threadIdx.x + G7_NT * i;
+    if (id >= 256 * 16) break;
     const int r = id >> 4, m = m0 + r, n = n0 + 8 * c;
     if (m < P.M && n < P.N) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(smem + g7_img_row(nkt, r) + ((c ^ (r & 15)) << 4));
       u32x4* dst = reinterpret_cast<u32x4*>(C + (int64_t)m * P.E.ldc + n);
       __builtin_nontemporal_store(v, dst);
-      if (st) {
+      if constexpr (st) {
         float f[8];
         bf16x8_unpack(v, f);
 #pragma unroll
@@ -1185,9 +1226,27 @@ TT2_DEV void g7_store_c(const G7Prob& P, char* smem, int m0, int n0, int nkt) {
           s2[j] += d * d;
         }
       }
+      if constexpr (sb) {
+        float d[8], yf[8];
+        bf16x8_unpack(v, d);
+        bf16x8_unpack(yv[i % YB], yf);
+        const DropDesc& dd = P.E.bnb.drop;
+        const uint32_t bits = dd.thr ? drop_bits8(seed, dd.site, (uint32_t)((int64_t)m * P.N + n), dd.thr) : 0xFFu;
+        const float sc = dd.thr ? dd.scale : 1.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float keep = (bits >> j) & 1u ? sc : 0.f;
+          const float xh = (yf[j] - mu[j]) * rs[j];
+          const float z = act_f(P.E.bnb.act, xh * ga[j] + be[j]);
+          const float dp = d[j] * keep * act_grad_from_out(P.E.bnb.act, z);
+          s1[j] += dp;
+          s2[j] += dp * xh;
+        }
+      }
     }
   }
-  if (!st) return;
+  if constexpr (!st && !sb) return;
+  else {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {   // lanes c, c + 16, c + 32, c + 48 of the wave hold the same chunk
     s1[j] += __shfl_xor(s1[j], 16);
@@ -1215,10 +1274,17 @@ TT2_DEV void g7_store_c(const G7Prob& P, char* smem, int m0, int n0, int nkt) {
     }
     const float kt = __uint_as_float((uint32_t)*reinterpret_cast<const uint16_t*>(smem + g7_img_row(nkt, 0) +
                                                                                   2 * t) << 16);
-    const float nr = (float)min(256, P.M - m0);
-    float* out = P.E.cstats + (int64_t)(m0 / 256) * 2 * P.N + n0 + t;
-    out[0] = kt + S1 / nr;
-    out[P.N] = fmaxf(S2 - S1 * S1 / nr, 0.f);
+    if constexpr (st) {
+      const float nr = (float)min(256, P.M - m0);
+      float* out = P.E.cstats + (int64_t)(m0 / 256) * 2 * P.N + n0 + t;
+      out[0] = kt + S1 / nr;
+      out[P.N] = fmaxf(S2 - S1 * S1 / nr, 0.f);
+    } else {
+      float* out = P.E.bnb.part + (int64_t)(m0 / 256) * 2 * P.N + n0 + t;
+      out[0] = S1;
+      out[P.N] = S2;
+    }
+  }
   }
 }
 
@@ -1292,7 +1358,7 @@ TT2_DEV void g7_epi_fast(const EpiParams& E, const f32x4 (&acc)[4][4], const f32
   }
 }
 
-template <bool AK, bool BKC>
+template <bool AK, bool BKC, int SM = 0>
 TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem, unsigned long long* span) {
 #ifdef TT2_PHASE
   unsigned long long* srec = span ? span + TT2_SPAN_W * blockIdx.x : nullptr;
@@ -1353,7 +1419,7 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem, unsigned 
     }
     if (!P.lds_epi) return;
     __syncthreads();   // the MFMA waves' C image is in LDS
-    g7_store_c(P, smem, m0, n0, nkt);
+    g7_store_c<SM>(P, smem, m0, n0, nkt);
     return;
   }
 
@@ -1506,7 +1572,7 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem, unsigned 
     G7_STAMP(nkt, 1)
     __syncthreads();
     G7_STAMP(nkt, 2)
-    g7_store_c(P, smem, m0, n0, nkt);
+    g7_store_c<SM>(P, smem, m0, n0, nkt);
     G7_STAMP(nkt, 3)
     return;
   }
@@ -1556,14 +1622,14 @@ TT2_DEV int xcd_item(int bid, int n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
-template <bool AK, bool BKC>
+template <bool AK, bool BKC, int SM = 0>
 __global__ __launch_bounds__(G7_NT, 1) void gemm7_kernel(G7Prob P) {
   __shared__ __attribute__((aligned(1024))) char smem[G7_SMEM];
   __shared__ int span_done;
   G7_RT(0)
   span_begin(P.span, &span_done);
   const int u = xcd_item(blockIdx.x, P.items);
-  g7_item<AK, BKC>(P, u % (P.items / P.splits), u / (P.items / P.splits), smem, P.span);
+  g7_item<AK, BKC, SM>(P, u % (P.items / P.splits), u / (P.items / P.splits), smem, P.span);
   span_end(P.span, &span_done, G7_NT / 64);
   G7_RT(1)
 }
@@ -1650,10 +1716,19 @@ hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
   P.epi_fast = g7_fast_code(P, AK && BKC);
   ProbeScope ps(s, P.items);
   P.span = ps.span;
-  if (ps.ext())
-    hipExtLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, ps.e0, ps.e1, 0, P);
-  else
-    hipLaunchKernelGGL((gemm7_kernel<AK, BKC>), dim3(P.items), dim3(G7_NT), 0, s, P);
+  // fused BatchNorm statistics: own instantiations (the forward / dgrad conv layout only)
+  const int sm = E.cstats ? 1 : E.bnb.part ? 2 : 0;
+  auto go = [&](auto kern) {
+    if (ps.ext()) hipExtLaunchKernelGGL(kern, dim3(P.items), dim3(G7_NT), 0, s, ps.e0, ps.e1, 0, P);
+    else hipLaunchKernelGGL(kern, dim3(P.items), dim3(G7_NT), 0, s, P);
+  };
+  if constexpr (AK && BKC) {
+    if (sm == 1) go(gemm7_kernel<AK, BKC, 1>);
+    else if (sm == 2) go(gemm7_kernel<AK, BKC, 2>);
+    else go(gemm7_kernel<AK, BKC, 0>);
+  } else {
+    go(gemm7_kernel<AK, BKC, 0>);
+  }
   if (P.splits > 1 && !E.main_only)
     hipLaunchKernelGGL(gemm_splitk_reduce, dim3(splitk_blocks(M, N, E)), dim3(256), 0, s, ws, P.splits, E, M, N);
   return hipGetLastError();
@@ -2181,6 +2256,20 @@ static int gemm_prep(const tt2_gemm_args* a, OpDesc& A, OpDesc& B, EpiParams& ep
   ep.ksum_beta = a->a_ksum_beta;
   ep.main_only = a->main_only;
   ep.cstats = a->col_stats;
+  if (const tt2_bn_args* bn = a->bn_bwd) {
+    const int rp = TT2_GEMM_STATS_ROWS;
+    if (bn->dtype != TT2_DT_BF16 || bn->c != a->n || bn->m != a->m || !bn->y || !bn->mean || !bn->rstd ||
+        !bn->gamma || !bn->beta || !bn->workspace ||
+        bn->ws_bytes < (size_t)((a->m + rp - 1) / rp) * 2 * a->n * sizeof(float) || a->col_stats ||
+        (bn->drop_thr && !bn->drop_seed))
+      return tt2_set_error(TT2_E_INVALID, "tt2_gemm: bn_bwd needs a bf16 BatchNorm of this GEMM's m x n, its "
+                                          "y / mean / rstd / gamma / beta, a chunk-sums workspace, no col_stats");
+    ep.bnb.y = reinterpret_cast<const bf16*>(bn->y);
+    ep.bnb.mean = bn->mean; ep.bnb.rstd = bn->rstd; ep.bnb.gamma = bn->gamma; ep.bnb.beta = bn->beta;
+    ep.bnb.part = reinterpret_cast<float*>(bn->workspace);
+    ep.bnb.drop = DropDesc{bn->drop_seed, bn->drop_site, bn->drop_thr, bn->drop_scale};
+    ep.bnb.act = bn->act;
+  }
   {
     // vectorised epilogue: rows of C / res / gate start 16-B aligned at every 8th column
     auto ok = [](const void* p, int64_t ld, int dt) {
@@ -2219,15 +2308,16 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
     b.kernel_variant = 13;
     plan = gemm_plan(&b);
   }
-  if (ep.cstats && plan != 13) {   // the fused column statistics exist on v7's LDS-image path only
+  const bool fstats = ep.cstats || ep.bnb.part;
+  if (fstats && plan != 13) {   // the fused column statistics exist on v7's LDS-image path only
     tt2_gemm_args b = *a;
     b.kernel_variant = 14;
     plan = gemm_plan(&b);
   }
-  if (ep.cstats && !(plan == 13 && g7_lds_epi(a->kernel_variant) && sp == 1 && a->dtype_out == TT2_BF16 && ep.vec &&
+  if (fstats && !(plan == 13 && !a->trans_a && !a->trans_b && g7_lds_epi(a->kernel_variant) && sp == 1 && a->dtype_out == TT2_BF16 && ep.vec &&
                      a->n % 128 == 0 && (reinterpret_cast<uintptr_t>(a->col_stats) & 3) == 0))
-    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: col_stats needs the v7 LDS-image path (bf16 C, 16-B aligned "
-                                        "rows, no split-K, n % 128 == 0)");
+    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: col_stats / bn_bwd need the v7 LDS-image path (bf16 C, 16-B "
+                                        "aligned rows, no split-K, n % 128 == 0)");
   if (plan == 3) {   // skinny-M weight-streaming path (decode step)
     SkinnyFuse F{reinterpret_cast<const bf16*>(a->a_ln_branch), a->a_ln_gamma, a->a_ln_beta,
                  reinterpret_cast<bf16*>(a->a_ln_out), a->a_ln_eps, a->kv_cache, a->kv_t,
@@ -2330,7 +2420,7 @@ extern "C" int tt2_gemm_grouped_ex(const tt2_gemm_args* probs, int n, const tt2_
     if (gemm_plan(a) != 13)
       return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: every problem must take the v7 kernel (bf16, "
                                           "8-aligned inner dims, conv T, C >= 64, no decode fusions)");
-    if (a->col_stats) return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: no col_stats");
+    if (a->col_stats || a->bn_bwd) return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: no col_stats / bn_bwd");
     if (ta < 0) { ta = a->trans_a; tb = a->trans_b; }
     if (a->trans_a != ta || a->trans_b != tb)
       return tt2_set_error(TT2_E_INVALID, "tt2_gemm_grouped: problems must share trans_a / trans_b");

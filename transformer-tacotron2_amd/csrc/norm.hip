@@ -356,18 +356,7 @@ struct BnArgs {
   const float* inv_m;   // SyncBN backward apply: 1 / (sum of the ranks' rows), written by bn_bwd_sync_kernel
 };
 
-// tanh through one v_exp_f32 and one v_rcp_f32 (ocml's tanhf is a long branchy sequence and
-// the BatchNorm passes evaluate it per element, twice in the backward): |error| < 1e-6
-TT2_DEV float fast_tanh(float x) {
-  const float t = 1.f - __fdividef(2.f, __expf(2.f * fabsf(x)) + 1.f);
-  return copysignf(t, x);
-}
-TT2_DEV float act_f(int act, float v) {
-  return act == ACT_RELU ? fmaxf(v, 0.f) : (act == ACT_TANH ? fast_tanh(v) : v);
-}
-TT2_DEV float act_grad_from_out(int act, float z) {
-  return act == ACT_RELU ? (z > 0.f ? 1.f : 0.f) : (act == ACT_TANH ? 1.f - z * z : 1.f);
-}
+// (fast_tanh, act_f, act_grad_from_out: tt2_common.h, shared with the GEMM's fused BatchNorm sums)
 
 // All BatchNorm kernels work on 8-column groups (16-B loads/stores; C % 8 == 0).
 // Statistics: one workgroup per chunk of rows_per rows; CG = C/8 column groups x
@@ -885,7 +874,7 @@ extern "C" int tt2_batchnorm_bwd(const tt2_bn_args* p, hipStream_t s) {
   else if (bf) hipLaunchKernelGGL((KER<bf16, float>), grid, dim3(NT), 0, s, a);                 \
   else if (dbf) hipLaunchKernelGGL((KER<float, bf16>), grid, dim3(NT), 0, s, a);                \
   else hipLaunchKernelGGL((KER<float, float>), grid, dim3(NT), 0, s, a);
-  TT2_BN_DISPATCH(bn_bwd_stats_kernel, dim3(a.R))
+  if (p->stats_rows <= 0) { TT2_BN_DISPATCH(bn_bwd_stats_kernel, dim3(a.R)) }   // else: tt2_gemm bn_bwd's sums
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
   const int ga = grid_for((int64_t)p->m * p->c / 8);
   TT2_BN_DISPATCH(bn_bwd_apply_kernel, dim3(ga))
@@ -958,7 +947,7 @@ extern "C" int tt2_batchnorm_bwd_stats(const tt2_bn_args* p, hipStream_t s) {
     return TT2_E_INVALID;
   const BnArgs a = bn_sync_args(p);
   const bool bf = p->dtype == TT2_DT_BF16, dbf = p->dout_dtype == TT2_DT_BF16;
-  TT2_BN_DISPATCH2(bn_bwd_stats_kernel, dim3(a.R), a)
+  if (p->stats_rows <= 0) { TT2_BN_DISPATCH2(bn_bwd_stats_kernel, dim3(a.R), a) }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
   return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_bwd_stats");
 }

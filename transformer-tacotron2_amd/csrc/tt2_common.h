@@ -227,3 +227,16 @@ TT2_DEV float max16(float v) {
 
 enum { TT2_F32 = 0, TT2_BF16 = 1, TT2_F16 = 2 };
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };
+
+// tanh through one v_exp_f32 and one v_rcp_f32 (ocml's tanhf is a long branchy sequence and
+// the BatchNorm passes evaluate it per element, twice in the backward): |error| < 1e-6
+TT2_DEV float fast_tanh(float x) {
+  const float t = 1.f - __fdividef(2.f, __expf(2.f * fabsf(x)) + 1.f);
+  return copysignf(t, x);
+}
+TT2_DEV float act_f(int act, float v) {
+  return act == ACT_RELU ? fmaxf(v, 0.f) : (act == ACT_TANH ? fast_tanh(v) : v);
+}
+TT2_DEV float act_grad_from_out(int act, float z) {
+  return act == ACT_RELU ? (z > 0.f ? 1.f : 0.f) : (act == ACT_TANH ? 1.f - z * z : 1.f);
+}

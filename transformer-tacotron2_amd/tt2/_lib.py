@@ -47,7 +47,7 @@ class GemmArgs(C.Structure):
         ("emit_mel", vp), ("emit_stop", vp), ("emit_prev", vp), ("emit_t", vp), ("emit_seed", vp),
         ("emit_done", vp), ("emit_nmels", i32), ("emit_tmax", i32),
         ("emit_stop_bias", vp), ("emit_stop_len", vp), ("emit_stop_thr", f32),
-        ("col_stats", vp),
+        ("col_stats", vp), ("bn_bwd", vp),
     ]
 
 

@@ -349,10 +349,13 @@ class TTSEngine:
                  ldr=ldo or n_in, gate=gate, ldg=ldo or n_in, gate_scale=gate_scale, a_conv=a_conv, beta=beta,
                  ws=self.ws, splits=act_splits(m, n_in, n_out, _wide(dy.dtype, a_conv, m, n_out, n_in)))
 
-    def _conv_dgrad(self, dy, wflip, out, m, cin, cout, K, T, ldo=None, beta=0.0):
-        """out[m, cin] = conv1d(dy, flipped W): implicit im2col of dy x wflip[cin][tap][cout]"""
+    def _conv_dgrad(self, dy, wflip, out, m, cin, cout, K, T, ldo=None, beta=0.0, bn_bwd=None):
+        """out[m, cin] = conv1d(dy, flipped W): implicit im2col of dy x wflip[cin][tap][cout].
+        bn_bwd: out is that BatchNorm backward's dout; the GEMM also leaves its column sums (one
+        tile per output, no split-K)"""
         ops.gemm(dy, wflip, out, m, cin, K * cout, cout, K * cout, ldo or cin, a_conv=(T, cout, (K - 1) // 2),
-                 beta=beta, ws=self.ws, splits=act_splits(m, cin, K * cout))
+                 beta=beta, ws=self.ws, splits=1 if bn_bwd is not None else act_splits(m, cin, K * cout),
+                 bn_bwd=bn_bwd)
 
     def _wgrad(self, dy, x, gw, n_out, n_in, m, ldy=None, ldx=None, b_conv=None, gb=None, now=False):
         """gw[n_out, n_in] (f32) = dy[m, n_out]^T @ x[m, n_in]; gb (optional) = the
@@ -858,22 +861,36 @@ class TTSEngine:
         nl = c.postnet_layers
         g = A["g_after"]
         scratch = [A["g_pa"], A["g_pb"]]
+        # the BatchNorm backward statistics of layer i - 1 from the conv dgrad of layer i that
+        # produces their dout (v7 LDS-image epilogue; TT2_BN_GEMM_STATS=0: the BN's own pass)
+        fused = lambda j: (self.bn_gemm_stats and cd == torch.bfloat16 and chans[j + 1] % 128 == 0  # noqa: E731
+                           and _wide(cd, (Ty, chans[j + 2], pad), Md, K * chans[j + 2]))
+        bstats = None   # (buf, rows) of this layer's sums, when the previous dgrad left them
         for i in reversed(range(nl)):
             cin, cout = chans[i], chans[i + 1]
             last = i == nl - 1
+            act = ACT_NONE if last else ACT_TANH
             # BN backward may run in place (g is dead afterwards)
             dyv = gbuf("g_pa", f"p{i}", (Md, cout)) if ov else scratch[i % 2].view(-1)[:Md * cout].view(Md, cout)
             ops.batchnorm_bwd(A[f"pcv_y{i}"], g, self.P(f"post.bn{i}.g"), self.P(f"post.bn{i}.b"),
                               A[f"pcv_mean{i}"], A[f"pcv_rstd{i}"], dyv, self.G(f"post.bn{i}.g"),
-                              self.G(f"post.bn{i}.b"), Md, cout, ACT_NONE if last else ACT_TANH,
-                              drop=self.drop(SITE_POSTNET + i, c.postnet_dropout), ws=self.ws, sync=self.bn_sync)
+                              self.G(f"post.bn{i}.b"), Md, cout, act,
+                              drop=self.drop(SITE_POSTNET + i, c.postnet_dropout), ws=self.ws, sync=self.bn_sync,
+                              stats=bstats)
+            bstats = None
             x_in = A[f"pcv_o{i - 1}"] if i > 0 else A["pin"]
             self._wgrad(dyv, x_in, self.G(f"post.conv{i}.w").view(cout, K * cin), cout, K * cin, Md, ldx=cin,
                         b_conv=(Ty, cin, pad), gb=self.G(f"post.conv{i}.b"))
             wflip = self._wflip(f"post.conv{i}.w", cout, cin, K)
             if i > 0:
                 gn = scratch[(i + 1) % 2].view(-1)[:Md * cin].view(Md, cin)
-                self._conv_dgrad(dyv, wflip, gn, Md, cin, cout, K, Ty)
+                j, bnb = i - 1, None
+                if fused(j):
+                    bstats = (A[f"pcv_part{j}"], GEMM_STATS_ROWS)   # (the forward's moments are consumed)
+                    bnb = ops.bn_bwd_args(A[f"pcv_y{j}"], self.P(f"post.bn{j}.g"), self.P(f"post.bn{j}.b"),
+                                          A[f"pcv_mean{j}"], A[f"pcv_rstd{j}"], Md, cin, ACT_TANH,
+                                          self.drop(SITE_POSTNET + j, c.postnet_dropout), bstats)
+                self._conv_dgrad(dyv, wflip, gn, Md, cin, cout, K, Ty, bn_bwd=bnb)
                 g = gn
             else:
                 # d(mel_before) += postnet input gradient (g_heads already holds direct + residual terms)

@@ -66,7 +66,7 @@ def gemm_args(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bia
               gate=None, ldg=0, gate_scale=1.0, alpha=1.0, beta=0.0, act=0, drop: Drop = NO_DROP, splits=1,
               a_conv=None, b_conv=None, ws: Workspace | None = None, variant: int = 0, a_ksum=None,
               a_ksum_beta=0.0, a_ln=None, kv=None, pe=None, emit=None, main_only=False,
-              defer_ws: bool = False, col_stats=None) -> GemmArgs:
+              defer_ws: bool = False, col_stats=None, bn_bwd=None) -> GemmArgs:
     """Build the tt2_gemm_args of one request (see tt2_capi.h).  defer_ws: only size the
     split-K workspace (ws_bytes); the caller places it."""
     L = lib()
@@ -93,6 +93,9 @@ def gemm_args(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bia
         g.b_conv_t, g.b_conv_c, g.b_conv_pad = b_conv
     g.kernel_variant = variant
     g.col_stats = ptr(col_stats)
+    if bn_bwd is not None:   # a _lib.BnArgs (bn_bwd_args); kept alive on the args for the call
+        g.bn_bwd = C.addressof(bn_bwd)
+        g._bn_keep = bn_bwd
     g.a_ksum, g.a_ksum_beta = ptr(a_ksum), a_ksum_beta
     if a_ln is not None:
         br, gam, bet, out, eps = a_ln
@@ -127,7 +130,9 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, **kw):
     emit = (mel_seq, stop_seq, prev, t_ptr, seed, done, n_mels, t_max): the decode frame emit
     (see tt2_capi.h), which also advances *t_ptr.
     col_stats (f32, 2 * ceil(m / 256) * n): the stored C's column moments per 256-row chunk
-    (mean, M2), for batchnorm_fwd(stats=(col_stats, GEMM_STATS_ROWS)); v7 LDS-image path only."""
+    (mean, M2), for batchnorm_fwd(stats=(col_stats, GEMM_STATS_ROWS)); v7 LDS-image path only.
+    bn_bwd (bn_bwd_args(...)): C is that BatchNorm backward's dout; its per-chunk sums go to the
+    args' stats buffer, for batchnorm_bwd(stats=(buf, GEMM_STATS_ROWS)); same path only."""
     L = lib()
     g = gemm_args(a, b, c, m, n, k, lda, ldb, ldc, **kw)
     if PROBE is not None:
@@ -400,11 +405,7 @@ def batchnorm_fwd(y, gamma, beta, mean, rstd, run_mean, run_var, out, m, c, act,
     a.out, a.out_dtype = out.data_ptr(), dt(out)
     a.res, a.res_dtype, a.res_ld = ptr(res), (dt(res) if res is not None else 0), res_ld
     if stats is not None and training:
-        sbuf, a.stats_rows = stats
-        need = L.tt2_batchnorm_workspace_size(C.byref(a))
-        if sbuf.dtype != torch.float32 or sbuf.numel() * 4 < need:
-            raise _lib.TT2Error(f"batchnorm_fwd: stats buffer needs {need} bytes of f32")
-        a.workspace, a.ws_bytes = sbuf.data_ptr(), sbuf.numel() * 4
+        _bn_stats_into(L, a, stats)
     else:
         buf = (ws or _WS).get(L.tt2_batchnorm_workspace_size(C.byref(a)))
         a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
@@ -417,16 +418,38 @@ def batchnorm_fwd(y, gamma, beta, mean, rstd, run_mean, run_var, out, m, c, act,
     check(L.tt2_batchnorm_fwd_apply(C.byref(a), stream_ptr()), "tt2_batchnorm_fwd_apply")
 
 
+def _bn_stats_into(L, a, stats):
+    sbuf, a.stats_rows = stats
+    need = L.tt2_batchnorm_workspace_size(C.byref(a))
+    if sbuf.dtype != torch.float32 or sbuf.numel() * 4 < need:
+        raise _lib.TT2Error(f"batchnorm: stats buffer needs {need} bytes of f32")
+    a.workspace, a.ws_bytes = sbuf.data_ptr(), sbuf.numel() * 4
+
+
+def bn_bwd_args(y, gamma, beta, mean, rstd, m, c, act, drop: Drop, stats) -> _lib.BnArgs:
+    """The BatchNorm backward whose column sums a GEMM producing its dout computes
+    (gemm(..., bn_bwd=...)); stats = (buf, GEMM_STATS_ROWS) as then given to batchnorm_bwd."""
+    L = lib()
+    a = _bn(y, gamma, beta, mean, rstd, m, c, act, True, drop, 1e-5, 0.1, None)
+    _bn_stats_into(L, a, stats)
+    return a
+
+
 def batchnorm_bwd(y, dout, gamma, beta, mean, rstd, dy, dgamma, dbeta, m, c, act, drop: Drop = NO_DROP,
-                  ws: Workspace | None = None, sync=None):
+                  ws: Workspace | None = None, sync=None, stats=None):
     """sync: SyncBatchNorm backward (the column sums over all ranks' rows; dgamma / dbeta
-    stay this rank's sums for the gradient all-reduce)."""
+    stay this rank's sums for the gradient all-reduce).
+    stats = (buf, rows): the per-chunk column sums are already in buf (the GEMM that produced
+    dout, gemm(..., bn_bwd=bn_bwd_args(...))), so the statistics pass is skipped."""
     L = lib()
     a = _bn(y, gamma, beta, mean, rstd, m, c, act, True, drop, 1e-5, 0.1, ws)
     a.dout, a.dout_dtype, a.dy = dout.data_ptr(), dt(dout), dy.data_ptr()
     a.dgamma, a.dbeta = dgamma.data_ptr(), dbeta.data_ptr()
-    buf = (ws or _WS).get(L.tt2_batchnorm_workspace_size(C.byref(a)))
-    a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
+    if stats is not None:
+        _bn_stats_into(L, a, stats)
+    else:
+        buf = (ws or _WS).get(L.tt2_batchnorm_workspace_size(C.byref(a)))
+        a.workspace, a.ws_bytes = buf.data_ptr(), buf.numel()
     if sync is None:
         check(L.tt2_batchnorm_bwd(C.byref(a), stream_ptr()), "tt2_batchnorm_bwd")
         return
