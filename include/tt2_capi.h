@@ -124,23 +124,26 @@ typedef struct tt2_gemm_args {
   float emit_stop_thr;
   /* fused BatchNorm statistics: when col_stats != NULL, each 256-row chunk r of the stored
    * (bf16) output C also leaves its column moments, col_stats[(2 r) * n + j] = mean and
-   * col_stats[(2 r + 1) * n + j] = sum over the chunk's rows of (C - mean)^2 (rows < m only;
-   * the last chunk holds m - 256 r rows), in the chunk layout tt2_batchnorm_fwd reads with
-   * stats_rows = TT2_GEMM_STATS_ROWS.  Only on the 256 x 128 LDS-image path: bf16 C, no split-K,
-   * n % 128 == 0 (tt2_gemm_plan 13 with the default epilogue); other requests fail with
-   * TT2_E_INVALID. */
+   * col_stats[(2 r + 1) * n + j] = sum over the chunk's rows of (C - mean)^2 (rows < m only),
+   * in the chunk layout tt2_batchnorm_fwd reads with stats_rows = the chunk's rows.  A chunk is the
+   * kernel's tile height, tt2_gemm_stats_rows(): 64 rows on the 64 x 64 kernel (plan 15), else 256
+   * on the 256 x 128 LDS-image path (bf16 C, A and B K-contiguous, n % 128 == 0); bf16 C, 16-B
+   * aligned rows and no split-K either way.  Other requests fail with TT2_E_INVALID. */
   float* col_stats;
   /* fused BatchNorm backward sums: when bn_bwd != NULL, C is that BatchNorm's dout (the gradient
    * of its output: bn_bwd->y is its input, mean / rstd / gamma / beta / act / dropout as for
    * tt2_batchnorm_bwd, c == n, m == m), and each 256-row chunk r of the stored (bf16) C leaves the
    * column sums of dpre = dout * keep * act'(z) and of dpre * xhat in bn_bwd->workspace
-   * ([r][2][n], the layout tt2_batchnorm_bwd reads with stats_rows = TT2_GEMM_STATS_ROWS).  The
+   * ([r][2][n], the layout tt2_batchnorm_bwd reads with stats_rows = tt2_gemm_stats_rows()).  The
    * tt2_bn_args struct is read during the call only.  Same path restrictions as col_stats. */
   const struct tt2_bn_args* bn_bwd;
 } tt2_gemm_args;
-#define TT2_GEMM_STATS_ROWS 256
+#define TT2_GEMM_STATS_ROWS 256   /* the 256 x 128 kernel's chunk (tt2_gemm_stats_rows) */
 
 size_t tt2_gemm_workspace_size(const tt2_gemm_args* a);
+/* Rows per chunk of a col_stats / bn_bwd request's statistics (the kernel's tile height): 64 on
+ * the 64 x 64 kernel, 256 on the 256 x 128 one, 0 when the request cannot fuse them.  Host-only. */
+int32_t tt2_gemm_stats_rows(const tt2_gemm_args* a);
 int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream);
 /* Kernel tt2_gemm would launch for these args (no device work): 1 register-staged
  * 128x128 (any dtype), 2 LDS-DMA 128x128 (bf16), 3 skinny decode (m <= 64),

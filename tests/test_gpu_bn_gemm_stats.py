@@ -1,14 +1,16 @@
-"""BatchNorm statistics fused into the producing conv GEMM (tt2_gemm col_stats + tt2_bn_args
-stats_rows, GPU): the chunk moments against float64 of the stored bf16 output, the BatchNorm
-forward from them against the BatchNorm's own statistics pass, and the requests the fusion
-refuses (tests/test_gpu_norm.py covers the BatchNorm kernels themselves)."""
+"""BatchNorm statistics fused into the producing conv GEMM (tt2_gemm col_stats / bn_bwd +
+tt2_bn_args stats_rows, GPU), on both kernels that carry them (64-row chunks on the 64 x 64
+kernel, 256-row chunks on the 256 x 128 one; tt2_gemm_stats_rows says which): the chunk
+statistics against float64 of the stored bf16 output, the BatchNorm forward / backward from them
+against the BatchNorm's own statistics pass, and the requests the fusion refuses
+(tests/test_gpu_norm.py covers the BatchNorm kernels themselves)."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
 from tt2 import ops  # noqa: E402
-from tt2._lib import ACT_TANH, GEMM_STATS_ROWS, TT2Error  # noqa: E402
+from tt2._lib import ACT_RELU, ACT_TANH, TT2Error  # noqa: E402
 
 
 def _conv(m, cin, cout, T, g):
@@ -20,36 +22,39 @@ def _conv(m, cin, cout, T, g):
     return x, w, b, (T, cin, pad), K * cin
 
 
-@pytest.mark.parametrize("m,cin,cout,T", [(12800, 512, 512, 800), (12800, 80, 512, 800), (3 * 96, 512, 256, 96),
-                                          (1000, 512, 128, 125)])
-def test_gemm_col_stats(m, cin, cout, T):
+@pytest.mark.parametrize("m,cin,cout,T,rows", [(12800, 512, 512, 800, 256), (12800, 80, 512, 800, 256),
+                                               (12500, 512, 512, 125, 256), (3 * 96, 512, 256, 96, 64),
+                                               (1000, 512, 128, 125, 64), (2048, 512, 512, 128, 64)])
+def test_gemm_col_stats(m, cin, cout, T, rows):
     g = torch.Generator().manual_seed(m + cin)
     x, w, b, conv, k = _conv(m, cin, cout, T, g)
     y = torch.empty(m, cout, dtype=torch.bfloat16, device="cuda")
-    R = (m + GEMM_STATS_ROWS - 1) // GEMM_STATS_ROWS
+    assert ops.gemm_stats_rows(x, w, y, m, cout, k, cin, k, cout, bias=b, a_conv=conv) == rows
+    R = (m + rows - 1) // rows
     st = torch.full((2 * R * cout,), float("nan"), device="cuda")
     ops.gemm(x, w, y, m, cout, k, cin, k, cout, bias=b, a_conv=conv, col_stats=st)
-    y_ref = torch.empty_like(y)   # the same kernel without the statistics (variant 14: v7, LDS image;
-    ops.gemm(x, w, y_ref, m, cout, k, cin, k, cout, bias=b, a_conv=conv, variant=14)   # auto may take v8)
+    y_ref = torch.empty_like(y)   # the same kernel (the auto plan) without the statistics
+    ops.gemm(x, w, y_ref, m, cout, k, cin, k, cout, bias=b, a_conv=conv)
     torch.cuda.synchronize()
     assert torch.equal(y, y_ref)          # the statistics do not change what is stored
     yd = y.double().cpu()
     st = st.view(R, 2, cout).double().cpu()
     for r in range(R):
-        blk = yd[r * GEMM_STATS_ROWS:(r + 1) * GEMM_STATS_ROWS]
+        blk = yd[r * rows:(r + 1) * rows]
         mu = blk.mean(0)
         m2 = ((blk - mu) ** 2).sum(0)
         assert torch.allclose(st[r, 0], mu, rtol=1e-5, atol=1e-6), (r, (st[r, 0] - mu).abs().max())
         assert torch.allclose(st[r, 1], m2, rtol=1e-4, atol=1e-4 * blk.shape[0]), (r, (st[r, 1] - m2).abs().max())
 
 
-@pytest.mark.parametrize("m,T", [(12800, 800), (1000, 125)])
+@pytest.mark.parametrize("m,T", [(12800, 800), (1000, 125), (2048, 128)])
 def test_batchnorm_fwd_from_gemm_stats(m, T):
     cin = cout = 512
     g = torch.Generator().manual_seed(7 + m)
     x, w, b, conv, k = _conv(m, cin, cout, T, g)
     y = torch.empty(m, cout, dtype=torch.bfloat16, device="cuda")
-    R = (m + GEMM_STATS_ROWS - 1) // GEMM_STATS_ROWS
+    rows = ops.gemm_stats_rows(x, w, y, m, cout, k, cin, k, cout, bias=b, a_conv=conv)
+    R = (m + rows - 1) // rows
     st = torch.empty(2 * R * cout, device="cuda")
     ops.gemm(x, w, y, m, cout, k, cin, k, cout, bias=b, a_conv=conv, col_stats=st)
     gamma = (1 + 0.1 * torch.randn(cout, generator=g)).cuda()
@@ -57,7 +62,7 @@ def test_batchnorm_fwd_from_gemm_stats(m, T):
     seed = torch.tensor([5], dtype=torch.int32, device="cuda")
     drop = ops.Drop(seed, 40, 0.5)
     outs = []
-    for stats in ((st, GEMM_STATS_ROWS), None):
+    for stats in ((st, rows), None):
         mean, rstd = torch.empty(cout, device="cuda"), torch.empty(cout, device="cuda")
         rm, rv = torch.zeros(cout, device="cuda"), torch.ones(cout, device="cuda")
         out = torch.empty_like(y)
@@ -80,21 +85,24 @@ def test_col_stats_refused():
     g = torch.Generator().manual_seed(3)
     m, cin, cout, T = 12800, 512, 512, 800
     x, w, b, conv, k = _conv(m, cin, cout, T, g)
-    st = torch.empty(2 * 50 * cout, device="cuda")
+    st = torch.empty(2 * 200 * cout, device="cuda")
     with pytest.raises(TT2Error):   # split-K
         ops.gemm(x, w, torch.empty(m, cout, dtype=torch.bfloat16, device="cuda"), m, cout, k, cin, k, cout,
                  a_conv=conv, splits=2, col_stats=st, ws=ops.Workspace())
     with pytest.raises(TT2Error):   # f32 C
         ops.gemm(x, w, torch.empty(m, cout, device="cuda"), m, cout, k, cin, k, cout, a_conv=conv, col_stats=st)
-    with pytest.raises(TT2Error):   # n % 128
-        ops.gemm(x, w[:80], torch.empty(m, 80, dtype=torch.bfloat16, device="cuda"), m, 80, k, cin, k, 80,
-                 a_conv=conv, col_stats=st)
+    w2 = torch.zeros(576, k, dtype=torch.bfloat16, device="cuda")
+    y2 = torch.empty(m, 576, dtype=torch.bfloat16, device="cuda")
+    assert ops.gemm_stats_rows(x, w2, y2, m, 576, k, cin, k, 576, a_conv=conv) == 0
+    with pytest.raises(TT2Error):   # the 256 x 128 kernel with n % 128 != 0
+        ops.gemm(x, w2, y2, m, 576, k, cin, k, 576, a_conv=conv, col_stats=st)
 
 
-@pytest.mark.parametrize("m,T,p", [(12800, 800, 0.5), (1000, 125, 0.0)])
-def test_batchnorm_bwd_from_gemm_sums(m, T, p):
-    """the post-net backward's pairing: the conv dgrad that produces a BatchNorm's dout also
-    leaves its column sums (tt2_gemm bn_bwd), and the BatchNorm backward skips its own pass"""
+@pytest.mark.parametrize("m,T,p,act", [(12800, 800, 0.5, ACT_TANH), (1000, 125, 0.0, ACT_TANH),
+                                       (2048, 128, 0.5, ACT_RELU)])
+def test_batchnorm_bwd_from_gemm_sums(m, T, p, act):
+    """the post-net / pre-net backward's pairing: the conv dgrad that produces a BatchNorm's dout
+    also leaves its column sums (tt2_gemm bn_bwd), and the BatchNorm backward skips its own pass"""
     c = 512
     g = torch.Generator().manual_seed(11 + m)
     dyn, wf, _, conv, k = _conv(m, c, c, T, g)          # the next layer's dy and flipped weights
@@ -105,18 +113,19 @@ def test_batchnorm_bwd_from_gemm_sums(m, T, p):
     rstd = 1 / torch.sqrt(y.float().var(0, unbiased=False) + 1e-5)
     seed = torch.tensor([9], dtype=torch.int32, device="cuda")
     drop = ops.Drop(seed, 41, p)
-    R = (m + GEMM_STATS_ROWS - 1) // GEMM_STATS_ROWS
-    sums = torch.full((2 * R * c,), float("nan"), device="cuda")
-    bnb = ops.bn_bwd_args(y, gamma, beta, mean, rstd, m, c, ACT_TANH, drop, (sums, GEMM_STATS_ROWS))
     dout = torch.empty(m, c, dtype=torch.bfloat16, device="cuda")
+    rows = ops.gemm_stats_rows(dyn, wf, dout, m, c, k, c, k, c, a_conv=conv)
+    R = (m + rows - 1) // rows
+    sums = torch.full((2 * R * c,), float("nan"), device="cuda")
+    bnb = ops.bn_bwd_args(y, gamma, beta, mean, rstd, m, c, act, drop, (sums, rows))
     ops.gemm(dyn, wf, dout, m, c, k, c, k, c, a_conv=conv, bn_bwd=bnb)
     dout_ref = torch.empty_like(dout)
-    ops.gemm(dyn, wf, dout_ref, m, c, k, c, k, c, a_conv=conv, variant=14)
+    ops.gemm(dyn, wf, dout_ref, m, c, k, c, k, c, a_conv=conv)
     res = []
-    for stats in ((sums, GEMM_STATS_ROWS), None):
+    for stats in ((sums, rows), None):
         dy = torch.empty_like(y)
         dg, db = torch.empty(c, device="cuda"), torch.empty(c, device="cuda")
-        ops.batchnorm_bwd(y, dout, gamma, beta, mean, rstd, dy, dg, db, m, c, ACT_TANH, drop=drop,
+        ops.batchnorm_bwd(y, dout, gamma, beta, mean, rstd, dy, dg, db, m, c, act, drop=drop,
                           ws=ops.Workspace(), stats=stats)
         res.append((dy, dg, db))
     torch.cuda.synchronize()
@@ -127,8 +136,12 @@ def test_batchnorm_bwd_from_gemm_sums(m, T, p):
         from tt2_oracle import dropout_keep
         keep = torch.from_numpy(dropout_keep(9, 41, m * c, p)).view(m, c).double() / (1 - p)
     xh = (y.double().cpu() - mean.double().cpu()) * rstd.double().cpu()
-    z = torch.tanh(xh * gamma.double().cpu() + beta.double().cpu())
-    dp = dout.double().cpu() * keep * (1 - z * z)
+    u = xh * gamma.double().cpu() + beta.double().cpu()
+    if act == ACT_TANH:
+        z = torch.tanh(u)
+        dp = dout.double().cpu() * keep * (1 - z * z)
+    else:
+        dp = dout.double().cpu() * keep * (u > 0).double()
     s = sums.view(R, 2, c).double().cpu().sum(0)
     assert torch.allclose(s[0], dp.sum(0), rtol=1e-4, atol=1e-3), (s[0] - dp.sum(0)).abs().max()
     assert torch.allclose(s[1], (dp * xh).sum(0), rtol=1e-4, atol=1e-3), (s[1] - (dp * xh).sum(0)).abs().max()

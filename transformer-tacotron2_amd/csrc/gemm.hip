@@ -1824,7 +1824,84 @@ TT2_DEV bf16x8 g8_frag_mc(const char* img, int col0, int s, int lane) {
   return u.v;
 }
 
-template <bool BKC>
+// v8's fused BatchNorm statistics (SM 1: col_stats moments, 2: bn_bwd sums; see g7_store_c): each
+// thread holds one row x 8 columns of the 64 x 64 image; the 8 rows of a wave that share a chunk
+// combine by shuffles, the 8 waves through a free ring slot, and 64 threads write the 64-row
+// chunk's value per column.
+template <int SM>
+TT2_DEV void g8_stats(const EpiParams& E, char* smem, int m0, int n0, int M, int N) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rr = tid >> 3, c = tid & 7, m = m0 + rr, n = n0 + 8 * c;
+  const bool ok = m < M && n < N;
+  float v[8], s1[8], s2[8];
+  bf16x8_unpack(*reinterpret_cast<const u32x4*>(smem + rr * 128 + ((c ^ g8_swz(rr)) << 4)), v);
+  if constexpr (SM == 1) {
+    float k[8];
+    bf16x8_unpack(*reinterpret_cast<const u32x4*>(smem + ((c ^ g8_swz(0)) << 4)), k);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = ok ? v[j] - k[j] : 0.f;
+      s1[j] = d;
+      s2[j] = d * d;
+    }
+  } else {
+    const int mc = min(m, M - 1), nc = min(n, N - 8);
+    float yf[8];
+    bf16x8_unpack(*reinterpret_cast<const u32x4*>(E.bnb.y + (int64_t)mc * N + nc), yf);
+    const DropDesc& dd = E.bnb.drop;
+    const uint32_t seed = dd.thr ? *dd.seed : 0u;
+    const uint32_t bits = dd.thr ? drop_bits8(seed, dd.site, (uint32_t)((int64_t)m * N + n), dd.thr) : 0xFFu;
+    const float sc = dd.thr ? dd.scale : 1.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float keep = (bits >> j) & 1u ? sc : 0.f;
+      const float xh = (yf[j] - E.bnb.mean[nc + j]) * E.bnb.rstd[nc + j];
+      const float z = act_f(E.bnb.act, xh * E.bnb.gamma[nc + j] + E.bnb.beta[nc + j]);
+      const float dp = ok ? v[j] * keep * act_grad_from_out(E.bnb.act, z) : 0.f;
+      s1[j] = dp;
+      s2[j] = dp * xh;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {   // lanes c, c + 8, ..., c + 56: the wave's 8 rows of this chunk
+    s1[j] += __shfl_xor(s1[j], 8);
+    s2[j] += __shfl_xor(s2[j], 8);
+    s1[j] += __shfl_xor(s1[j], 16);
+    s2[j] += __shfl_xor(s2[j], 16);
+    s1[j] += __shfl_xor(s1[j], 32);
+    s2[j] += __shfl_xor(s2[j], 32);
+  }
+  float* red = reinterpret_cast<float*>(smem + 2 * G8_STAGE);   // [8 waves][64 cols][2], past the image
+  if (lane < 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(w * 64 + 8 * c + j) * 2 + 0] = s1[j];
+      red[(w * 64 + 8 * c + j) * 2 + 1] = s2[j];
+    }
+  }
+  __syncthreads();
+  if (tid < 64 && n0 + tid < N) {
+    float S1 = 0.f, S2 = 0.f;
+    for (int q = 0; q < G8_NT / 64; ++q) {
+      S1 += red[(q * 64 + tid) * 2 + 0];
+      S2 += red[(q * 64 + tid) * 2 + 1];
+    }
+    float* out = (SM == 1 ? E.cstats : E.bnb.part) + (int64_t)(m0 / 64) * 2 * N + n0 + tid;
+    if constexpr (SM == 1) {
+      const int cc = tid >> 3;
+      const float kt = __uint_as_float((uint32_t)*reinterpret_cast<const uint16_t*>(
+                                           smem + ((cc ^ g8_swz(0)) << 4) + 2 * (tid & 7)) << 16);
+      const float nr = (float)min(64, M - m0);
+      out[0] = kt + S1 / nr;
+      out[N] = fmaxf(S2 - S1 * S1 / nr, 0.f);
+    } else {
+      out[0] = S1;
+      out[N] = S2;
+    }
+  }
+}
+
+template <bool BKC, int SM = 0>
 __global__ __launch_bounds__(G8_NT, 2) void gemm8_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
                                                          int ntn, int items, unsigned long long* span) {
   __shared__ __attribute__((aligned(1024))) char smem[G8_STAGES * G8_STAGE];
@@ -1908,6 +1985,7 @@ __global__ __launch_bounds__(G8_NT, 2) void gemm8_kernel(OpDesc A, OpDesc B, Epi
   if (mm < M && nn < N)   // nontemporal, as v7's C (g7_store_c)
     __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(smem + rr * 128 + ((c ^ g8_swz(rr)) << 4)),
                                 reinterpret_cast<u32x4*>(C + (int64_t)mm * E.ldc + nn));
+  if constexpr (SM != 0) g8_stats<SM>(E, smem, m0, n0, M, N);
   span_end(span, &span_done, G8_NT / 64);
 }
 
@@ -1915,11 +1993,16 @@ template <bool BKC>
 hipError_t launch8(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, hipStream_t s) {
   const int ntn = (N + 63) / 64, items = ((M + 63) / 64) * ntn;
   ProbeScope ps(s, items);
-  if (ps.ext())
-    hipExtLaunchKernelGGL((gemm8_kernel<BKC>), dim3(items), dim3(G8_NT), 0, s, ps.e0, ps.e1, 0, A, B, E, M, N, K, ntn,
-                          items, ps.span);
-  else
-    hipLaunchKernelGGL((gemm8_kernel<BKC>), dim3(items), dim3(G8_NT), 0, s, A, B, E, M, N, K, ntn, items, ps.span);
+  auto go = [&](auto kern) {
+    if (ps.ext())
+      hipExtLaunchKernelGGL(kern, dim3(items), dim3(G8_NT), 0, s, ps.e0, ps.e1, 0, A, B, E, M, N, K, ntn, items,
+                            ps.span);
+    else
+      hipLaunchKernelGGL(kern, dim3(items), dim3(G8_NT), 0, s, A, B, E, M, N, K, ntn, items, ps.span);
+  };
+  if (E.cstats) go(gemm8_kernel<BKC, 1>);   // fused BatchNorm statistics (64-row chunks)
+  else if (E.bnb.part) go(gemm8_kernel<BKC, 2>);
+  else go(gemm8_kernel<BKC, 0>);
   return hipGetLastError();
 }
 
@@ -2220,6 +2303,31 @@ static int gemm_plan(const tt2_gemm_args* a) {
 
 extern "C" int tt2_gemm_plan(const tt2_gemm_args* a) { return gemm_plan(a); }
 
+// The kernel a fused-statistics request (col_stats / bn_bwd) runs on, given the auto plan: v8
+// (64-row chunks) when the plan takes it, else v7's LDS-image epilogue (256-row chunks); -1 when
+// neither can (split-K, f32 C, unaligned rows, v7 with a transposed operand or n % 128).
+static int stats_plan(const tt2_gemm_args* a, int plan) {
+  auto al = [](const void* p, int64_t ld) { return reinterpret_cast<uintptr_t>(p) % 16 == 0 && (ld * 2) % 16 == 0; };
+  if (a->splits > 1 || a->dtype_out != TT2_BF16 || !al(a->c, a->ldc) || a->n % 8 ||
+      (reinterpret_cast<uintptr_t>(a->col_stats) & 3))
+    return -1;
+  if (plan == 15) return 15;
+  if (plan != 13) {
+    tt2_gemm_args b = *a;
+    b.kernel_variant = 14;
+    plan = gemm_plan(&b);
+  }
+  if (plan != 13 || a->trans_a || a->trans_b || !g7_lds_epi(a->kernel_variant) || a->n % 128) return -1;
+  return 13;
+}
+
+extern "C" int32_t tt2_gemm_stats_rows(const tt2_gemm_args* a) {
+  const int plan = gemm_plan(a);
+  if (plan < 0) return 0;
+  const int sp = stats_plan(a, plan);
+  return sp == 15 ? 64 : sp == 13 ? 256 : 0;
+}
+
 // Validate one GEMM request and build its operand / epilogue descriptors.
 static int gemm_prep(const tt2_gemm_args* a, OpDesc& A, OpDesc& B, EpiParams& ep) {
   const int esz = a->dtype_in == TT2_F32 ? 4 : 2;
@@ -2257,11 +2365,8 @@ static int gemm_prep(const tt2_gemm_args* a, OpDesc& A, OpDesc& B, EpiParams& ep
   ep.main_only = a->main_only;
   ep.cstats = a->col_stats;
   if (const tt2_bn_args* bn = a->bn_bwd) {
-    const int rp = TT2_GEMM_STATS_ROWS;
     if (bn->dtype != TT2_DT_BF16 || bn->c != a->n || bn->m != a->m || !bn->y || !bn->mean || !bn->rstd ||
-        !bn->gamma || !bn->beta || !bn->workspace ||
-        bn->ws_bytes < (size_t)((a->m + rp - 1) / rp) * 2 * a->n * sizeof(float) || a->col_stats ||
-        (bn->drop_thr && !bn->drop_seed))
+        !bn->gamma || !bn->beta || !bn->workspace || a->col_stats || (bn->drop_thr && !bn->drop_seed))
       return tt2_set_error(TT2_E_INVALID, "tt2_gemm: bn_bwd needs a bf16 BatchNorm of this GEMM's m x n, its "
                                           "y / mean / rstd / gamma / beta, a chunk-sums workspace, no col_stats");
     ep.bnb.y = reinterpret_cast<const bf16*>(bn->y);
@@ -2308,16 +2413,15 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
     b.kernel_variant = 13;
     plan = gemm_plan(&b);
   }
-  const bool fstats = ep.cstats || ep.bnb.part;
-  if (fstats && plan != 13) {   // the fused column statistics exist on v7's LDS-image path only
-    tt2_gemm_args b = *a;
-    b.kernel_variant = 14;
-    plan = gemm_plan(&b);
+  if (ep.cstats || ep.bnb.part) {   // fused BatchNorm statistics: v8's or v7's image epilogue
+    plan = stats_plan(a, plan);
+    if (plan < 0)
+      return tt2_set_error(TT2_E_INVALID, "tt2_gemm: col_stats / bn_bwd need the v8 path or v7's LDS-image path "
+                                          "(bf16 C, 16-B aligned rows, no split-K; v7: NT and n % 128 == 0)");
+    const int rp = plan == 15 ? 64 : 256;
+    if (a->bn_bwd && a->bn_bwd->ws_bytes < (size_t)((a->m + rp - 1) / rp) * 2 * a->n * sizeof(float))
+      return tt2_set_error(TT2_E_INVALID, "tt2_gemm: bn_bwd workspace smaller than its chunk sums");
   }
-  if (fstats && !(plan == 13 && !a->trans_a && !a->trans_b && g7_lds_epi(a->kernel_variant) && sp == 1 && a->dtype_out == TT2_BF16 && ep.vec &&
-                     a->n % 128 == 0 && (reinterpret_cast<uintptr_t>(a->col_stats) & 3) == 0))
-    return tt2_set_error(TT2_E_INVALID, "tt2_gemm: col_stats / bn_bwd need the v7 LDS-image path (bf16 C, 16-B "
-                                        "aligned rows, no split-K, n % 128 == 0)");
   if (plan == 3) {   // skinny-M weight-streaming path (decode step)
     SkinnyFuse F{reinterpret_cast<const bf16*>(a->a_ln_branch), a->a_ln_gamma, a->a_ln_beta,
                  reinterpret_cast<bf16*>(a->a_ln_out), a->a_ln_eps, a->kv_cache, a->kv_t,

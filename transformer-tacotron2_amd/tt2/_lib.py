@@ -64,6 +64,7 @@ SIGNATURES: dict[str, tuple[list, object]] = {
     "tt2_gemm_workspace_size": ([C.POINTER(GemmArgs)], sz),
     "tt2_gemm": ([C.POINTER(GemmArgs), vp], C.c_int),
     "tt2_gemm_plan": ([C.POINTER(GemmArgs)], C.c_int),
+    "tt2_gemm_stats_rows": ([C.POINTER(GemmArgs)], C.c_int32),
     "tt2_gemm_grouped": ([C.POINTER(GemmArgs), C.c_int32, vp], C.c_int),
     "tt2_gemm_grouped_fin": ([C.POINTER(GemmArgs), C.c_int32, vp, vp], C.c_int),
     "tt2_gemm_grouped_ex": ([C.POINTER(GemmArgs), C.c_int32, vp, C.c_int32, vp], C.c_int),

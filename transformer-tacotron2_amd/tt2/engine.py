@@ -20,7 +20,7 @@ import os
 import torch
 
 from . import ops
-from ._lib import ACT_NONE, ACT_RELU, ACT_TANH, GEMM_STATS_ROWS
+from ._lib import ACT_NONE, ACT_RELU, ACT_TANH
 from .trace import ranged
 from .config import (SITE_DEC_FC1, SITE_DEC_FC2, SITE_DEC_LAYER, SITE_DEC_PE, SITE_ENC_CONV, SITE_ENC_LAYER,
                      SITE_ENC_PE, SITE_POSTNET, TTSConfig)
@@ -97,6 +97,7 @@ class Arena:
         mk("emb", (Me, d))
         for i in range(c.enc_conv_layers):
             mk(f"ecv_y{i}", (Me, d))
+            mk(f"ecv_part{i}", (2 * ((Me + 63) // 64) * d,), f32)   # fused BatchNorm statistics (see pcv_part)
             mk(f"ecv_o{i}", (Me, d))
             mk(f"ecv_mean{i}", (d,), f32)
             mk(f"ecv_rstd{i}", (d,), f32)
@@ -148,8 +149,9 @@ class Arena:
                 mk(f"pcv_o{i}", (Md, chans[i + 1]))
             mk(f"pcv_mean{i}", (chans[i + 1],), f32)
             mk(f"pcv_rstd{i}", (chans[i + 1],), f32)
-            # the conv GEMM's fused BatchNorm statistics (256-row chunk moments, bf16 training)
-            mk(f"pcv_part{i}", (2 * ((Md + GEMM_STATS_ROWS - 1) // GEMM_STATS_ROWS) * chans[i + 1],), f32)
+            # the conv GEMM's fused BatchNorm statistics (chunk moments / sums, bf16 training; sized
+            # for the smallest chunk, the 64 x 64 kernel's)
+            mk(f"pcv_part{i}", (2 * ((Md + 63) // 64) * chans[i + 1],), f32)
         mk("mel_after", (Md, c.n_mels), f32)
         mk("loss", (4,), f32)
         # ---- gradient scratch
@@ -343,11 +345,12 @@ class TTSEngine:
                  a_conv=a_conv, beta=beta, ws=self.ws, splits=sp, **fuse)
 
     def _dgrad(self, dy, w, out, m, n_in, n_out, res=None, gate=None, gate_scale=1.0, ldy=None, ldo=None,
-               a_conv=None, beta=0.0):
-        """out[m, n_in] = dy[m, n_out] @ W[n_out, n_in] (+res) (*gate)"""
+               a_conv=None, beta=0.0, bn_bwd=None):
+        """out[m, n_in] = dy[m, n_out] @ W[n_out, n_in] (+res) (*gate); bn_bwd: see _conv_dgrad"""
+        sp = 1 if bn_bwd is not None else act_splits(m, n_in, n_out, _wide(dy.dtype, a_conv, m, n_out, n_in))
         ops.gemm(dy, w, out, m, n_in, n_out, ldy or n_out, n_in, ldo or n_in, trans_b=True, res=res,
                  ldr=ldo or n_in, gate=gate, ldg=ldo or n_in, gate_scale=gate_scale, a_conv=a_conv, beta=beta,
-                 ws=self.ws, splits=act_splits(m, n_in, n_out, _wide(dy.dtype, a_conv, m, n_out, n_in)))
+                 ws=self.ws, splits=sp, bn_bwd=bn_bwd)
 
     def _conv_dgrad(self, dy, wflip, out, m, cin, cout, K, T, ldo=None, beta=0.0, bn_bwd=None):
         """out[m, cin] = conv1d(dy, flipped W): implicit im2col of dy x wflip[cin][tap][cout].
@@ -670,12 +673,14 @@ class TTSEngine:
         x = A["emb"]
         for i in range(c.enc_conv_layers):
             y = A[f"ecv_y{i}"]
-            self._lin(x, self.W(f"enc.conv{i}.w"), y, Me, d, K * d, bias=self.P(f"enc.conv{i}.b"), ldx=d,
-                      a_conv=(Tx, d, pad))
+            conv = dict(bias=self.P(f"enc.conv{i}.b"), ldx=d, a_conv=(Tx, d, pad))
+            st = self._fused_stats(tr, A[f"ecv_part{i}"], x, self.W(f"enc.conv{i}.w"), y, Me, d, K * d, **conv)
+            self._lin(x, self.W(f"enc.conv{i}.w"), y, Me, d, K * d, **conv,
+                      **({"col_stats": st[0]} if st is not None else {}))
             ops.batchnorm_fwd(y, self.P(f"enc.bn{i}.g"), self.P(f"enc.bn{i}.b"), A[f"ecv_mean{i}"],
                               A[f"ecv_rstd{i}"], self.S(f"enc.bn{i}.rm"), self.S(f"enc.bn{i}.rv"), A[f"ecv_o{i}"],
                               Me, d, ACT_RELU, tr, drop=self.drop(SITE_ENC_CONV + i, c.prenet_dropout),
-                              eps=c.bn_eps, momentum=c.bn_momentum, ws=self.ws, sync=self.bn_sync)
+                              eps=c.bn_eps, momentum=c.bn_momentum, ws=self.ws, sync=self.bn_sync, stats=st)
             x = A[f"ecv_o{i}"]
         self._lin(x, self.W("enc.proj.w"), A["eproj"], Me, d, d, bias=self.P("enc.proj.b"))
         ops.posenc_fwd(A["eproj"], self.P("enc.alpha"), self.pe, A["ex0"], Me, Tx,
@@ -799,11 +804,11 @@ class TTSEngine:
             cin, cout = chans[i], chans[i + 1]
             y = A[f"pcv_y{i}"]
             # training in bf16: the conv GEMM leaves the BatchNorm's column moments from its output
-            # tiles (v7 LDS image), so the statistics pass over y is skipped (TT2_BN_GEMM_STATS=0: not)
-            st = A[f"pcv_part{i}"] if (tr and self.bn_gemm_stats and self.cd == torch.bfloat16 and cout % 128 == 0
-                                       and _wide(self.cd, (Ty, cin, pad), Md, K * cin)) else None
-            self._lin(x, self.W(f"post.conv{i}.w"), y, Md, cout, K * cin, bias=self.P(f"post.conv{i}.b"), ldx=cin,
-                      a_conv=(Ty, cin, pad), **({"col_stats": st} if st is not None else {}))
+            # tiles, so the statistics pass over y is skipped (_fused_stats)
+            conv = dict(bias=self.P(f"post.conv{i}.b"), ldx=cin, a_conv=(Ty, cin, pad))
+            st = self._fused_stats(tr, A[f"pcv_part{i}"], x, self.W(f"post.conv{i}.w"), y, Md, cout, K * cin, **conv)
+            self._lin(x, self.W(f"post.conv{i}.w"), y, Md, cout, K * cin, **conv,
+                      **({"col_stats": st[0]} if st is not None else {}))
             last = i == nl - 1
             out = A["mel_after"] if last else A[f"pcv_o{i}"]
             ops.batchnorm_fwd(y, self.P(f"post.bn{i}.g"), self.P(f"post.bn{i}.b"), A[f"pcv_mean{i}"],
@@ -811,8 +816,7 @@ class TTSEngine:
                               ACT_NONE if last else ACT_TANH, tr,
                               drop=self.drop(SITE_POSTNET + i, c.postnet_dropout),
                               res=res if last else None, res_ld=res_ld, eps=c.bn_eps, momentum=c.bn_momentum,
-                              ws=self.ws, sync=self.bn_sync,
-                              stats=(st, GEMM_STATS_ROWS) if st is not None else None)
+                              ws=self.ws, sync=self.bn_sync, stats=st)
             x = out
 
     # ------------------------------------------------------------ loss
@@ -862,9 +866,7 @@ class TTSEngine:
         g = A["g_after"]
         scratch = [A["g_pa"], A["g_pb"]]
         # the BatchNorm backward statistics of layer i - 1 from the conv dgrad of layer i that
-        # produces their dout (v7 LDS-image epilogue; TT2_BN_GEMM_STATS=0: the BN's own pass)
-        fused = lambda j: (self.bn_gemm_stats and cd == torch.bfloat16 and chans[j + 1] % 128 == 0  # noqa: E731
-                           and _wide(cd, (Ty, chans[j + 2], pad), Md, K * chans[j + 2]))
+        # produces their dout (_fused_stats; TT2_BN_GEMM_STATS=0: the BN's own pass)
         bstats = None   # (buf, rows) of this layer's sums, when the previous dgrad left them
         for i in reversed(range(nl)):
             cin, cout = chans[i], chans[i + 1]
@@ -885,8 +887,9 @@ class TTSEngine:
             if i > 0:
                 gn = scratch[(i + 1) % 2].view(-1)[:Md * cin].view(Md, cin)
                 j, bnb = i - 1, None
-                if fused(j):
-                    bstats = (A[f"pcv_part{j}"], GEMM_STATS_ROWS)   # (the forward's moments are consumed)
+                bstats = self._fused_stats(True, A[f"pcv_part{j}"], dyv, wflip, gn, Md, cin, K * cout, ldx=cout,
+                                           a_conv=(Ty, cout, pad))   # (the forward's moments are consumed)
+                if bstats is not None:
                     bnb = ops.bn_bwd_args(A[f"pcv_y{j}"], self.P(f"post.bn{j}.g"), self.P(f"post.bn{j}.b"),
                                           A[f"pcv_mean{j}"], A[f"pcv_rstd{j}"], Md, cin, ACT_TANH,
                                           self.drop(SITE_POSTNET + j, c.postnet_dropout), bstats)
@@ -1054,22 +1057,36 @@ class TTSEngine:
         self._wgrad(gbr, A[f"ecv_o{c.enc_conv_layers - 1}"], self.G("enc.proj.w"), d, d, Me,
                     gb=self.G("enc.proj.b"))
         gc = gxe2
-        self._dgrad(gbr, self.W("enc.proj.w"), gc, Me, d, d)
+        nl_e = c.enc_conv_layers
+
+        def enc_bnb(j, st):   # the BatchNorm backward of pre-net layer j, for the GEMM producing its dout
+            if st is None:
+                return None
+            return ops.bn_bwd_args(A[f"ecv_y{j}"], self.P(f"enc.bn{j}.g"), self.P(f"enc.bn{j}.b"),
+                                   A[f"ecv_mean{j}"], A[f"ecv_rstd{j}"], Me, d, ACT_RELU,
+                                   self.drop(SITE_ENC_CONV + j, c.prenet_dropout), st)
+        bstats = self._fused_stats(True, A[f"ecv_part{nl_e - 1}"], gbr, self.W("enc.proj.w"), gc, Me, d, d,
+                                   trans_b=True)
+        self._dgrad(gbr, self.W("enc.proj.w"), gc, Me, d, d, bn_bwd=enc_bnb(nl_e - 1, bstats))
         gdy = gres
-        for i in reversed(range(c.enc_conv_layers)):
+        for i in reversed(range(nl_e)):
             if ov:
                 gdy = gbuf("g_res", f"c{i}", (Me, d))
             ops.batchnorm_bwd(A[f"ecv_y{i}"], gc, self.P(f"enc.bn{i}.g"), self.P(f"enc.bn{i}.b"), A[f"ecv_mean{i}"],
                               A[f"ecv_rstd{i}"], gdy, self.G(f"enc.bn{i}.g"), self.G(f"enc.bn{i}.b"), Me, d,
                               ACT_RELU, drop=self.drop(SITE_ENC_CONV + i, c.prenet_dropout), ws=self.ws,
-                              sync=self.bn_sync)
+                              sync=self.bn_sync, stats=bstats)
+            bstats = None
             x_in = A[f"ecv_o{i - 1}"] if i > 0 else A["emb"]
             if ov:
                 self._pump(1)
             self._wgrad(gdy, x_in, self.G(f"enc.conv{i}.w").view(d, K * d), d, K * d, Me, ldx=d,
                         b_conv=(Tx, d, pad), gb=self.G(f"enc.conv{i}.b"))
             wflip = self._wflip(f"enc.conv{i}.w", d, d, K)
-            self._conv_dgrad(gdy, wflip, gc, Me, d, d, K, Tx)
+            if i > 0:
+                bstats = self._fused_stats(True, A[f"ecv_part{i - 1}"], gdy, wflip, gc, Me, d, K * d, ldx=d,
+                                           a_conv=(Tx, d, pad))
+            self._conv_dgrad(gdy, wflip, gc, Me, d, d, K, Tx, bn_bwd=enc_bnb(i - 1, bstats) if i > 0 else None)
         ops.embedding_bwd(A["text"], gc, self.G("enc.embed"), Me, c.vocab, pad_idx=0)
         self._ready("enc.embed")
         if ov:
@@ -1155,6 +1172,16 @@ class TTSEngine:
     def drop_pending_update(self):
         """Forget a pending pipelined update (its gradients belong to replaced weights)."""
         self.adam_gate.zero_()
+
+    def _fused_stats(self, on, buf, x, w, out, m, n, k, ldx=None, a_conv=None, trans_b=False, bias=None):
+        """(buf, rows) when the GEMM out = x W^T (or its dgrad form, trans_b) can leave a BatchNorm's
+        per-chunk statistics of out in buf (bf16, TT2_BN_GEMM_STATS; rows = its tile height), else
+        None (the BatchNorm runs its own statistics pass)."""
+        if not (on and self.bn_gemm_stats and self.cd == torch.bfloat16):
+            return None
+        rows = ops.gemm_stats_rows(x, w, out, m, n, k, ldx or k, n if trans_b else k, n, a_conv=a_conv,
+                                   trans_b=trans_b, bias=bias)
+        return (buf, rows) if rows else None
 
     def _heads_padded(self) -> bool:
         return self.cd == torch.bfloat16 and self.pad_heads

@@ -121,6 +121,12 @@ def gemm_args(a, b, c, m, n, k, lda, ldb, ldc, trans_a=False, trans_b=False, bia
     return g
 
 
+def gemm_stats_rows(a, b, c, m, n, k, lda, ldb, ldc, **kw) -> int:
+    """Rows per chunk of this request's fused BatchNorm statistics (col_stats / bn_bwd): 64 on
+    the 64 x 64 kernel, 256 on the 256 x 128 one, 0 when it cannot fuse them."""
+    return int(lib().tt2_gemm_stats_rows(C.byref(gemm_args(a, b, c, m, n, k, lda, ldb, ldc, defer_ws=True, **kw))))
+
+
 def gemm(a, b, c, m, n, k, lda, ldb, ldc, **kw):
     """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see tt2_capi.h tt2_gemm_args.
     a_ksum (f32 [m], bf16 trans_a only): a_ksum = a_ksum_beta * a_ksum + sum_k A(m,k).
@@ -129,10 +135,10 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, **kw):
     pe = (table, alpha, t_ptr): add alpha * table[*t_ptr] to every output row (skinny path).
     emit = (mel_seq, stop_seq, prev, t_ptr, seed, done, n_mels, t_max): the decode frame emit
     (see tt2_capi.h), which also advances *t_ptr.
-    col_stats (f32, 2 * ceil(m / 256) * n): the stored C's column moments per 256-row chunk
-    (mean, M2), for batchnorm_fwd(stats=(col_stats, GEMM_STATS_ROWS)); v7 LDS-image path only.
+    col_stats (f32, 2 * ceil(m / rows) * n, rows = gemm_stats_rows(...)): the stored C's column
+    moments per chunk (mean, M2), for batchnorm_fwd(stats=(col_stats, rows)).
     bn_bwd (bn_bwd_args(...)): C is that BatchNorm backward's dout; its per-chunk sums go to the
-    args' stats buffer, for batchnorm_bwd(stats=(buf, GEMM_STATS_ROWS)); same path only."""
+    args' stats buffer, for batchnorm_bwd(stats=(buf, rows))."""
     L = lib()
     g = gemm_args(a, b, c, m, n, k, lda, ldb, ldc, **kw)
     if PROBE is not None:
@@ -428,7 +434,8 @@ def _bn_stats_into(L, a, stats):
 
 def bn_bwd_args(y, gamma, beta, mean, rstd, m, c, act, drop: Drop, stats) -> _lib.BnArgs:
     """The BatchNorm backward whose column sums a GEMM producing its dout computes
-    (gemm(..., bn_bwd=...)); stats = (buf, GEMM_STATS_ROWS) as then given to batchnorm_bwd."""
+    (gemm(..., bn_bwd=...)); stats = (buf, rows) as then given to batchnorm_bwd (rows:
+    gemm_stats_rows of that GEMM)."""
     L = lib()
     a = _bn(y, gamma, beta, mean, rstd, m, c, act, True, drop, 1e-5, 0.1, None)
     _bn_stats_into(L, a, stats)
