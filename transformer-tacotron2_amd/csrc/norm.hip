@@ -175,7 +175,9 @@ __global__ __launch_bounds__(NT) void ln_combine_kernel(const T* x, const float*
 // dropout keep-mask of an element is hashed once and used for both s = x + drop(br)
 // and dbranch = drop(ds).  Per-workgroup (dgamma, dbeta, dbias) column partials go to
 // part[block][3][C]; ln_bwd_finalize sums them (fixed order: bitwise reproducible).
-constexpr int LNB_NT = 512;
+// 12 waves: 17.0-17.5 us at 12800 x 512 against 18.0-18.5 with 8 and 18.0 with 16
+// (tools/norm_ab.py, gpurun_out/r05ln)
+constexpr int LNB_NT = 768;
 template <typename T> struct LnRow { uint4 x[sizeof(T) / 2], dy[sizeof(T) / 2], br[sizeof(T) / 2]; float mean, rstd; };
 
 template <typename T>
@@ -223,7 +225,8 @@ __global__ __launch_bounds__(LNB_NT) void ln_fin_kernel(LnFin f, int C) {
 
 template <typename T>
 __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
-  __shared__ float red[3][4][512];
+  constexpr int HW = LNB_NT / 128;   // half the waves
+  __shared__ float red[3][HW][512];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c0 = lane * 8;
   float g[8];
@@ -236,8 +239,8 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) pg[j] = pb[j] = pd[j] = 0.f;
   const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
-  const int stride = gridDim.x * 8;
-  int row = blockIdx.x * 8 + w;
+  const int stride = gridDim.x * (LNB_NT / 64);
+  int row = blockIdx.x * (LNB_NT / 64) + w;
   LnRow<T> cur, nxt;
   if (row < a.M) ln_row_load<T>(cur, a, row, c0);
   for (; row < a.M; row += stride) {
@@ -281,21 +284,23 @@ __global__ __launch_bounds__(LNB_NT) void ln_bwd_kernel(LnArgs a) {
     if (a.dbranch) st8nt(reinterpret_cast<T*>(a.dbranch) + off, db);
     cur = nxt;
   }
-  // 8 waves -> 4 rows of LDS partials -> 1
-  if (w >= 4) {
+  // the waves' partials: the upper half into LDS rows, the lower half adds its own, then rows summed
+  if (w >= HW) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { red[0][w - 4][c0 + j] = pg[j]; red[1][w - 4][c0 + j] = pb[j]; red[2][w - 4][c0 + j] = pd[j]; }
+    for (int j = 0; j < 8; ++j) { red[0][w - HW][c0 + j] = pg[j]; red[1][w - HW][c0 + j] = pb[j]; red[2][w - HW][c0 + j] = pd[j]; }
   }
   __syncthreads();
-  if (w < 4) {
+  if (w < HW) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) { red[0][w][c0 + j] += pg[j]; red[1][w][c0 + j] += pb[j]; red[2][w][c0 + j] += pd[j]; }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 3 * a.C; i += LNB_NT) {
     const int which = i / a.C, c = i % a.C;
-    a.part[((int64_t)blockIdx.x * 3 + which) * a.C + c] =
-        red[which][0][c] + red[which][1][c] + red[which][2][c] + red[which][3][c];
+    float v = red[which][0][c] + red[which][1][c] + red[which][2][c] + red[which][3][c];
+#pragma unroll
+    for (int h = 4; h < HW; ++h) v += red[which][h][c];
+    a.part[((int64_t)blockIdx.x * 3 + which) * a.C + c] = v;
   }
   if (a.fin.nb) {   // the previous LayerNorm's column sums, spread over every workgroup's waves
     const int per = (3 * a.C + gridDim.x - 1) / gridDim.x;
@@ -778,7 +783,7 @@ extern "C" int tt2_layernorm_bwd(const tt2_ln_args* p, hipStream_t s) {
     if (q->m > 0) a.fin = ln_fin_of(q);
   }
   if (p->m == 0) {   // nothing of our own; still complete the chained finalize
-    if (a.fin.nb) hipLaunchKernelGGL(ln_fin_kernel, dim3((3 * p->c + 7) / 8), dim3(LNB_NT), 0, s, a.fin, p->c);
+    if (a.fin.nb) hipLaunchKernelGGL(ln_fin_kernel, dim3((3 * p->c + LNB_NT / 64 - 1) / (LNB_NT / 64)), dim3(LNB_NT), 0, s, a.fin, p->c);
     return tt2_check_launch(hipGetLastError(), "tt2_layernorm_bwd");
   }
   const int nb = ln_bwd_blocks(p->m);
@@ -794,7 +799,7 @@ extern "C" int tt2_layernorm_bwd(const tt2_ln_args* p, hipStream_t s) {
 extern "C" int tt2_layernorm_bwd_finalize(const tt2_ln_args* p, hipStream_t s) {
   if (!p->defer_finalize || !p->workspace) return tt2_set_error(TT2_E_INVALID, "tt2_layernorm_bwd_finalize: not a deferred call");
   if (p->m == 0) return TT2_OK;
-  hipLaunchKernelGGL(ln_fin_kernel, dim3((3 * p->c + 7) / 8), dim3(LNB_NT), 0, s, ln_fin_of(p), p->c);
+  hipLaunchKernelGGL(ln_fin_kernel, dim3((3 * p->c + LNB_NT / 64 - 1) / (LNB_NT / 64)), dim3(LNB_NT), 0, s, ln_fin_of(p), p->c);
   return tt2_check_launch(hipGetLastError(), "tt2_layernorm_bwd_finalize");
 }
 
