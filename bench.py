@@ -243,10 +243,10 @@ def gemm_kernel_name(plan: int, ta: int, tb: int) -> str:
         return f"gemm2_kernel<{ak}, {bk}>"
     if plan == 3:
         return "gemm_skinny_kernel"
-    if plan == 13:
-        return f"gemm7_kernel<{ak}, {bk}>"
+    if plan == 13:   # (the third argument: the fused-statistics epilogue, 0 = none)
+        return f"gemm7_kernel<{ak}, {bk}, 0>"
     if plan == 15:
-        return f"gemm8_kernel<{bk}>"
+        return f"gemm8_kernel<{bk}, 0>"
     if plan == 16:
         return "gemm10_kernel"
     if plan == 1:
@@ -338,7 +338,7 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
     achieved = flops / secs / 1e12
     kname = gemm_kernel_name(*key[1:4])
     if key[0] == "gemm_grouped":
-        kname = kname.replace("gemm7_kernel", "gemm7g_kernel")
+        kname = kname.replace("gemm7_kernel", "gemm7g_kernel").replace(", 0>", ">")
     traffic, tsrc = None, None
     prof = os.path.join(ROOT, "profiles")
     tfiles = sorted(f for f in os.listdir(prof) if f.endswith("_traffic.json")
@@ -365,7 +365,7 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
         "all_gemms": {"launches": round(sum(v[0] for v in allg.values())), "ms_per_step": round(tot_t * 1e3, 3),
                       "tflops": round(tot_f / tot_t / 1e12, 1)},
         # the four GEMM variants with the most in-step device time, same timing as above
-        "top_gemms": [{"kernel": (gemm_kernel_name(*k[1:4]).replace("gemm7_kernel", "gemm7g_kernel")
+        "top_gemms": [{"kernel": (gemm_kernel_name(*k[1:4]).replace("gemm7_kernel", "gemm7g_kernel").replace(", 0>", ">")
                                   if k[0] == "gemm_grouped" else gemm_kernel_name(*k[1:4])),
                        "launches": round(v[0]), "avg_launch_us": round(v[2] / v[0] * 1e6, 2),
                        "frac": round(v[1] / v[2] / 1e12 / PEAK_BF16_TFLOPS, 4)}

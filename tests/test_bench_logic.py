@@ -42,7 +42,7 @@ def test_roofline_detaches_dp_hook(monkeypatch):
     assert m.hook_seen is None                      # no all-reduce from the rank-0-only step
     assert m.engine.grad_ready_hook == "dp-hook"    # restored for later steps
     assert ops.PROBE is None
-    assert r["kernel"] == "gemm7_kernel<true, true>" and r["launches_per_step"] == 2
+    assert r["kernel"] == "gemm7_kernel<true, true, 0>" and r["launches_per_step"] == 2
     assert abs(r["achieved"] - 2000.0) < 1e-6 and r["bound"] == "mfma"
 
 

@@ -32,7 +32,8 @@ def short(name: str) -> str:
 
 def main(tag: str, src: str | None = None):
     src = src or os.path.join(ROOT, "gpurun_out", tag)
-    trace = next((os.path.join(d, f) for d, _, fs in os.walk(src) for f in fs if f.endswith("kernel_trace.csv")), None)
+    kt = os.path.join(src, "kt") if os.path.isdir(os.path.join(src, "kt")) else src   # not dk/ (decode)
+    trace = next((os.path.join(d, f) for d, _, fs in os.walk(kt) for f in fs if f.endswith("kernel_trace.csv")), None)
     if trace is None:
         raise SystemExit(f"no *kernel_trace.csv under {src}")
     bench = json.loads([ln for ln in open(os.path.join(src, "bench_step.json")) if ln.startswith("{")][-1])
