@@ -58,3 +58,37 @@ def test_explicit_variants():
     assert plan(12800, 2048, 512, variant=13) == 13
     assert plan(12800, 512, 512, variant=16) == 16
     assert plan(12800, 2048, 512, trans_b=True, variant=16) != 16   # v10 is NT only
+
+
+_L.tt2_gemm_stats_rows.argtypes = [C.POINTER(_lib.GemmArgs)]
+_L.tt2_gemm_stats_rows.restype = C.c_int32
+
+
+def stats_rows(m, n, k, trans_a=False, trans_b=False, splits=1, dtype_out=DT_BF16, conv=None):
+    """tt2_gemm_stats_rows: the chunk height of a fused BatchNorm statistics request (host code)"""
+    g = _lib.GemmArgs()
+    g.a, g.b, g.c = _A.data_ptr(), _A.data_ptr(), _C.data_ptr()
+    g.m, g.n, g.k = m, n, k
+    g.lda, g.ldb, g.ldc = m if trans_a else k, n if trans_b else k, n
+    if conv is not None:
+        g.a_conv_t, g.a_conv_c, g.a_conv_pad = conv
+        g.lda = conv[1]
+    g.dtype_in, g.dtype_out = DT_BF16, dtype_out
+    g.trans_a, g.trans_b = int(trans_a), int(trans_b)
+    g.alpha = 1.0
+    g.splits = splits
+    return _L.tt2_gemm_stats_rows(C.byref(g))
+
+
+def test_fused_statistics_chunk_height():
+    # the post-net conv (v7: 256-row chunks) and the encoder pre-net conv (v8: 64-row chunks)
+    assert stats_rows(12800, 512, 2560, conv=(800, 512, 2)) == 256
+    assert stats_rows(2048, 512, 2560, conv=(128, 512, 2)) == 64
+    assert stats_rows(2048, 512, 512, trans_b=True) == 64        # the pre-net projection's dgrad (v8)
+    # a request that plans v10 falls back to v7's image epilogue; split-K, f32 C, n % 128 on v7
+    # and a transposed v7 operand cannot carry the statistics
+    assert stats_rows(12800, 2048, 512) == 256
+    assert stats_rows(12800, 512, 2560, conv=(800, 512, 2), splits=2) == 0
+    assert stats_rows(12800, 512, 512, dtype_out=0) == 0
+    assert stats_rows(12800, 576, 512) == 0
+    assert stats_rows(12800, 512, 512, trans_b=True) == 0
