@@ -1,5 +1,5 @@
 """The training step's LayerNorm / BatchNorm passes on their own (dev tool, GPU): the decoder's
-LayerNorm backward (12800 x 512, residual branch, dropout) and the post-net's BatchNorm forward
+LayerNorm forward and backward (12800 x 512, residual branch, dropout) and the post-net's BatchNorm forward
 and backward (12800 x 512, tanh, dropout), each as 10 launches replayed from a hipGraph (best
 of 3), plus a checksum so two builds (TT2_LIB=...) can be compared bit for bit.
 
@@ -33,6 +33,8 @@ def main():
     ws = ops.Workspace()
     ln = lambda: ops.layernorm_bwd(dy, x, br, g, mean, rstd, dx, dbr, dg, db, M, drop=drop, ws=ws)  # noqa: E731
     t_ln = min(time_graph(graph_of(ln)) for _ in range(3))
+    lnf = lambda: ops.layernorm_fwd(x, br, g, b, y, mean, rstd, M, drop=drop)  # noqa: E731
+    t_lnf = min(time_graph(graph_of(lnf)) for _ in range(3))
     bm, br_ = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
     rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
     out = torch.empty_like(x)
@@ -43,7 +45,8 @@ def main():
     t_bnb = min(time_graph(graph_of(bnb)) for _ in range(3))
     torch.cuda.synchronize()
     cs = [t.float().sum().item() for t in (dx, dbr, dg, db, out, bm, br_, dyb, dgb, dbb)]
-    print(f"lib {os.environ.get('TT2_LIB', 'default')}: ln_bwd {t_ln * 1e6:.2f} us | bn_fwd {t_bnf * 1e6:.2f} us | "
+    print(f"lib {os.environ.get('TT2_LIB', 'default')}: ln_fwd {t_lnf * 1e6:.2f} us | ln_bwd {t_ln * 1e6:.2f} us | "
+          f"bn_fwd {t_bnf * 1e6:.2f} us | "
           f"bn_bwd {t_bnb * 1e6:.2f} us | checksums {' '.join(f'{v:.9e}' for v in cs)}", flush=True)
 
 
