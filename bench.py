@@ -254,12 +254,16 @@ def gemm_kernel_name(plan: int, ta: int, tb: int) -> str:
     return f"gemm plan {plan}"
 
 
-def graph_probe(model, text, tl, mel, ml, reps: int = 5):
+def graph_probe(model, text, tl, mel, ml, reps: int = 5, serial: bool = False):
     """Per-launch GEMM times inside GRAPH-REPLAYED steps: the training step is captured once
     more with libtt2's launch probe armed for every GEMM (under capture each v7 / v8 kernel
     records only its own wall-clock span; nothing is added to the graph), replayed `reps`
     times, and each replay's spans read back.  Returns {key: [launches/step, flops, seconds,
-    bytes]} averaged over the replays, or None if a probed launch recorded no span."""
+    bytes]} averaged over the replays, or None if a probed launch recorded no span.
+    serial: the engine's side stream (overlapped weight gradients, encoder forward) is the
+    capture stream itself, so the step's launches run one after another in issue order, as
+    rocprofv3's kernel trace serialises them: each span is then the kernel's own duration,
+    not its duration while another stream holds part of the chip."""
     from tt2 import ops
     eng = model.engine
     B, Tx, Ty = text.shape[0], text.shape[1], mel.shape[1]
@@ -270,6 +274,11 @@ def graph_probe(model, text, tl, mel, ml, reps: int = 5):
     s.wait_stream(torch.cuda.current_stream())
     torch.cuda.synchronize()
     nbt = dict(eng.nbt)
+    side = eng._side
+    if serial:
+        eng._side = s
+        if eng._side_ws is None:
+            eng._side_ws = ops.Workspace()
     ops.PROBE = probe
     try:
         with torch.cuda.graph(g, stream=s, capture_error_mode=ops.CAPTURE_MODE):
@@ -277,6 +286,7 @@ def graph_probe(model, text, tl, mel, ml, reps: int = 5):
     finally:
         ops.PROBE = None
         eng.nbt = nbt
+        eng._side = side
     torch.cuda.current_stream().wait_stream(s)
     acc: dict = {}
     try:
@@ -311,6 +321,7 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
         model.train_step(text, tl, mel, ml)
         summ = probe.summary()
         gsum = graph_probe(model, text, tl, mel, ml) if text is not None else None
+        gser = graph_probe(model, text, tl, mel, ml, serial=True) if gsum else None
     finally:
         ops.PROBE = None
         eng.grad_ready_hook = hook
@@ -319,20 +330,32 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
     # dominant = the GEMM variant with the most device time
     key, (n, flops, secs, abytes) = max(summ.items(), key=lambda kv: kv[1][2])
     eager_us = secs / n * 1e6
-    gk = (gsum or {}).get(key)
+    gk, gs = (gsum or {}).get(key), (gser or {}).get(key)
+    conc = None
     if gk:
-        # the launches inside the replayed step graph, as the timed steps run them (rocprofv3's
-        # average over the timed replays agrees, profiles/r03*_step_kernels.md)
-        secs = gk[2] * n / gk[0]
+        # beside it: the same launches in the timed step's own schedule, where the side stream's
+        # weight-gradient GEMMs hold part of the chip while the main stream's kernels run
+        conc = {"avg_launch_us": round(gk[2] / gk[0] * 1e6, 2),
+                "frac": round(gk[1] / gk[2] / 1e12 / PEAK_BF16_TFLOPS, 4),
+                "all_gemms_ms_per_step": round(sum(v[2] for v in gsum.values()) * 1e3, 3)}
+    if gs:
+        # the launches inside the replayed step graph with the streams serialised in issue
+        # order, as rocprofv3's kernel trace runs them (its average agrees, profiles/*_step_kernels.md)
+        secs = gs[2] * n / gs[0]
         timing = ("in-step kernel spans (tt2_probe_span_ms: device wall clock, first workgroup start to last "
-                  "wave end) of the launches inside graph-replayed training steps, mean of 5 replays")
+                  "wave end) of the launches inside graph-replayed training steps, streams serialised in "
+                  "issue order as under rocprofv3, mean of 5 replays")
+    elif gk:
+        secs = gk[2] * n / gk[0]
+        timing = ("in-step kernel spans (tt2_probe_span_ms) of the launches inside graph-replayed training "
+                  "steps, mean of 5 replays")
     else:
         timing = "in-step kernel dispatch events (tt2_probe_arm: the kernel's own dispatch records them), eager step"
     # beside it, for reference only: the eager step's dispatch events (each carries the
     # event's completion signal and host-gap clocks, reads high) and a back-to-back replay
     # of the same launches (warm caches, no step context).
     replay = probe.replay_time(key) if replay else None
-    allg = gsum if gk else summ
+    allg = gser if gs else (gsum if gk else summ)
     tot_t = sum(v[2] for v in allg.values())
     tot_f = sum(v[1] for v in allg.values())
     achieved = flops / secs / 1e12
@@ -362,6 +385,7 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
         "avg_launch_us": round(secs / n * 1e6, 2), "timing": timing,
         "eager_dispatch_avg_launch_us": round(eager_us, 2),
         "replay_avg_launch_us": round(replay / n * 1e6, 2) if replay is not None else None,
+        "concurrent": conc,
         "all_gemms": {"launches": round(sum(v[0] for v in allg.values())), "ms_per_step": round(tot_t * 1e3, 3),
                       "tflops": round(tot_f / tot_t / 1e12, 1)},
         # the four GEMM variants with the most in-step device time, same timing as above

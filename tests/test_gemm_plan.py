@@ -92,3 +92,24 @@ def test_fused_statistics_chunk_height():
     assert stats_rows(12800, 512, 512, dtype_out=0) == 0
     assert stats_rows(12800, 576, 512) == 0
     assert stats_rows(12800, 512, 512, trans_b=True) == 0
+
+
+def test_algorithmic_bytes_count_epilogue_inputs_and_unique_conv_rows():
+    """bench.py's roofline bytes per GEMM (tt2.ops.gemm_algo_bytes): operands and C once, each
+    epilogue input once, an implicit-im2col operand as its unique rows."""
+    from tt2.ops import gemm_algo_bytes
+    g = _lib.GemmArgs()
+    g.m, g.n, g.k = 12800, 512, 2048
+    g.dtype_in = g.dtype_out = DT_BF16
+    g.alpha, g.beta = 1.0, 0.0
+    base = 2 * (12800 * 2048 + 512 * 2048) + 2 * 12800 * 512
+    assert gemm_algo_bytes(g) == base
+    g.res, g.res_dtype = _A.data_ptr(), DT_BF16
+    g.gate, g.gate_dtype = _A.data_ptr(), DT_BF16
+    g.bias = _BIAS.data_ptr()
+    assert gemm_algo_bytes(g) == base + 2 * (2 * 12800 * 512) + 4 * 512
+    c = _lib.GemmArgs()   # post-net conv: k = 5 taps x 512 channels, A read as 12800 x 512
+    c.m, c.n, c.k = 12800, 512, 2560
+    c.dtype_in = c.dtype_out = DT_BF16
+    c.a_conv_t, c.a_conv_c, c.a_conv_pad = 800, 512, 2
+    assert gemm_algo_bytes(c) == 2 * (12800 * 512 + 512 * 2560) + 2 * 12800 * 512

@@ -78,6 +78,26 @@ def main(tag: str):
                            "write_bytes_per_launch": write, "hbm_bytes_per_launch": fetch + write,
                            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; FETCH_SIZE x2 "
                                      "(gfx950 counts 128-B requests as 64 B), KiB -> bytes"}
+        # per launch shape (grid size) of the dominant kernel: which launches re-read
+        by_grid = {}
+        for path, cname, col in ((fpath, "FETCH_SIZE", 0), (wpath, "WRITE_SIZE", 1)):
+            with open(path) as f:
+                for r in csv.DictReader(f):
+                    if r["Counter_Name"] == cname and DOMINANT in r["Kernel_Name"]:
+                        d = by_grid.setdefault(int(float(r.get("Grid_Size", 0))), [0, 0.0, 0, 0.0])
+                        d[2 * col] += 1
+                        d[2 * col + 1] += float(r["Counter_Value"]) * 1024.0 * (2.0 if col == 0 else 1.0)
+        if traffic:
+            # every kernel's PMC bytes per dispatch, the 12 with the most fetched bytes
+            top = sorted(fe.items(), key=lambda kv: -kv[1][1])[:12]
+            traffic["top_kernels"] = {
+                name.split("(")[0][:80]: {"dispatches": n, "fetch_bytes": round(2.0 * v / n * 1024.0),
+                                          "write_bytes": round(wr.get(name, (1, 0.0))[1] / max(wr.get(name, (1, 0.0))[0], 1)
+                                                               * 1024.0)}
+                for name, (n, v) in top}
+            traffic["by_grid_size"] = {str(g): {"fetch_bytes": round(v[1] / max(v[0], 1)),
+                                                "write_bytes": round(v[3] / max(v[2], 1)),
+                                                "dispatches": v[0]} for g, v in sorted(by_grid.items())}
         lines += ["", "PMC HBM traffic of the dominant kernel (separate --pmc passes): "
                       f"{json.dumps(traffic)}"]
     open(os.path.join(dst, f"{tag}_kernel_stats.md"), "w").write("\n".join(lines) + "\n")

@@ -1289,7 +1289,12 @@ TT2_DEV void g7_store_c(const G7Prob& P, char* smem, int m0, int n0, int nkt) {
 }
 
 // Loader waves: stage rows [r0, r0 + 4 * ni * 4) of the residual / gate tile (bf16, 16-B
-// aligned rows) into the image, ni copies per wave (rows past M repeat row M - 1).
+// aligned rows) into the image, ni copies per wave (rows past M repeat row M - 1).  The copies
+// are nontemporal (G7_X_AUX 2 = nt): each line is read once, and as default-policy lines they
+// pushed the B operand, which every row tile of the launch re-reads, out of the XCD's L2.
+#ifndef G7_X_AUX
+#define G7_X_AUX 2
+#endif
 TT2_DEV void g7_issue_x(const G7Prob& P, const void* x, int64_t ldx, char* smem, int nkt, int m0, int n0, int r0,
                         int ni, int lane, int lw) {
   const char* base = reinterpret_cast<const char*>(x);
@@ -1297,7 +1302,7 @@ TT2_DEV void g7_issue_x(const G7Prob& P, const void* x, int64_t ldx, char* smem,
     const int inst = lw * ni + i, r = r0 + inst * 4 + (lane >> 4);
     const int m = min(m0 + r, P.M - 1), c = (lane & 15) ^ (r & 15);
     __builtin_amdgcn_global_load_lds((gvoid_t*)(base + ((int64_t)m * ldx + n0 + 8 * c) * 2),
-                                     (lvoid_t*)(smem + g7_img_row(nkt, r0 + inst * 4)), 16, 0, 0);
+                                     (lvoid_t*)(smem + g7_img_row(nkt, r0 + inst * 4)), 16, 0, G7_X_AUX);
   }
 }
 

@@ -127,6 +127,30 @@ def gemm_stats_rows(a, b, c, m, n, k, lda, ldb, ldc, **kw) -> int:
     return int(lib().tt2_gemm_stats_rows(C.byref(gemm_args(a, b, c, m, n, k, lda, ldb, ldc, defer_ws=True, **kw))))
 
 
+def gemm_algo_bytes(g) -> int:
+    """Algorithmic HBM bytes of one GEMM request: each operand once (an implicit-im2col
+    operand as its unique sequence rows, not the tap-expanded matrix), C once, and every
+    epilogue input once (residual, gate, beta * C, the BatchNorm rows of a bn_bwd epilogue,
+    bias)."""
+    esz = 2 if g.dtype_in == _lib.DT_BF16 else 4
+    sz = lambda d: 2 if d == _lib.DT_BF16 else 4  # noqa: E731
+    mn = g.m * g.n
+    a_b = esz * g.m * (g.a_conv_c if g.a_conv_t > 0 else g.k)
+    b_b = esz * (g.k * g.b_conv_c if g.b_conv_t > 0 else g.n * g.k)
+    out = a_b + b_b + sz(g.dtype_out) * mn
+    if g.res:
+        out += sz(g.res_dtype) * mn
+    if g.gate:
+        out += sz(g.gate_dtype) * mn
+    if g.beta != 0.0:
+        out += sz(g.dtype_out) * mn
+    if g.bn_bwd:
+        out += 2 * mn
+    if g.bias:
+        out += 4 * g.n
+    return out
+
+
 def gemm(a, b, c, m, n, k, lda, ldb, ldc, **kw):
     """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); see tt2_capi.h tt2_gemm_args.
     a_ksum (f32 [m], bf16 trans_a only): a_ksum = a_ksum_beta * a_ksum + sum_k A(m,k).
@@ -143,8 +167,7 @@ def gemm(a, b, c, m, n, k, lda, ldb, ldc, **kw):
     g = gemm_args(a, b, c, m, n, k, lda, ldb, ldc, **kw)
     if PROBE is not None:
         key = ("gemm", L.tt2_gemm_plan(C.byref(g)), g.trans_a, g.trans_b)
-        esz = 2 if g.dtype_in == _lib.DT_BF16 else 4
-        algo_bytes = esz * (m * k + n * k) + (2 if g.dtype_out == _lib.DT_BF16 else 4) * m * n
+        algo_bytes = gemm_algo_bytes(g)
         PROBE.begin()
         check(L.tt2_gemm(C.byref(g), stream_ptr()), "tt2_gemm")
         PROBE.end(key, 2.0 * m * n * k, algo_bytes, [g])
@@ -175,7 +198,7 @@ def gemm_grouped(problems, ws: Workspace | None = None, fin=None, max_groups: in
     if PROBE is not None:
         key = ("gemm_grouped", 13, arr[0].trans_a, arr[0].trans_b)
         flops = sum(2.0 * g.m * g.n * g.k for g in arr)
-        ab = sum(2 * (g.m * g.k + g.n * g.k) + (2 if g.dtype_out == _lib.DT_BF16 else 4) * g.m * g.n for g in arr)
+        ab = sum(gemm_algo_bytes(g) for g in arr)
         PROBE.begin()
         check(L.tt2_gemm_grouped_ex(arr, len(problems), finp, max_groups, stream_ptr()), "tt2_gemm_grouped")
         PROBE.end(key, flops, ab, list(arr))
