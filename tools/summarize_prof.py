@@ -91,7 +91,7 @@ def main(tag: str):
             # every kernel's PMC bytes per dispatch, the 12 with the most fetched bytes
             top = sorted(fe.items(), key=lambda kv: -kv[1][1])[:12]
             traffic["top_kernels"] = {
-                name.split("(")[0][:80]: {"dispatches": n, "fetch_bytes": round(2.0 * v / n * 1024.0),
+                name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:80]: {"dispatches": n, "fetch_bytes": round(2.0 * v / n * 1024.0),
                                           "write_bytes": round(wr.get(name, (1, 0.0))[1] / max(wr.get(name, (1, 0.0))[0], 1)
                                                                * 1024.0)}
                 for name, (n, v) in top}
