@@ -392,6 +392,7 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
         "top_gemms": [{"kernel": (gemm_kernel_name(*k[1:4]).replace("gemm7_kernel", "gemm7g_kernel").replace(", 0>", ">")
                                   if k[0] == "gemm_grouped" else gemm_kernel_name(*k[1:4])),
                        "launches": round(v[0]), "avg_launch_us": round(v[2] / v[0] * 1e6, 2),
+                       "algo_mb_per_step": round(v[3] / 1e6, 1),
                        "frac": round(v[1] / v[2] / 1e12 / PEAK_BF16_TFLOPS, 4)}
                       for k, v in sorted(allg.items(), key=lambda kv: -kv[1][2])[:4]],
     }
