@@ -59,41 +59,47 @@ struct DecArgs {
 };
 
 // q-prologue (wq != null): this head's 64 query values from the projection input row x[b]
-// (H*64 wide): wave w computes output rows 8w .. 8w+7 (NW = 8), eight lanes per row, each lane
-// 64 consecutive k (8 x 16-B chunks of W and of x, all issued before the first FMA); the eight
-// partials of a row meet by xor shuffles.  Result (f32, + bias) in sq[64].
+// (H*64 wide): wave w computes output rows 8w .. 8w+7 (NW = 8), eight lanes per row; load i
+// of lane c covers k = 64 i + 8 c .. + 7, so each wave instruction reads 8 whole 128-B row
+// segments (lanes 64 consecutive k each touched 64 lines per instruction: 3.8 us of the
+// launch); all 8 loads issued before the first FMA; the eight partials of a row meet by xor
+// shuffles.  Result (f32, + bias) in sq[64].
 // The projection weights are loaded first (qproj_w: they do not depend on x, so their latency
 // overlaps the fused LayerNorm prologue); sx: the input row already in LDS (f32 values of T,
 // that prologue), or null (x read from q).
+template <typename T>
+using T8 = T __attribute__((ext_vector_type(8)));
+// the raw rows (converted at their use in qproj, so no wait for them is placed before the
+// loads that follow: they are issued first thing in the kernel)
 template <typename T, int NW>
-TT2_DEV void qproj_w(const DecArgs& a, int h, float (&wv)[8][8]) {
+TT2_DEV void qproj_w(const DecArgs& a, int h, T8<T> (&wraw)[8]) {
   static_assert(NW == 8, "one wave per 8 query rows");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 7, g = lane >> 3;
   const int r = h * D + 8 * w + g;   // output feature
-  const T* wr = reinterpret_cast<const T*>(a.wq) + (int64_t)r * a.wq_ld + 64 * c;
+  const T* wr = reinterpret_cast<const T*>(a.wq) + (int64_t)r * a.wq_ld + 8 * c;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) load8f(wr + 8 * i, wv[i]);
+  for (int i = 0; i < 8; ++i) wraw[i] = *reinterpret_cast<const T8<T>*>(wr + 64 * i);
 }
 template <typename T, int NW>
-TT2_DEV void qproj(const DecArgs& a, int b, int h, float* sq, const float* sx, const float (&wv)[8][8]) {
+TT2_DEV void qproj(const DecArgs& a, int b, int h, float* sq, const float* sx, const T8<T> (&wraw)[8]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 7, g = lane >> 3;
   const int r = h * D + 8 * w + g;   // output feature
-  const T* x = reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld + 64 * c;
+  const T* x = reinterpret_cast<const T*>(a.q) + (int64_t)b * a.q_ld + 8 * c;
   float xv[8][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     if (sx) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xv[i][j] = sx[64 * c + 8 * i + j];
+      for (int j = 0; j < 8; ++j) xv[i][j] = sx[64 * i + 8 * c + j];
     } else {
-      load8f(x + 8 * i, xv[i]);
+      load8f(x + 64 * i, xv[i]);
     }
   }
   float p = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) p += xv[i][j] * wv[i][j];
+    for (int j = 0; j < 8; ++j) p += xv[i][j] * (float)wraw[i][j];
   p += __shfl_xor(p, 1, 64);
   p += __shfl_xor(p, 2, 64);
   p += __shfl_xor(p, 4, 64);
@@ -108,8 +114,6 @@ TT2_DEV void qproj(const DecArgs& a, int b, int h, float* sq, const float* sx, c
 // pre: this wave's first 8 rows, loaded by oproj_prefetch at the start of the kernel (behind the
 // first keys, so no earlier wait drains them): the projection then costs no memory round trip
 // of its own when H * 64 == NW * 64 (one row block per wave)
-template <typename T>
-using T8 = T __attribute__((ext_vector_type(8)));
 template <typename T, int NW>
 TT2_DEV void oproj_prefetch(const DecArgs& a, int h, T8<T> (&pre)[8]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = lane & 7, g = lane >> 3;
@@ -171,6 +175,16 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
     }
     if (h == 0) *reinterpret_cast<t8*>(reinterpret_cast<T*>(a.ln_out) + (int64_t)b * 512 + lane * 8) = y;
   };
+  // the weights first: they depend on nothing the kernel reads (step, stop, key counts), so their
+  // memory round trip overlaps those scalar loads instead of following them
+  T8<T> wpre[8];   // 16-bit types only: the f32 (parity-mode) kernel has no registers to spare
+  if constexpr (sizeof(T) == 2) {
+    // only waves that own a row block (w * 64 < H * 64): with fewer heads than waves the
+    // rows past N do not exist (oproj_slab's loop then skips the wave too)
+    if (a.wo && w * 64 < a.H * D) oproj_prefetch<T, NW>(a, h, wpre);
+  }
+  T8<T> wq[8];
+  if (a.wq) qproj_w<T, NW>(a, h, wq);
   if (a.stop_len && *a.step >= a.stop_len[b]) {
     if (a.ln_part) ln_prologue();   // the row stays defined for the sublayers after this one
     // a finished utterance: its frames past the stop are discarded, so skip the key stream
@@ -206,21 +220,13 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(DecArgs a) {
   };
   // the first iteration's keys do not depend on the query: in flight during its projection
   if (k0 < k1) load_keys(k0, 0);
-  T8<T> wpre[8];   // 16-bit types only: the f32 (parity-mode) kernel has no registers to spare
-  if constexpr (sizeof(T) == 2) {
-    // only waves that own a row block (w * 64 < H * 64): with fewer heads than waves the
-    // rows past N do not exist (oproj_slab's loop then skips the wave too)
-    if (a.wo && (int)(threadIdx.x >> 6) * 64 < a.H * D) oproj_prefetch<T, NW>(a, h, wpre);
-  }
   float qv[8];
   if (a.wq) {
-    float wv[8][8];
-    qproj_w<T, NW>(a, h, wv);
     if (a.ln_part) {   // the projection input row: residual combine + LayerNorm, rounded to T
       ln_prologue();
       __syncthreads();
     }
-    qproj<T, NW>(a, b, h, sq, a.ln_part ? sx : nullptr, wv);
+    qproj<T, NW>(a, b, h, sq, a.ln_part ? sx : nullptr, wq);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 8; ++j) qv[j] = sq[dc * 8 + j];
