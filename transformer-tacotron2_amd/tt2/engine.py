@@ -46,13 +46,13 @@ def _wide(dtype, conv, m: int, *inner: int) -> bool:
     return dtype == torch.bfloat16 and conv_ok and m > 32 and all(d % 8 == 0 for d in inner)
 
 
-def auto_splits(n_out: int, n_in: int, k: int, wide: bool = False) -> int:
+def auto_splits(n_out: int, n_in: int, k: int, wide: bool = False, items: int = 256) -> int:
     """Split-K factor for a weight-gradient GEMM (long K = tokens, few output tiles).
-    v7 (256 x 128 tiles): ~256 workgroups, >= 512 k each, at most 16 slabs (measured:
+    v7 (256 x 128 tiles): ~`items` workgroups, >= 512 k each, at most 16 slabs (measured alone:
     512x512x12800 sp16 < sp32 < sp8; 2048x512x12800 sp8 best)."""
     if wide:
         tiles = ((n_out + 255) // 256) * ((n_in + 127) // 128)
-        return max(1, min(16, 256 // tiles, k // 512))
+        return max(1, min(16, items // tiles, k // 512))
     tiles = ((n_out + 127) // 128) * ((n_in + 127) // 128)
     if tiles >= 256:
         return 1
@@ -238,6 +238,9 @@ class TTSEngine:
         self._norm_buf = None
         self._norm_pending = None   # (ranges, computed on the side stream) of the last overlapped backward
         self.side_split = int(os.environ.get("TT2_SIDE_SPLIT", "1"))
+        # work items a grouped weight-gradient launch aims at (its split-K factor: items / tiles)
+        self.wgrad_items = int(os.environ.get("TT2_WGRAD_ITEMS", "128"))
+        self.wgrad_items_direct = int(os.environ.get("TT2_WGRAD_DIRECT", "128"))   # the ungrouped ones
         self.side_groups = int(os.environ.get("TT2_SIDE_WG", "0"))
         # ... for the jobs issued while the decoder backward runs (side_start >= 0): the 200-tile
         # N = 512 dgrads there leave 56 CUs idle, which a capped side grid can fill
@@ -374,7 +377,7 @@ class TTSEngine:
                 # schedule sums every weight gradient in the same order (bit-identical)
                 req = {"direct": dict(a=dy, b=x, c=gw, m=n_out, n=n_in, k=m, lda=ldy or n_out, ldb=ldx or n_in,
                                       ldc=n_in, trans_a=True, trans_b=True, b_conv=b_conv, a_ksum=gb,
-                                      splits=auto_splits(n_out, n_in, m, True))}
+                                      splits=auto_splits(n_out, n_in, m, True, self.wgrad_items_direct))}
                 if self._wq is None:
                     self._wq = []
             else:
@@ -385,7 +388,8 @@ class TTSEngine:
         # the fused path rides on the LDS-DMA kernel: bf16 with 8-aligned M and N
         fused = gb is not None and dy.dtype == torch.bfloat16 and n_out % 8 == 0 and n_in % 8 == 0
         ops.gemm(dy, x, gw, n_out, n_in, m, ldy or n_out, ldx or n_in, n_in, trans_a=True, trans_b=True,
-                 splits=auto_splits(n_out, n_in, m, _wide(dy.dtype, b_conv, n_out, n_out, n_in)), b_conv=b_conv, ws=self.ws,
+                 splits=auto_splits(n_out, n_in, m, _wide(dy.dtype, b_conv, n_out, n_out, n_in), self.wgrad_items_direct),
+                 b_conv=b_conv, ws=self.ws,
                  a_ksum=gb if fused else None)
         if gb is not None and not fused:
             self._bias(dy, ldy or n_out, m, n_out, gb)
@@ -455,7 +459,7 @@ class TTSEngine:
             grp = q[i:i + 8]
             tiles = sum(((p["m"] + 255) // 256) * ((p["n"] + 127) // 128) for p in grp)
             kmin = min(p["k"] for p in grp)
-            sp = max(1, min(16, 256 // tiles, kmin // 512))
+            sp = max(1, min(16, self.wgrad_items // tiles, kmin // 512))
             if side:   # beside the encoder backward: shorter items, a capped grid
                 sp = max(1, min(16 * self.side_split, sp * self.side_split, kmin // 256))
             ops.gemm_grouped([dict(p, splits=sp) for p in grp], ws=ws, fin=fin if i == 0 else None,
