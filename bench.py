@@ -259,7 +259,8 @@ def graph_probe(model, text, tl, mel, ml, reps: int = 5, serial: bool = False):
     more with libtt2's launch probe armed for every GEMM (under capture each v7 / v8 kernel
     records only its own wall-clock span; nothing is added to the graph), replayed `reps`
     times, and each replay's spans read back.  Returns {key: [launches/step, flops, seconds,
-    bytes]} averaged over the replays, or None if a probed launch recorded no span.
+    bytes]} averaged over the replays (and, as acc["_wgs"], the work groups of each grouped
+    launch: {key: [per launch]}), or None if a probed launch recorded no span.
     serial: the engine's side stream (overlapped weight gradients, encoder forward) is the
     capture stream itself, so the step's launches run one after another in issue order, as
     rocprofv3's kernel trace serialises them: each span is then the kernel's own duration,
@@ -304,6 +305,8 @@ def graph_probe(model, text, tl, mel, ml, reps: int = 5, serial: bool = False):
     finally:
         probe.close()
         del g
+    acc["_wgs"] = dict(probe.wgs)     # per grouped call: its work groups
+    acc["_disp"] = dict(probe.disp)   # per call: its kernel dispatches (capped grouped grids: several)
     return acc
 
 
@@ -328,25 +331,35 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
         if hasattr(probe, "close"):
             probe.close()
     # dominant = the GEMM variant with the most device time
-    key, (n, flops, secs, abytes) = max(summ.items(), key=lambda kv: kv[1][2])
+    key, (n_calls, flops, secs, abytes) = max(summ.items(), key=lambda kv: kv[1][2])
+    wgs_ser = (gser or {}).pop("_wgs", {})
+    disp_calls = (gser or {}).pop("_disp", None) or dict(getattr(probe, "disp", {}))
+    for d in (gsum, gser):
+        if d:
+            d.pop("_wgs", None)
+            d.pop("_disp", None)
+    # counted per kernel DISPATCH, as rocprofv3 counts them: a grouped call whose grid is capped
+    # (the side stream's weight gradients) goes out as several consecutive launches
+    ndisp = {k: sum(v) for k, v in disp_calls.items()}
+    n = ndisp.get(key, n_calls)
     eager_us = secs / n * 1e6
     gk, gs = (gsum or {}).get(key), (gser or {}).get(key)
     conc = None
     if gk:
         # beside it: the same launches in the timed step's own schedule, where the side stream's
         # weight-gradient GEMMs hold part of the chip while the main stream's kernels run
-        conc = {"avg_launch_us": round(gk[2] / gk[0] * 1e6, 2),
+        conc = {"avg_launch_us": round(gk[2] / n * 1e6, 2),
                 "frac": round(gk[1] / gk[2] / 1e12 / PEAK_BF16_TFLOPS, 4),
                 "all_gemms_ms_per_step": round(sum(v[2] for v in gsum.values()) * 1e3, 3)}
     if gs:
         # the launches inside the replayed step graph with the streams serialised in issue
         # order, as rocprofv3's kernel trace runs them (its average agrees, profiles/*_step_kernels.md)
-        secs = gs[2] * n / gs[0]
+        secs = gs[2] * n_calls / gs[0]
         timing = ("in-step kernel spans (tt2_probe_span_ms: device wall clock, first workgroup start to last "
                   "wave end) of the launches inside graph-replayed training steps, streams serialised in "
                   "issue order as under rocprofv3, mean of 5 replays")
     elif gk:
-        secs = gk[2] * n / gk[0]
+        secs = gk[2] * n_calls / gk[0]
         timing = ("in-step kernel spans (tt2_probe_span_ms) of the launches inside graph-replayed training "
                   "steps, mean of 5 replays")
     else:
@@ -359,6 +372,9 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
     tot_t = sum(v[2] for v in allg.values())
     tot_f = sum(v[1] for v in allg.values())
     achieved = flops / secs / 1e12
+    share = None
+    if wgs_ser.get(key):   # mean share of the 256 CUs one dispatch's work groups can hold
+        share = sum(d * min(w / d, 256) for w, d in zip(wgs_ser[key], disp_calls[key])) / (256 * n)
     kname = gemm_kernel_name(*key[1:4])
     if key[0] == "gemm_grouped":
         kname = kname.replace("gemm7_kernel", "gemm7g_kernel").replace(", 0>", ">")
@@ -384,14 +400,21 @@ def roofline(model, text, tl, mel, ml, replay: bool = True):
         "algo_bytes_per_launch": round(abytes / n), "launches_per_step": n, "flops_per_launch": flops / n,
         "avg_launch_us": round(secs / n * 1e6, 2), "timing": timing,
         "eager_dispatch_avg_launch_us": round(eager_us, 2),
-        "replay_avg_launch_us": round(replay / n * 1e6, 2) if replay is not None else None,
+        # (per call: the back-to-back replay launches a grouped call's items as one grid)
+        "replay_avg_launch_us": round(replay / n_calls * 1e6, 2) if replay is not None else None,
         "concurrent": conc,
-        "all_gemms": {"launches": round(sum(v[0] for v in allg.values())), "ms_per_step": round(tot_t * 1e3, 3),
-                      "tflops": round(tot_f / tot_t / 1e12, 1)},
+        # a grouped launch on the side stream runs a capped grid (<= 128 work groups while the
+        # dgrad chain holds the rest): the share of the 256 CUs its work groups can occupy, and
+        # the fraction of that share's MFMA peak
+        "cu_share": round(share, 3) if share else None,
+        "frac_of_cu_share": round(achieved / PEAK_BF16_TFLOPS / share, 4) if share else None,
+        "all_gemms": {"launches": sum(ndisp.get(k, round(v[0])) for k, v in allg.items()),
+                      "ms_per_step": round(tot_t * 1e3, 3), "tflops": round(tot_f / tot_t / 1e12, 1)},
         # the four GEMM variants with the most in-step device time, same timing as above
         "top_gemms": [{"kernel": (gemm_kernel_name(*k[1:4]).replace("gemm7_kernel", "gemm7g_kernel").replace(", 0>", ">")
                                   if k[0] == "gemm_grouped" else gemm_kernel_name(*k[1:4])),
-                       "launches": round(v[0]), "avg_launch_us": round(v[2] / v[0] * 1e6, 2),
+                       "launches": ndisp.get(k, round(v[0])),
+                       "avg_launch_us": round(v[2] / ndisp.get(k, v[0]) * 1e6, 2),
                        "algo_mb_per_step": round(v[3] / 1e6, 1),
                        "frac": round(v[1] / v[2] / 1e12 / PEAK_BF16_TFLOPS, 4)}
                       for k, v in sorted(allg.items(), key=lambda kv: -kv[1][2])[:4]],

@@ -2551,16 +2551,17 @@ extern "C" int tt2_gemm_grouped_ex(const tt2_gemm_args* probs, int n, const tt2_
   }
   // max_groups > 0: at most that many work groups at a time (rounded down to a multiple of 8,
   // >= 8): the items go out as consecutive launches of that many, so a launch beside other
-  // work leaves the rest of the CUs free (no probe span: a capped launch is not one kernel)
-  // (an armed launch probe times one kernel: the cap is ignored for it)
-  const int grid = max_groups > 0 && g_probe_armed < 0 ? std::min(G.items, std::max(8, max_groups / 8 * 8)) : G.items;
-  ProbeScope ps(stream, grid < G.items ? 0 : grid);
-  G.p[0].span = ps.span;
+  // work leaves the rest of the CUs free.  An armed launch probe times the whole sequence: the
+  // span slots of launch i start at item ibase, the eager events ride on the first and last.
+  const int grid = max_groups > 0 ? std::min(G.items, std::max(8, max_groups / 8 * 8)) : G.items;
+  ProbeScope ps(stream, G.items);
   for (G.ibase = 0; G.ibase < G.items; G.ibase += grid) {
     const dim3 g(std::min(grid, G.items - G.ibase));
+    G.p[0].span = ps.span ? ps.span + (size_t)TT2_SPAN_W * G.ibase : nullptr;
+    hipEvent_t ev0 = G.ibase == 0 ? ps.e0 : nullptr, ev1 = G.ibase + grid >= G.items ? ps.e1 : nullptr;
 #define TT2_G7G(A_, B_)                                                                                    \
-  if (ps.ext() && grid >= G.items)                                                                       \
-    hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_>), g, dim3(G7_NT), 0, stream, ps.e0, ps.e1, 0, G);        \
+  if (ps.ext())                                                                                          \
+    hipExtLaunchKernelGGL((gemm7g_kernel<A_, B_>), g, dim3(G7_NT), 0, stream, ev0, ev1, 0, G);            \
   else                                                                                                   \
     hipLaunchKernelGGL((gemm7g_kernel<A_, B_>), g, dim3(G7_NT), 0, stream, G);
     if (!ta && !tb) { TT2_G7G(true, true) }
@@ -2570,6 +2571,7 @@ extern "C" int tt2_gemm_grouped_ex(const tt2_gemm_args* probs, int n, const tt2_
 #undef TT2_G7G
   }
   G.ibase = 0;
+  G.p[0].span = nullptr;
   if (main_only) reduce_blocks = 0;
   G.fin_only = reduce_blocks == 0 && fin_blocks > 0;
   if (G.fin_only)

@@ -201,7 +201,11 @@ def gemm_grouped(problems, ws: Workspace | None = None, fin=None, max_groups: in
         ab = sum(gemm_algo_bytes(g) for g in arr)
         PROBE.begin()
         check(L.tt2_gemm_grouped_ex(arr, len(problems), finp, max_groups, stream_ptr()), "tt2_gemm_grouped")
-        PROBE.end(key, flops, ab, list(arr))
+        # work groups of the call, and its kernel dispatches (a capped grid goes out as consecutive
+        # launches of at most the cap, rounded down to a multiple of 8: tt2_gemm_grouped_ex)
+        items = sum(((g.m + 255) // 256) * ((g.n + 127) // 128) * max(1, g.splits) for g in arr)
+        grid = min(items, max(8, max_groups // 8 * 8)) if max_groups > 0 else items
+        PROBE.end(key, flops, ab, list(arr), wgs=items, disp=-(-items // grid))
         return
     check(L.tt2_gemm_grouped_ex(arr, len(problems), finp, max_groups, stream_ptr()), "tt2_gemm_grouped")
 
@@ -214,6 +218,8 @@ class LaunchProbe:
 
     def __init__(self):
         self.rec = []
+        self.wgs = {}    # key -> [work groups of each recorded grouped call]
+        self.disp = {}   # key -> [kernel dispatches of each recorded call] (grouped: capped grids)
         self._s = None
 
     def begin(self):
@@ -221,7 +227,10 @@ class LaunchProbe:
         if self._s < 0:
             check(self._s, "tt2_probe_arm")
 
-    def end(self, key, flops, algo_bytes=0, args=None):
+    def end(self, key, flops, algo_bytes=0, args=None, wgs=None, disp=1):
+        if wgs is not None:
+            self.wgs.setdefault(key, []).append(wgs)
+        self.disp.setdefault(key, []).append(disp)
         e = None
         saved = None
         if args is not None:   # a copy of the launch's tt2_gemm_args (array for a grouped launch)
