@@ -412,70 +412,65 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
   }
 }
 
-// grid ceil(C/4): 4 columns x 64 chunk groups per block (C = 512 -> 128 blocks, each
-// lane combining ~R/64 chunks with its loads unrolled 4 deep).  Exact two-pass combine of
-// the chunk moments (no per-chunk division): mean = sum n_c mean_c / n, then
-// M2 = sum M2_c + n_c (mean_c - mean)^2, accumulated in double.
-constexpr int BNF_COLS = 4, BNF_GROUPS = 64;
-__global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
-  __shared__ double red[BNF_GROUPS][BNF_COLS + 1];
-  __shared__ double smean[BNF_COLS];
-  const int cl = threadIdx.x % BNF_COLS, g = threadIdx.x / BNF_COLS;
-  const int c = blockIdx.x * BNF_COLS + cl;
-  if (!a.training) {
-    if (g == 0 && c < a.C) {
-      a.mean[c] = a.run_mean[c];
-      a.rstd[c] = rsqrtf(a.run_var[c] + a.eps);
-    }
-    return;
-  }
+// Chunk combine of 64 columns per workgroup: thread (column cl = t % 64, group g = t / 64)
+// walks chunks r = g, g + 4, ... (4 loads in flight), then the 4 group partials are added in
+// order.  Exact two-pass combine of the chunk moments (no per-chunk division): mean =
+// sum n_c mean_c / n, then M2 = sum M2_c + n_c (mean_c - mean)^2, accumulated in double.  The
+// standalone finalize (grid ceil(C / 64)) and the apply kernels that finalize their own column
+// block (bn_apply_fin_kernel) run this same code, so both give the same statistics.
+constexpr int BNC_COLS = 64, BNC_G = NT / BNC_COLS;
+struct BnFinScratch { double red[BNC_G][BNC_COLS]; double mu[BNC_COLS]; float mean[BNC_COLS], rstd[BNC_COLS]; };
+
+// forward: mean / rstd of column block cb into S.mean / S.rstd; write: also a.mean / a.rstd and
+// the running statistics (or, SyncBN, this rank's slots)
+TT2_DEV void bn_fin64(const BnArgs& a, int cb, BnFinScratch& S, bool write) {
+  const int cl = threadIdx.x % BNC_COLS, g = threadIdx.x / BNC_COLS;
+  const int c = cb * BNC_COLS + cl;
   const bool ok = c < a.C;
   const int cc = ok ? c : 0;
   auto nrows = [&](int r) { return (double)min(a.rows_per, a.M - r * a.rows_per); };
+  auto pm = [&](int r, int w) { return a.part[((int64_t)r * 2 + w) * a.C + cc]; };
   double acc = 0.0;
   int r = g;
-  for (; r + 3 * BNF_GROUPS < a.R; r += 4 * BNF_GROUPS) {
+  for (; r + 3 * BNC_G < a.R; r += 4 * BNC_G) {
     float v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = a.part[((int64_t)(r + u * BNF_GROUPS) * 2 + 0) * a.C + cc];
+    for (int u = 0; u < 4; ++u) v[u] = pm(r + u * BNC_G, 0);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc += nrows(r + u * BNF_GROUPS) * v[u];
+    for (int u = 0; u < 4; ++u) acc += nrows(r + u * BNC_G) * v[u];
   }
-  for (; r < a.R; r += BNF_GROUPS) acc += nrows(r) * a.part[((int64_t)r * 2 + 0) * a.C + cc];
-  red[g][cl] = acc;
+  for (; r < a.R; r += BNC_G) acc += nrows(r) * pm(r, 0);
+  S.red[g][cl] = acc;
   __syncthreads();
-  if (g == 0) {
-    double t = 0.0;
-    for (int k = 0; k < BNF_GROUPS; ++k) t += red[k][cl];
-    smean[cl] = t / a.M;
-  }
+  if (g == 0) S.mu[cl] = (((S.red[0][cl] + S.red[1][cl]) + S.red[2][cl]) + S.red[3][cl]) / a.M;
   __syncthreads();
-  const double mu = smean[cl];
+  const double mu = S.mu[cl];
   acc = 0.0;
   r = g;
-  for (; r + 3 * BNF_GROUPS < a.R; r += 4 * BNF_GROUPS) {
+  for (; r + 3 * BNC_G < a.R; r += 4 * BNC_G) {
     float m1[4], m2[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      m1[u] = a.part[((int64_t)(r + u * BNF_GROUPS) * 2 + 0) * a.C + cc];
-      m2[u] = a.part[((int64_t)(r + u * BNF_GROUPS) * 2 + 1) * a.C + cc];
-    }
+    for (int u = 0; u < 4; ++u) { m1[u] = pm(r + u * BNC_G, 0); m2[u] = pm(r + u * BNC_G, 1); }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const double d = m1[u] - mu;
-      acc += m2[u] + nrows(r + u * BNF_GROUPS) * d * d;
+      acc += m2[u] + nrows(r + u * BNC_G) * d * d;
     }
   }
-  for (; r < a.R; r += BNF_GROUPS) {
-    const double d = a.part[((int64_t)r * 2 + 0) * a.C + cc] - mu;
-    acc += a.part[((int64_t)r * 2 + 1) * a.C + cc] + nrows(r) * d * d;
+  for (; r < a.R; r += BNC_G) {
+    const double d = pm(r, 0) - mu;
+    acc += pm(r, 1) + nrows(r) * d * d;
   }
   __syncthreads();
-  red[g][cl] = acc;
+  S.red[g][cl] = acc;
   __syncthreads();
-  if (g != 0 || !ok) return;
-  double m2 = 0.0;
-  for (int k = 0; k < BNF_GROUPS; ++k) m2 += red[k][cl];
+  if (g != 0) return;
+  const double m2 = ((S.red[0][cl] + S.red[1][cl]) + S.red[2][cl]) + S.red[3][cl];
+  const double n = a.M;
+  const double var = m2 / n;
+  S.mean[cl] = (float)mu;
+  S.rstd[cl] = (float)(1.0 / sqrt(var + a.eps));
+  if (!write || !ok) return;
   if (a.sync) {   // this rank's (mean, M2, rows) into its slot; the other ranks' slots zero
     for (int r2 = 0; r2 < a.W; ++r2) {
       a.sync[((int64_t)r2 * 3 + 0) * a.C + c] = r2 == a.rank ? (float)mu : 0.f;
@@ -484,15 +479,26 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
     }
     return;
   }
-  const double n = a.M;
-  const double var = m2 / n;
-  a.mean[c] = (float)mu;
-  a.rstd[c] = (float)(1.0 / sqrt(var + a.eps));
+  a.mean[c] = S.mean[cl];
+  a.rstd[c] = S.rstd[cl];
   if (a.run_mean) {
     const double unb = n > 1 ? m2 / (n - 1) : var;
     a.run_mean[c] = (float)((1.0 - a.momentum) * a.run_mean[c] + a.momentum * mu);
     a.run_var[c] = (float)((1.0 - a.momentum) * a.run_var[c] + a.momentum * unb);
   }
+}
+
+__global__ __launch_bounds__(NT) void bn_finalize_kernel(BnArgs a) {
+  __shared__ BnFinScratch S;
+  if (!a.training) {   // eval: the running statistics
+    const int c = blockIdx.x * BNC_COLS + threadIdx.x;
+    if (threadIdx.x < BNC_COLS && c < a.C) {
+      a.mean[c] = a.run_mean[c];
+      a.rstd[c] = rsqrtf(a.run_var[c] + a.eps);
+    }
+    return;
+  }
+  bn_fin64(a, blockIdx.x, S, true);
 }
 
 // SyncBatchNorm: combine the W exchanged rank moments in rank order, exactly as
@@ -634,33 +640,39 @@ __global__ __launch_bounds__(NT) void bn_bwd_stats_kernel(BnArgs a) {
   }
 }
 
-__global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(BnArgs a) {
-  __shared__ float red[2][BNF_GROUPS][BNF_COLS + 1];
-  const int cl = threadIdx.x % BNF_COLS, g = threadIdx.x / BNF_COLS;
-  const int c = blockIdx.x * BNF_COLS + cl;
+// backward: the chunk sums (sum dpre, sum dpre * xhat) of column block cb, in bn_fin64's order,
+// into db / dg (LDS); write: also a.dbeta / a.dgamma (this rank's parameter gradients) and the
+// SyncBN slots
+struct BnBsumScratch { float red[2][BNC_G][BNC_COLS]; float db[BNC_COLS], dg[BNC_COLS]; };
+TT2_DEV void bn_bsum64(const BnArgs& a, int cb, BnBsumScratch& S, bool write) {
+  const int cl = threadIdx.x % BNC_COLS, g = threadIdx.x / BNC_COLS;
+  const int c = cb * BNC_COLS + cl;
   const int cc = c < a.C ? c : 0;
   float s1 = 0.f, s2 = 0.f;
   int r = g;
-  for (; r + 3 * BNF_GROUPS < a.R; r += 4 * BNF_GROUPS) {
+  for (; r + 3 * BNC_G < a.R; r += 4 * BNC_G) {
     float v1[4], v2[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      v1[u] = a.part[((int64_t)(r + u * BNF_GROUPS) * 2 + 0) * a.C + cc];
-      v2[u] = a.part[((int64_t)(r + u * BNF_GROUPS) * 2 + 1) * a.C + cc];
+      v1[u] = a.part[((int64_t)(r + u * BNC_G) * 2 + 0) * a.C + cc];
+      v2[u] = a.part[((int64_t)(r + u * BNC_G) * 2 + 1) * a.C + cc];
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) { s1 += v1[u]; s2 += v2[u]; }
   }
-  for (; r < a.R; r += BNF_GROUPS) {
+  for (; r < a.R; r += BNC_G) {
     s1 += a.part[((int64_t)r * 2 + 0) * a.C + cc];
     s2 += a.part[((int64_t)r * 2 + 1) * a.C + cc];
   }
-  red[0][g][cl] = s1;
-  red[1][g][cl] = s2;
+  S.red[0][g][cl] = s1;
+  S.red[1][g][cl] = s2;
   __syncthreads();
-  if (g != 0 || c >= a.C) return;
-  float t1 = 0.f, t2 = 0.f;
-  for (int k = 0; k < BNF_GROUPS; ++k) { t1 += red[0][k][cl]; t2 += red[1][k][cl]; }
+  if (g != 0) return;
+  const float t1 = ((S.red[0][0][cl] + S.red[0][1][cl]) + S.red[0][2][cl]) + S.red[0][3][cl];
+  const float t2 = ((S.red[1][0][cl] + S.red[1][1][cl]) + S.red[1][2][cl]) + S.red[1][3][cl];
+  S.db[cl] = t1;
+  S.dg[cl] = t2;
+  if (!write || c >= a.C) return;
   a.dbeta[c] = t1;    // this rank's parameter gradients (the DP all-reduce sums them)
   a.dgamma[c] = t2;
   if (a.sync) {
@@ -669,6 +681,25 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(BnArgs a) {
       a.sync[((int64_t)r2 * 3 + 1) * a.C + c] = r2 == a.rank ? t2 : 0.f;
       a.sync[((int64_t)r2 * 3 + 2) * a.C + c] = r2 == a.rank ? (float)a.M : 0.f;
     }
+  }
+}
+
+__global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(BnArgs a) {
+  __shared__ BnBsumScratch S;
+  bn_bsum64(a, blockIdx.x, S, true);
+}
+
+// one 8-column group of the backward apply (shared by bn_bwd_apply_kernel and the fused
+// bn_bwd_apply_fin_kernel, so both compile the same expression: SyncBN at one rank stays
+// bit-identical to plain BatchNorm)
+TT2_DEV void bn_dy8(const BnArgs& a, const float (&v)[8], const float (&d)[8], const float (&kp)[8],
+                    const float (&mu)[8], const float (&rs)[8], const float (&g)[8], const float (&b)[8],
+                    const float (&db)[8], const float (&dg)[8], float invM, float (&o)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float xh = (v[j] - mu[j]) * rs[j];
+    const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[j]);
+    o[j] = a.training ? g[j] * rs[j] * (dp - db[j] * invM - xh * dg[j] * invM) : g[j] * rs[j] * dp;
   }
 }
 
@@ -690,14 +721,114 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_kernel(BnArgs a) {
     if (a.training) { col8(a.dbeta, c0, db); col8(a.dgamma, c0, dg); }
     float kp[8];
     bn_keep8(a, seed, i0, kp);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float xh = (v[j] - mu[j]) * rs[j];
-      const float dp = bn_dpre(a, kp[j], xh, g[j], b[j], d[j]);
-      o[j] = a.training ? g[j] * rs[j] * (dp - db[j] * invM - xh * dg[j] * invM) : g[j] * rs[j] * dp;
-    }
+    bn_dy8(a, v, d, kp, mu, rs, g, b, db, dg, invM, o);
     st8nt(reinterpret_cast<T*>(a.dy) + i0, o);
   }
+}
+
+// Training apply with the finalize folded in: workgroup (column block x, row block y)
+// first combines the chunk statistics of its 64 columns (bn_fin64 / bn_bsum64: the
+// standalone finalize's code and order, ≈ 25 KB of chunk partials per workgroup), row block
+// 0 writing mean / rstd / running statistics (forward) or dbeta / dgamma (backward), then
+// applies them to its rows: one launch fewer per BatchNorm pass on the step's critical path.
+// Threads: 8 column groups x 32 row lanes.
+#ifndef BN_FUSED_FIN
+#define BN_FUSED_FIN 1
+#endif
+TT2_DEV void bn_rows_of(const BnArgs& a, int& r0, int& r1) {
+  const int per = (a.M + gridDim.y - 1) / gridDim.y;
+  r0 = blockIdx.y * per;
+  r1 = min(a.M, r0 + per);
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_apply_fin_kernel(BnArgs a) {
+  __shared__ BnFinScratch S;
+  bn_fin64(a, blockIdx.x, S, blockIdx.y == 0);
+  __syncthreads();
+  const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.x * BNC_COLS + cg * 8;
+  if (c0 >= a.C) return;
+  int r0, r1;
+  bn_rows_of(a, r0, r1);
+  const T* y = reinterpret_cast<const T*>(a.y);
+  const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
+  float mu[8], rs[8], g[8], b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { mu[j] = S.mean[cg * 8 + j]; rs[j] = S.rstd[cg * 8 + j]; }
+  col8(a.gamma, c0, g); col8(a.beta, c0, b);
+  for (int m = r0 + rl; m < r1; m += NT / 8) {
+    const int64_t i0 = (int64_t)m * a.C + c0;
+    float v[8];
+    ld8(y + i0, v);
+    float z[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = act_f(a.act, (v[j] - mu[j]) * rs[j] * g[j] + b[j]);
+    if (a.drop.thr) drop_apply8(a.drop, seed, (uint32_t)i0, z);
+    if (a.res) {
+      float r[8];
+      ld8v(a.res, (int64_t)m * a.res_ld + c0, a.res_dt, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] += r[j];
+    }
+    if (a.out_dt == TT2_BF16) st8nt(reinterpret_cast<bf16*>(a.out) + i0, z);
+    else st8nt(reinterpret_cast<float*>(a.out) + i0, z);
+  }
+}
+
+// FIN = false: the sums are already final in a.dbeta / a.dgamma (SyncBatchNorm: the exchanged
+// global sums) and are only staged; the rest is the same code, so SyncBN at one rank stays
+// bit-identical to plain BatchNorm
+template <typename T, typename TD, bool FIN>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_fin_kernel(BnArgs a) {
+  __shared__ BnBsumScratch S;
+  if constexpr (FIN) {
+    bn_bsum64(a, blockIdx.x, S, blockIdx.y == 0);
+  } else if (threadIdx.x < BNC_COLS) {
+    const int c = blockIdx.x * BNC_COLS + threadIdx.x;
+    S.db[threadIdx.x] = c < a.C ? a.dbeta[c] : 0.f;
+    S.dg[threadIdx.x] = c < a.C ? a.dgamma[c] : 0.f;
+  }
+  __syncthreads();
+  const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.x * BNC_COLS + cg * 8;
+  if (c0 >= a.C) return;
+  int r0, r1;
+  bn_rows_of(a, r0, r1);
+  const T* y = reinterpret_cast<const T*>(a.y);
+  const TD* dout = reinterpret_cast<const TD*>(a.dout);
+  const uint32_t seed = a.drop.thr ? *a.drop.seed : 0u;
+  const float invM = a.inv_m ? *a.inv_m : 1.f / (float)a.Mtot;   // (bn_bwd_apply_kernel's form)
+  float mu[8], rs[8], g[8], b[8], db[8], dg[8];
+  col8(a.mean, c0, mu); col8(a.rstd, c0, rs); col8(a.gamma, c0, g); col8(a.beta, c0, b);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { db[j] = S.db[cg * 8 + j]; dg[j] = S.dg[cg * 8 + j]; }
+  for (int m = r0 + rl; m < r1; m += NT / 8) {
+    const int64_t i0 = (int64_t)m * a.C + c0;
+    float v[8], d[8], o[8], kp[8];
+    ld8(y + i0, v);
+    ld8(dout + i0, d);
+    bn_keep8(a, seed, i0, kp);
+    bn_dy8(a, v, d, kp, mu, rs, g, b, db, dg, invM, o);
+    st8nt(reinterpret_cast<T*>(a.dy) + i0, o);
+  }
+}
+
+void bn_bwd_apply_fin(const BnArgs& a, bool bf, bool dbf, bool fin, dim3 grid, hipStream_t s) {
+#define TT2_BNF(T_, TD_)                                                                           \
+  if (fin) hipLaunchKernelGGL((bn_bwd_apply_fin_kernel<T_, TD_, true>), grid, dim3(NT), 0, s, a);  \
+  else hipLaunchKernelGGL((bn_bwd_apply_fin_kernel<T_, TD_, false>), grid, dim3(NT), 0, s, a);
+  if (bf && dbf) { TT2_BNF(bf16, bf16) }
+  else if (bf) { TT2_BNF(bf16, float) }
+  else if (dbf) { TT2_BNF(float, bf16) }
+  else { TT2_BNF(float, float) }
+#undef TT2_BNF
+}
+
+// (column blocks, row blocks) of the fused applies: about 512 workgroups, >= 32 rows each
+dim3 bn_fin_grid(int m, int c) {
+  const int ncb = (c + BNC_COLS - 1) / BNC_COLS;
+  return dim3(ncb, std::max(1, std::min((m + 31) / 32, 512 / ncb)));
 }
 
 int grid_for(int64_t total) {
@@ -859,7 +990,12 @@ extern "C" int tt2_batchnorm_fwd(const tt2_bn_args* p, hipStream_t s) {
     if (bf) hipLaunchKernelGGL(bn_stats_kernel<bf16>, dim3(a.R), dim3(NT), 0, s, a);
     else hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(a.R), dim3(NT), 0, s, a);
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
+  if (BN_FUSED_FIN && p->training) {   // the finalize inside the apply
+    if (bf) hipLaunchKernelGGL(bn_apply_fin_kernel<bf16>, bn_fin_grid(p->m, p->c), dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL(bn_apply_fin_kernel<float>, bn_fin_grid(p->m, p->c), dim3(NT), 0, s, a);
+    return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_fwd");
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + BNC_COLS - 1) / BNC_COLS), dim3(NT), 0, s, a);
   const int g = grid_for((int64_t)p->m * p->c / 8);
   if (bf) hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(g), dim3(NT), 0, s, a);
   else hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(g), dim3(NT), 0, s, a);
@@ -880,7 +1016,11 @@ extern "C" int tt2_batchnorm_bwd(const tt2_bn_args* p, hipStream_t s) {
   else if (dbf) hipLaunchKernelGGL((KER<float, bf16>), grid, dim3(NT), 0, s, a);                \
   else hipLaunchKernelGGL((KER<float, float>), grid, dim3(NT), 0, s, a);
   if (p->stats_rows <= 0) { TT2_BN_DISPATCH(bn_bwd_stats_kernel, dim3(a.R)) }   // else: tt2_gemm bn_bwd's sums
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
+  if (BN_FUSED_FIN && p->training) {   // the finalize inside the apply
+    bn_bwd_apply_fin(a, bf, dbf, true, bn_fin_grid(p->m, p->c), s);
+    return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_bwd");
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + BNC_COLS - 1) / BNC_COLS), dim3(NT), 0, s, a);
   const int ga = grid_for((int64_t)p->m * p->c / 8);
   TT2_BN_DISPATCH(bn_bwd_apply_kernel, dim3(ga))
 #undef TT2_BN_DISPATCH
@@ -924,7 +1064,7 @@ extern "C" int tt2_batchnorm_fwd_stats(const tt2_bn_args* p, hipStream_t s) {
     if (p->dtype == TT2_DT_BF16) hipLaunchKernelGGL(bn_stats_kernel<bf16>, dim3(a.R), dim3(NT), 0, s, a);
     else hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(a.R), dim3(NT), 0, s, a);
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((p->c + BNC_COLS - 1) / BNC_COLS), dim3(NT), 0, s, a);
   return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_fwd_stats");
 }
 
@@ -953,7 +1093,7 @@ extern "C" int tt2_batchnorm_bwd_stats(const tt2_bn_args* p, hipStream_t s) {
   const BnArgs a = bn_sync_args(p);
   const bool bf = p->dtype == TT2_DT_BF16, dbf = p->dout_dtype == TT2_DT_BF16;
   if (p->stats_rows <= 0) { TT2_BN_DISPATCH2(bn_bwd_stats_kernel, dim3(a.R), a) }
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + BNF_COLS - 1) / BNF_COLS), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((p->c + BNC_COLS - 1) / BNC_COLS), dim3(NT), 0, s, a);
   return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_bwd_stats");
 }
 
@@ -967,6 +1107,10 @@ extern "C" int tt2_batchnorm_bwd_apply(const tt2_bn_args* p, hipStream_t s) {
   a.dgamma = a.dbeta + a.C;
   a.inv_m = a.dgamma + a.C;
   const bool bf = p->dtype == TT2_DT_BF16, dbf = p->dout_dtype == TT2_DT_BF16;
+  if (BN_FUSED_FIN) {   // plain BatchNorm's apply code with the exchanged sums staged (one rank: bitwise equal)
+    bn_bwd_apply_fin(a, bf, dbf, false, bn_fin_grid(p->m, p->c), s);
+    return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_bwd_apply");
+  }
   const int ga = grid_for((int64_t)p->m * p->c / 8);
   TT2_BN_DISPATCH2(bn_bwd_apply_kernel, dim3(ga), a)
   return tt2_check_launch(hipGetLastError(), "tt2_batchnorm_bwd_apply");
