@@ -60,6 +60,10 @@ constexpr int64_t PROBE_SPAN_PAIRS = 1 << 20;
 thread_local unsigned long long* g_span = nullptr;
 thread_local int64_t g_span_used = 0;
 thread_local std::vector<std::pair<int64_t, int>> g_span_rec;   // per slot: pool offset, work groups
+// per slot: work groups per launch when one probed call goes out as consecutive launches (a
+// capped grouped grid): the span is then the sum of the launches' own spans, as rocprofv3
+// times each dispatch (0: one launch)
+thread_local std::vector<int> g_span_chunk;
 
 int probe_take(hipEvent_t& e0, hipEvent_t& e1, unsigned long long*& span, int groups) {
   span = nullptr;
@@ -109,13 +113,15 @@ TT2_DEV void span_end(unsigned long long* span, int* done, int waves) {
 struct ProbeScope {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   unsigned long long* span = nullptr;   // the kernel's own span record (see g_span)
+  int slot = -1;
   ProbeScope(hipStream_t s, int groups) {
-    if (probe_take(e0, e1, span, groups) < 0) return;
+    if ((slot = probe_take(e0, e1, span, groups)) < 0) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) e0 = e1 = nullptr;
     (void)hipGetLastError();
   }
   bool ext() const { return e0 != nullptr; }
+  void chunk(int wgs) const { if (slot >= 0) g_span_chunk[slot] = wgs; }
 };
 
 
@@ -2555,6 +2561,7 @@ extern "C" int tt2_gemm_grouped_ex(const tt2_gemm_args* probs, int n, const tt2_
   // span slots of launch i start at item ibase, the eager events ride on the first and last.
   const int grid = max_groups > 0 ? std::min(G.items, std::max(8, max_groups / 8 * 8)) : G.items;
   ProbeScope ps(stream, G.items);
+  ps.chunk(grid);
   for (G.ibase = 0; G.ibase < G.items; G.ibase += grid) {
     const dim3 g(std::min(grid, G.items - G.ibase));
     G.p[0].span = ps.span ? ps.span + (size_t)TT2_SPAN_W * G.ibase : nullptr;
@@ -2605,6 +2612,7 @@ extern "C" int tt2_probe_arm(void) {
   if (e != hipSuccess) return tt2_check_launch(e, "tt2_probe_arm");
   g_probe.push_back(p);
   g_span_rec.push_back({-1, 0});
+  g_span_chunk.push_back(0);
   g_probe_armed = (int)g_probe.size() - 1;
   return g_probe_armed;
 }
@@ -2626,12 +2634,17 @@ extern "C" float tt2_probe_span_ms(int slot) {
   if (hipMemcpy(h.data(), g_span + TT2_SPAN_W * off, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1.f;
   // zeroed again, so the next replay of a graph must record every pair afresh
   if (hipMemset(g_span + TT2_SPAN_W * off, 0, h.size() * 8) != hipSuccess) return -1.f;
-  unsigned long long t0 = ~0ull, t1 = 0;
-  for (int i = 0; i < groups; ++i) {
-    const unsigned long long s0 = h[TT2_SPAN_W * i], s1 = h[TT2_SPAN_W * i + 1];
-    if (s0 == 0 || s1 < s0) return -1.f;   // a work group left no record
-    t0 = std::min(t0, s0);
-    t1 = std::max(t1, s1);
+  const int chunk = g_span_chunk[slot] > 0 ? g_span_chunk[slot] : groups;
+  unsigned long long total = 0;
+  for (int c0 = 0; c0 < groups; c0 += chunk) {   // each launch's own span
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int i = c0; i < std::min(groups, c0 + chunk); ++i) {
+      const unsigned long long s0 = h[TT2_SPAN_W * i], s1 = h[TT2_SPAN_W * i + 1];
+      if (s0 == 0 || s1 < s0) return -1.f;   // a work group left no record
+      t0 = std::min(t0, s0);
+      t1 = std::max(t1, s1);
+    }
+    total += t1 - t0;
   }
   static int khz = 0;
   if (!khz) {
@@ -2642,7 +2655,7 @@ extern "C" float tt2_probe_span_ms(int slot) {
       return -1.f;
     }
   }
-  return (float)((double)(t1 - t0) / khz);
+  return (float)((double)total / khz);
 }
 
 extern "C" int tt2_probe_span_records(int slot, unsigned long long* out, int cap) {
@@ -2666,6 +2679,7 @@ extern "C" void tt2_probe_reset(void) {
   if (g_span && g_span_used) (void)hipMemset(g_span, 0, TT2_SPAN_W * sizeof(unsigned long long) * g_span_used);
   g_span_used = 0;
   g_span_rec.clear();
+  g_span_chunk.clear();
   for (ProbeSlot& p : g_probe) {
     (void)hipEventDestroy(p.start);
     (void)hipEventDestroy(p.stop);
