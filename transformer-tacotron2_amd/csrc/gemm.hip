@@ -2242,6 +2242,12 @@ static bool g7_lds_epi(int variant) { return variant != 13; }
 // LDS-DMA 128^2, 3 skinny (M <= 64), 13 v7 warp-specialised 256x128 (auto; variant 14
 // forces its LDS-image epilogue, 13 its register epilogue), 15 v8 64x64, 16 v10 256x256 NT.
 // Returns -1 (error set) for an unsupported fusion request.
+#ifndef G8_SPLIT_TO_V7
+#define G8_SPLIT_TO_V7 1
+#endif
+#ifndef G8_SPLIT_MIN_K   // only the long-K ones (the encoder's K = 2048 products run faster unsplit on v8)
+#define G8_SPLIT_MIN_K 4096
+#endif
 static int gemm_plan(const tt2_gemm_args* a) {
   const int var = a->kernel_variant;
   const int64_t a_inner = a->trans_a ? a->m : a->k, b_inner = a->trans_b ? a->n : a->k;
@@ -2293,8 +2299,11 @@ static int gemm_plan(const tt2_gemm_args* a) {
                     (int64_t)(a->trans_b ? a->k : a->n) * a->ldb * 2 < (1LL << 31);
   // auto: v8 when v7 would run at most 64 tiles (the encoder's 2048-row products with N = 512,
   // the post-net's 80-channel conv): 1.4-1.6x v7 there, slower once v7 has >= 96 tiles
+  // (a long-K split-K request goes to v7, which splits: v8 has no split-K and ran it unsplit —
+  // the encoder's memory K/V dgrad, 2048 x 512 x 6144: 70 us unsplit on 256 64x64 tiles)
   const int64_t tiles7 = (int64_t)((a->m + 255) / 256) * ((a->n + 127) / 128);
-  if (v8ok && a->m >= 64 && (var == 15 || (var == 0 && tiles7 <= 64))) return 15;
+  const bool split_v7 = G8_SPLIT_TO_V7 && a->splits > 1 && v7ok && a->k >= G8_SPLIT_MIN_K;
+  if (v8ok && a->m >= 64 && (var == 15 || (var == 0 && tiles7 <= 64 && !split_v7))) return 15;
   // v10 (256 x 256, NT, bf16 C, K % 64 == 0, N % 256 == 0, no split / conv / k-sums; its epilogue
   // options are checked at launch): forced by variant 16; auto for the wide products
   const bool v10ok = v7ok && !a->trans_a && !a->trans_b && a->a_conv_t == 0 && !a->a_ksum &&
