@@ -2245,6 +2245,9 @@ static bool g7_lds_epi(int variant) { return variant != 13; }
 #ifndef G8_SPLIT_TO_V7
 #define G8_SPLIT_TO_V7 1
 #endif
+#ifndef G8_AUTO_TILES   // auto plan: v8 when v7 would run at most this many tiles
+#define G8_AUTO_TILES 64
+#endif
 #ifndef G8_SPLIT_MIN_K   // only the long-K ones (the encoder's K = 2048 products run faster unsplit on v8)
 #define G8_SPLIT_MIN_K 4096
 #endif
@@ -2303,7 +2306,7 @@ static int gemm_plan(const tt2_gemm_args* a) {
   // the encoder's memory K/V dgrad, 2048 x 512 x 6144: 70 us unsplit on 256 64x64 tiles)
   const int64_t tiles7 = (int64_t)((a->m + 255) / 256) * ((a->n + 127) / 128);
   const bool split_v7 = G8_SPLIT_TO_V7 && a->splits > 1 && v7ok && a->k >= G8_SPLIT_MIN_K;
-  if (v8ok && a->m >= 64 && (var == 15 || (var == 0 && tiles7 <= 64 && !split_v7))) return 15;
+  if (v8ok && a->m >= 64 && (var == 15 || (var == 0 && tiles7 <= G8_AUTO_TILES && !split_v7))) return 15;
   // v10 (256 x 256, NT, bf16 C, K % 64 == 0, N % 256 == 0, no split / conv / k-sums; its epilogue
   // options are checked at launch): forced by variant 16; auto for the wide products
   const bool v10ok = v7ok && !a->trans_a && !a->trans_b && a->a_conv_t == 0 && !a->a_ksum &&
