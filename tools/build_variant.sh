@@ -12,9 +12,10 @@ mkdir -p "$ROOT/abl"
 TMP=$(mktemp -d)
 OBJS=()
 for o in "$PKG"/build/*.o; do
-  if [[ $(basename "$o") == $SRC.hip.o || $(basename "$o") == $SRC.o ]]; then
+  if [[ $(basename "$o") == $SRC.hip.o || $(basename "$o") == $SRC.cpp.o || $(basename "$o") == $SRC.o ]]; then
+    SRCF="$PKG/csrc/$SRC.hip"; [ -f "$SRCF" ] || SRCF="$PKG/csrc/$SRC.cpp"
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -I"$PKG/csrc" \
-      -Wno-unused-result "$@" -c "$PKG/csrc/$SRC.hip" -o "$TMP/$SRC.o"
+      -Wno-unused-result "$@" -c "$SRCF" -o "$TMP/$SRC.o"
     OBJS+=("$TMP/$SRC.o")
   else
     OBJS+=("$o")

@@ -31,7 +31,10 @@ namespace {
 
 constexpr int SITE_INFER_FC1 = 128, SITE_INFER_FC2 = 129;
 constexpr int HEADS_LD = 96;
-constexpr int SPLIT_O = 4, SPLIT_F = 8;
+#ifndef DEC_SPLIT_F
+#define DEC_SPLIT_F 8
+#endif
+constexpr int SPLIT_O = 4, SPLIT_F = DEC_SPLIT_F;   // FFN2 (512 x 2048) split-K slabs
 
 struct Bufs {
   char *prev, *p1, *p2, *proj, *x0, *xa, *xb, *qkv, *att, *o, *h1, *cq, *catt, *co, *h2, *f1, *f2;
