@@ -18,6 +18,7 @@ import ctypes as C
 import torch
 import torch.distributed as dist
 
+from tt2.capture import check_join_target
 from tt2.dist import BnSync, GradSync, RcclGradSync
 
 
@@ -95,6 +96,7 @@ class RecordingBn(BnSync):
     def exchange(self, slots: torch.Tensor):
         gs = self.grad_sync
         cur = torch.cuda.current_stream()
+        check_join_target(cur, "BnSync.exchange")   # as the RCCL exchange: joins into the origin only
         gs.log.append(("bn", slots.numel(), _role_of(gs, cur)))
         _exchange(slots, cur, gs.stream, gs._tick, self.group, self.world)
         if self.snap_hook is not None:

@@ -147,3 +147,46 @@ def test_exception_inside_capture_is_raised_cleanly(gloo1, path):
     assert torch.equal(ref.engine.params, m.engine.params)
     if sync is not None:
         sync.close()
+
+
+def test_syncbn_exchange_from_side_stream_is_refused(gloo1):
+    """The capture rule as a guard: a SyncBatchNorm exchange issued from the
+    encoder's side stream under capture would join the comm stream into that non-origin stream,
+    the topology on which hipStreamEndCapture segfaults.  BnSync.exchange (here its recording
+    stand-in, which shares the check) raises CaptureError at the call instead; the capture is
+    ended cleanly, the process survives, and with the pre-net back on the main stream the same
+    model captures and replays in step with its eager twin."""
+    from _dp_recording import RecordingBn, RecordingSync
+    from tt2.dist import attach
+    b = _batch()
+    B, Tx, Ty = b[0].shape[0], b[0].shape[1], b[2].shape[1]
+    m, ref = _model(), _model()
+    syncs = [attach(x, bucket_bytes=4 << 20, sync_bn=True, sync_cls=RecordingSync, bn_cls=RecordingBn)
+             for x in (m, ref)]
+    e = m.engine
+    assert e.enc_overlap and e.bn_sync is not None
+    e.syncbn_prenet_on_main = False       # the pre-net's exchanges now come from the side stream
+    la = ref.train_step(*b, sync_grads=syncs[1].finish).clone()
+    lb = m.train_step(*b, sync_grads=syncs[0].finish).clone()   # eager: no capture, no guard
+    assert torch.equal(la, lb)
+    assert any(r[0] == "bn" and r[2] == "side" for r in syncs[0].log)
+    with pytest.raises(CaptureError, match="BnSync.exchange"):
+        m.capture_train_step(B, Tx, Ty, sync_grads=syncs[0].finish)
+    assert not torch.cuda.is_current_stream_capturing()
+    torch.cuda.synchronize()
+    e.syncbn_prenet_on_main = True
+    run = m.capture_train_step(B, Tx, Ty, sync_grads=syncs[0].finish)
+    for _ in range(2):
+        la = ref.train_step(*b, sync_grads=syncs[1].finish).clone()
+        lb = run(*b).clone()
+        assert torch.equal(la, lb)
+    torch.cuda.synchronize()
+    assert torch.equal(ref.engine.params, m.engine.params)
+    for s in syncs:
+        s.close()
+
+
+def test_check_join_target_outside_capture_is_noop():
+    from tt2.capture import active_origin, check_join_target
+    assert active_origin() is None
+    check_join_target(torch.cuda.Stream(), "test")   # no open capture: nothing to check

@@ -200,14 +200,18 @@ def test_sumsq_parts_and_adam_norm_parts():
     assert lib().tt2_sumsq_parts(C.c_void_p(g.data_ptr()), n, C.c_void_p(parts.data_ptr()), 0, None) != 0
 
 
+@pytest.mark.parametrize("enc_overlap", [1, 2])
 @pytest.mark.parametrize("graph", [False, True])
-def test_pipelined_optimizer_bitwise(graph):
+def test_pipelined_optimizer_bitwise(graph, enc_overlap):
     """The pipelined optimizer (each step's Adam deferred to the start of the next forward, the
     encoder's share on the side stream ahead of the encoder): 3 steps + flush equal 3 plain
     steps bit for bit (parameters, Adam moments, step counter, dropout seed), eager, and with
-    the captured step (one eager step, then two replays)."""
+    the captured step (one eager step, then two replays).  enc_overlap 2 issues the decoder's
+    part first, so the main stream's conv weight flip follows the side stream's encoder-conv
+    update closely: the flip must wait for that update, or the encoder conv
+    gradients are taken against stale weights."""
     b = _batch()
-    a, p = _model(True), _model(True)
+    a, p = _model(True, enc_overlap=enc_overlap), _model(True, enc_overlap=enc_overlap)
     p.pipeline_optimizer(True)
     la = [a.train_step(*b).clone() for _ in range(3)]
     if graph:
@@ -272,3 +276,22 @@ def test_pipelined_optimizer_flush_between_replays(tmp_path):
     eq = q.engine
     assert torch.equal(ea.params, eq.params) and torch.equal(ea.exp_avg_sq, eq.exp_avg_sq)
     assert eq.step_t.item() == 4
+
+
+def test_overlapped_forward_one_layer_decoder():
+    """The bf16 overlapped forward with n_dec = 1: the decoder generator then yields
+    once, and there is no part-1 memory K/V projection; the forward and the gradients equal the
+    in-place schedule's bit for bit."""
+    def mk(overlap):
+        torch.manual_seed(0)
+        m = TransformerTTS(TTSConfig(n_enc=2, n_dec=1), dtype=torch.bfloat16, seed=5)
+        m.configure_optimizer(lr=1e-3, warmup=10.0, clip_norm=1.0)
+        m.engine.wgrad_overlap = overlap
+        m.engine.enc_overlap = 1 if overlap else 0
+        return m.train()
+    b = _batch()
+    ref, got = _grads(mk(False), b), _grads(mk(True), b)
+    assert torch.equal(ref, got)
+    m = mk(True)
+    loss = [m.train_step(*b).clone() for _ in range(2)]
+    assert all(torch.isfinite(x).all() for x in loss)

@@ -1013,6 +1013,9 @@ TT2_DEV void g7_frag(Frag8<bf16>& f, const char* img, int r0, int kk, int lane) 
 #ifndef TT2_G10_AUTO
 #define TT2_G10_AUTO 1
 #endif
+#ifndef G7_REG   // the loader waves stage plain operand steps through VGPRs (1) or by LDS-DMA (0):
+#define G7_REG 0   // bit-identical, 3-17 % slower per GEMM, step 6.58 -> 6.88 ms
+#endif
 constexpr int G7_NT = 768;                          // 8 MFMA waves + 4 loader waves
 constexpr int G7_A = 256 * 128, G7_B = 128 * 128;   // bytes per stage: 64 k x 2 B per row
 constexpr int G7_STAGE = G7_A + G7_B;               // 48 KB
@@ -1117,6 +1120,13 @@ TT2_DEV void g7_issue(const OpDesc& d, G7Lane<NI>& L, char* lds, int k0, int ke,
     const void* src = ok ? (const void*)(base + L.off[i]) : (const void*)g_zero_page;
     __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(lds + inst * 1024), 16, 0, 0);
   }
+}
+
+// Register-staged copies into their ring slots (the LDS image LDS-DMA would have written).
+template <int NI>
+TT2_DEV void g7_put(const u32x4 (&r)[NI], char* lds, int lane, int lw) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) *reinterpret_cast<u32x4*>(lds + (lw * NI + i) * 1024 + lane * 16) = r[i];
 }
 
 // One GEMM problem of a (possibly grouped) v7 launch.  Work item = (split, tile).
@@ -1388,6 +1398,62 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem, unsigned 
   const bool tail = ((ke - kb) & 63) != 0;
   if (wave >= 8) {   // ------------------------------------------------ loader waves
     const int lw = wave - 8;
+    // staged epilogue operand (whole tiles only)
+    const bool px = P.pre_x && n0 + 128 <= N;
+    const void* xs = P.pre_x == 1 ? E.res : E.gate;
+    const int64_t ldx = P.pre_x == 1 ? E.ldr : E.ldg;
+#if G7_REG
+    // Register-staged operand steps (G7_REG; plain operands, no K tail -- conv operands and
+    // tails keep the LDS-DMA ring below): the loader lanes load a step's 16-B pieces into VGPRs
+    // (global_load_dwordx4, 48 per lane) and write them into the ring slot with ds_write_b128
+    // once the slot is free: step t + 2 is written at the start of step t (into the stage step
+    // t - 1 released), then step t + 3 is loaded, so one step is in flight in VGPRs.
+    // The same bytes land at the same LDS addresses as the LDS-DMA copies (bit-identical
+    // results).  Measured slower than the LDS-DMA ring on every shape (tools/lib_ab.py, DESIGN.md
+    // 5.2): off by default, kept for the A/B.
+    if (A.conv_t == 0 && B.conv_t == 0 && !tail) {
+      // (lane state per path: the conv path's coordinates are not live here)
+      G7Lane<G7_AI> la;
+      G7Lane<G7_BI> lb;
+      g7_lane_init<AK>(la, A, m0, kb, lane, lw);
+      g7_lane_init<BKC>(lb, B, n0, kb, lane, lw);
+      u32x4 ra[G7_AI], rb[G7_BI];
+      auto fetch = [&](int step) {   // plain operands: loop-invariant lane offsets
+        const int k0 = kb + 64 * step;
+        const char* ba = reinterpret_cast<const char*>(A.p) + (AK ? (int64_t)k0 : (int64_t)k0 * A.ld) * 2;
+        const char* bb = reinterpret_cast<const char*>(B.p) + (BKC ? (int64_t)k0 : (int64_t)k0 * B.ld) * 2;
+#pragma unroll
+        for (int i = 0; i < G7_AI; ++i) ra[i] = *reinterpret_cast<const u32x4*>(ba + la.off[i]);
+#pragma unroll
+        for (int i = 0; i < G7_BI; ++i) rb[i] = *reinterpret_cast<const u32x4*>(bb + lb.off[i]);
+      };
+      auto put = [&](int stage) {
+        char* sa = smem + stage * G7_STAGE;
+        g7_put<G7_AI>(ra, sa, lane, lw);
+        g7_put<G7_BI>(rb, sa + G7_A, lane, lw);
+      };
+      fetch(0);
+      put(0);
+      if (nkt > 1) { fetch(1); put(1); }
+      if (nkt > 2) fetch(2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      int st = 2;
+      for (int t = 0; t < nkt; ++t) {
+        if (t + 2 < nkt) {
+          put(st);   // step t + 2 into the stage step t - 1 released
+          st = st == 2 ? 0 : st + 1;
+          if (t + 3 < nkt) fetch(t + 3);
+        } else if (px) {
+          if (t == nkt - 2 || nkt == 1) g7_issue_x(P, xs, ldx, smem, nkt, m0, n0, 0, 12, lane, lw);
+          if (t == nkt - 1) g7_issue_x(P, xs, ldx, smem, nkt, m0, n0, 192, 4, lane, lw);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's slot writes are done
+        __builtin_amdgcn_s_barrier();
+      }
+    } else
+#endif
+    {
     G7Lane<G7_AI> la;
     G7Lane<G7_BI> lb;
     const bool cfast_a = g7_conv_fast(A) && !tail, cfast_b = g7_conv_fast(B) && !tail;
@@ -1400,10 +1466,6 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem, unsigned 
       g7_issue<AK>(A, la, sa, k0, ke, lane, lw, tl, cfast_a);
       g7_issue<BKC>(B, lb, sa + G7_A, k0, ke, lane, lw, tl, cfast_b);
     };
-    // staged epilogue operand (whole tiles only)
-    const bool px = P.pre_x && n0 + 128 <= N;
-    const void* xs = P.pre_x == 1 ? E.res : E.gate;
-    const int64_t ldx = P.pre_x == 1 ? E.ldr : E.ldg;
     issue(0, 0);
     if (nkt > 1) { issue(1, 1); asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); }
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1423,6 +1485,7 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem, unsigned 
       else if (!px)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+    }
     }
     if (px) {   // the staged tile has landed
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2326,6 +2389,31 @@ static int gemm_plan(const tt2_gemm_args* a) {
 
 extern "C" int tt2_gemm_plan(const tt2_gemm_args* a) { return gemm_plan(a); }
 
+// Vectorised epilogue: rows of C / res / gate start 16-B aligned at every 8th column.
+static bool epi_vec_ok(const tt2_gemm_args* a) {
+  auto ok = [](const void* p, int64_t ld, int dt) {
+    if (!p) return true;
+    const int esz = dt == TT2_BF16 ? 2 : 4;
+    return reinterpret_cast<uintptr_t>(p) % 16 == 0 && (ld * esz) % 16 == 0 && (8 * esz) % 16 == 0;
+  };
+  return a->dtype_out != TT2_F16 && a->res_dtype != TT2_F16 && a->gate_dtype != TT2_F16 &&
+         ok(a->c, a->ldc, a->dtype_out) && ok(a->res, a->ldr, a->res_dtype) && ok(a->gate, a->ldg, a->gate_dtype) &&
+         (reinterpret_cast<uintptr_t>(a->bias) % 16 == 0);
+}
+
+// The plan tt2_gemm launches: the auto plan, with v8 (which stores C / reads res and gate in
+// 16-B chunks) moved to v7 when those rows are not vector-aligned.  tt2_gemm_stats_rows asks
+// the same function, so the chunk height it reports is the one the kernel writes.
+static int launch_plan(const tt2_gemm_args* a) {
+  int plan = gemm_plan(a);
+  if (plan == 15 && !epi_vec_ok(a)) {
+    tt2_gemm_args b = *a;
+    b.kernel_variant = 13;
+    plan = gemm_plan(&b);
+  }
+  return plan;
+}
+
 // The kernel a fused-statistics request (col_stats / bn_bwd) runs on, given the auto plan: v8
 // (64-row chunks) when the plan takes it, else v7's LDS-image epilogue (256-row chunks); -1 when
 // neither can (split-K, f32 C, unaligned rows, v7 with a transposed operand or n % 128).
@@ -2345,7 +2433,7 @@ static int stats_plan(const tt2_gemm_args* a, int plan) {
 }
 
 extern "C" int32_t tt2_gemm_stats_rows(const tt2_gemm_args* a) {
-  const int plan = gemm_plan(a);
+  const int plan = launch_plan(a);
   if (plan < 0) return 0;
   const int sp = stats_plan(a, plan);
   return sp == 15 ? 64 : sp == 13 ? 256 : 0;
@@ -2398,17 +2486,7 @@ static int gemm_prep(const tt2_gemm_args* a, OpDesc& A, OpDesc& B, EpiParams& ep
     ep.bnb.drop = DropDesc{bn->drop_seed, bn->drop_site, bn->drop_thr, bn->drop_scale};
     ep.bnb.act = bn->act;
   }
-  {
-    // vectorised epilogue: rows of C / res / gate start 16-B aligned at every 8th column
-    auto ok = [](const void* p, int64_t ld, int dt) {
-      if (!p) return true;
-      const int esz = dt == TT2_BF16 ? 2 : 4;
-      return reinterpret_cast<uintptr_t>(p) % 16 == 0 && (ld * esz) % 16 == 0 && (8 * esz) % 16 == 0;
-    };
-    ep.vec = a->dtype_out != TT2_F16 && a->res_dtype != TT2_F16 && a->gate_dtype != TT2_F16 &&
-             ok(a->c, a->ldc, a->dtype_out) && ok(a->res, a->ldr, a->res_dtype) &&
-             ok(a->gate, a->ldg, a->gate_dtype) && (reinterpret_cast<uintptr_t>(a->bias) % 16 == 0);
-  }
+  ep.vec = epi_vec_ok(a);
   return TT2_OK;
 }
 
@@ -2429,13 +2507,8 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
   const int sp = a->splits > 1 ? a->splits : 1;
 
   hipError_t err;
-  int plan = gemm_plan(a);
+  int plan = launch_plan(a);             // v8 stores C in 16-B chunks: unaligned rows take v7 (or v2)
   if (plan < 0) return TT2_E_INVALID;   // message already set
-  if (plan == 15 && !ep.vec) {          // v8 stores C in 16-B chunks: unaligned rows take v7 (or v2)
-    tt2_gemm_args b = *a;
-    b.kernel_variant = 13;
-    plan = gemm_plan(&b);
-  }
   if (ep.cstats || ep.bnb.part) {   // fused BatchNorm statistics: v8's or v7's image epilogue
     plan = stats_plan(a, plan);
     if (plan < 0)

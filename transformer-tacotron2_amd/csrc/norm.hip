@@ -419,6 +419,9 @@ __global__ __launch_bounds__(NT) void bn_stats_kernel(BnArgs a) {
 // standalone finalize (grid ceil(C / 64)) and the apply kernels that finalize their own column
 // block (bn_apply_fin_kernel) run this same code, so both give the same statistics.
 constexpr int BNC_COLS = 64, BNC_G = NT / BNC_COLS;
+// bn_fin64 / bn_bsum64 combine exactly red[0..3] in a fixed order (the standalone finalize's
+// summation order, which the fused apply must reproduce bit for bit)
+static_assert(BNC_G == 4, "bn_fin64 / bn_bsum64 sum four chunk groups");
 struct BnFinScratch { double red[BNC_G][BNC_COLS]; double mu[BNC_COLS]; float mean[BNC_COLS], rstd[BNC_COLS]; };
 
 // forward: mean / rstd of column block cb into S.mean / S.rstd; write: also a.mean / a.rstd and

@@ -12,13 +12,22 @@ back into the capture's origin stream before the capture ends.  ``StepCapture`` 
 * on any exception inside the captured region it joins every registered stream that takes part
   in the capture, ends the capture and drops the graph, then re-raises: the process survives
   and no stream is left in capture mode (a capture left open made ``~CUDAGraph`` abort the
-  process).
+  process);
+* while it is open it is the thread's active capture (``active_origin()``), so code that joins a
+  forked stream back (the RCCL comm stream in ``RcclGradSync.finish`` / ``BnSync.exchange``) can
+  check, before it issues the join, that the join goes into the capture's origin stream
+  (``check_join_target``).  A join into any other stream is the topology on which
+  ``hipStreamEndCapture`` (the ROCm 7.0 runtime torch loads) segfaults even though the graph's
+  dependencies show every stream joined (``tools/capture_topo.py nested2s``; DESIGN.md section
+  6), so it is refused with ``CaptureError`` at the call instead of crashing the process at the
+  capture's end.
 """
 from __future__ import annotations
 
 import ctypes as C
 import os
 import sys
+import threading
 
 import torch
 
@@ -35,6 +44,43 @@ def _trace(*a):
 
 class CaptureError(RuntimeError):
     pass
+
+
+_active = threading.local()   # the open StepCaptures of this thread (captures are thread-local)
+
+
+def active_origin():
+    """The origin stream of this thread's innermost open StepCapture, or None."""
+    st = getattr(_active, "stack", None)
+    return st[-1].origin if st else None
+
+
+def check_join_target(stream: torch.cuda.Stream, what: str):
+    """Raise CaptureError if `stream` is capturing inside an open StepCapture and is not that
+    capture's origin: joining a forked stream into it would leave a join into a non-origin
+    stream in the graph (the hipStreamEndCapture segfault).  Outside a capture: no-op."""
+    origin = active_origin()
+    if origin is None or stream == origin:
+        return
+    with torch.cuda.stream(stream):
+        capturing = torch.cuda.is_current_stream_capturing()
+    if capturing:
+        raise CaptureError(f"{what}: joining into stream {stream.cuda_stream:#x}, which is not the capture's "
+                           f"origin {origin.cuda_stream:#x}; every forked stream must be joined into the origin "
+                           f"(DESIGN.md section 6, capture rule)")
+
+
+def _push(cap):
+    st = getattr(_active, "stack", None)
+    if st is None:
+        st = _active.stack = []
+    st.append(cap)
+
+
+def _pop(cap):
+    st = getattr(_active, "stack", None)
+    if st and cap in st:
+        st.remove(cap)
 
 
 def joined_status(origin: torch.cuda.Stream, streams: dict) -> dict:
@@ -63,6 +109,7 @@ class StepCapture:
 
     def begin(self):
         self.graph.capture_begin(capture_error_mode=self.mode)
+        _push(self)
 
     def _streams(self) -> dict:
         return {k: s for k, s in self.streams_fn().items() if s is not None and s != self.origin}
@@ -79,6 +126,7 @@ class StepCapture:
         _trace("capture_end")
         with torch.cuda.stream(self.origin):
             self.graph.capture_end()
+        _pop(self)
         _trace("capture ended")
 
     def abort(self):
@@ -86,6 +134,7 @@ class StepCapture:
         teardown itself are swallowed: the caller re-raises the original one)."""
         # torch ends a capture only on the stream it began on: make the origin current (the
         # caller may already have left its stream context)
+        _pop(self)
         with torch.cuda.stream(self.origin):
             try:
                 st = joined_status(self.origin, self._streams())

@@ -32,6 +32,8 @@ from datetime import timedelta
 import torch
 import torch.distributed as dist
 
+from .capture import check_join_target
+
 # RCCL channel floor for the bucket all-reduce (read by RCCL at communicator init).  A
 # ring is bound by one xGMI link (~153 GB/s); more channels spread the ring traffic over
 # the 7 links of an MI355X.  Only a floor: an explicit NCCL_MIN_NCHANNELS wins.
@@ -189,7 +191,9 @@ class RcclGradSync(GradSync):
             self._span[1].record(self.stream)
             self._done_span, self._span = tuple(self._span), None
         if self.pending:
-            torch.cuda.current_stream().wait_stream(self.stream)
+            cur = torch.cuda.current_stream()
+            check_join_target(cur, "RcclGradSync.finish")   # the comm stream joins the capture origin only
+            cur.wait_stream(self.stream)
         self.reset()
 
     def reset(self):
@@ -261,6 +265,9 @@ class BnSync:
             from . import _lib
             L = _lib.lib()
             cur, cs = torch.cuda.current_stream(), self.grad_sync.stream
+            # the exchange joins the comm stream back into `cur`: under capture that must be the
+            # capture's origin (raise here rather than segfault in hipStreamEndCapture)
+            check_join_target(cur, "BnSync.exchange")
             cs.wait_stream(cur)              # the stats kernel's slots are written on `cur`
             _lib.check(L.tt2_allreduce_bucket(C.c_void_p(slots.data_ptr()), slots.numel(), _lib.dt(slots), comm,
                                               C.c_void_p(cs.cuda_stream)), "tt2_allreduce_bucket")

@@ -254,6 +254,10 @@ class TTSEngine:
         # ... also with SyncBatchNorm (the encoder pre-net's exchanges then fork the comm stream
         # from the side stream); TT2_ENC_OVERLAP_SYNCBN=0 keeps the encoder on the main stream there
         self.enc_overlap_syncbn = os.environ.get("TT2_ENC_OVERLAP_SYNCBN", "1") != "0"
+        # SyncBatchNorm under the encoder overlap: the pre-net (its BatchNorm exchanges) on the
+        # main stream, the capture's origin (forward()).  False is for the capture guard's test
+        # only: the exchanges then come from the side stream and the capture refuses them.
+        self.syncbn_prenet_on_main = True
         # the post-net BatchNorms' statistics from their conv GEMMs' epilogues (_postnet_fwd)
         self.bn_gemm_stats = os.environ.get("TT2_BN_GEMM_STATS", "1") != "0"
         # pipelined optimizer (opt-in: TransformerTTS.pipeline_optimizer): a step's Adam is
@@ -580,6 +584,7 @@ class TTSEngine:
             main = torch.cuda.current_stream()
             side.wait_stream(main)
             dec = self._decoder_steps(A)
+            c_ndec = self.cfg.n_dec
             enc_r = self._enc_param_ranges() if parts is not None else []
 
             # SyncBatchNorm: the pre-net's exchanges stay on the main stream (the capture's
@@ -588,8 +593,9 @@ class TTSEngine:
             # segfaults on any stream joined into a stream other than the origin
             # (tools/capture_topo.py nested2s).  The decoder's first block
             # then overlaps the encoder layers instead of the pre-net: the chain is the same.
-            pre_main = self.bn_sync is not None
+            pre_main = self.bn_sync is not None and self.syncbn_prenet_on_main
             enc_r_side = [] if pre_main else enc_r   # with the pre-net on main, its update goes there
+            enc_adam_done = torch.cuda.Event() if enc_r_side else None
 
             def encoder():
                 ws, self.ws = self.ws, self._side_ws
@@ -597,6 +603,9 @@ class TTSEngine:
                     with torch.cuda.stream(side):
                         for lo, hi in enc_r_side:   # the encoder's parameters first
                             self._adam(lo, hi, parts, gated=True)
+                        if enc_r_side:
+                            # the main stream's conv weight flip below reads these weights
+                            enc_adam_done.record()
                         if not pre_main:
                             self.forward_encoder_prenet(A)
                         self.forward_encoder_layers(A, rest_kv_later=True)
@@ -626,21 +635,25 @@ class TTSEngine:
                 encoder()
             if self.training and self.wflip_batch:
                 # the dgrad conv weights (tap-flipped) for the backward, on the main stream while it
-                # waits for the encoder (they depend on the weights only)
+                # waits for the encoder (they depend on the weights only; with the pipelined
+                # optimizer, on the encoder convs' deferred update issued on the side stream)
+                if enc_adam_done is not None:
+                    main.wait_event(enc_adam_done)
                 self._flip_conv_weights()
                 self._wflip_ready = True
             self._pad_heads_weights()   # (also while the main stream waits for the encoder)
             main.wait_stream(side)   # layer 0's memory K/V, before layer 0's cross-attention
             if parts is not None:
                 ops.adam_gate(self.adam_gate, self.step_t)   # both halves of the deferred Adam have read it
-            ws, self.ws = self.ws, self._side_ws
-            try:
-                with torch.cuda.stream(side):   # layers 1..'s memory K/V beside decoder layer 0
-                    self.forward_memory_kv(A, 1)
-            finally:
-                self.ws = ws
-            next(dec)                # decoder layer 0 and layer 1's self-attention block
-            main.wait_stream(side)
+            if c_ndec > 1:
+                ws, self.ws = self.ws, self._side_ws
+                try:
+                    with torch.cuda.stream(side):   # layers 1..'s memory K/V beside decoder layer 0
+                        self.forward_memory_kv(A, 1)
+                finally:
+                    self.ws = ws
+            next(dec, None)          # decoder layer 0 and layer 1's self-attention block (or all of
+            main.wait_stream(side)   # a one-layer decoder)
             for _ in dec:
                 pass
         else:
@@ -728,6 +741,8 @@ class TTSEngine:
         d, Me = c.d_model, A.Me
         kvld, w, b = c.n_dec * 2 * d, self.W("dec.kv.w"), self.P("dec.kv.b")
         lo, hi = (0, 2 * d) if part == 0 else (2 * d, kvld)
+        if hi <= lo:   # a one-layer decoder has no part 1
+            return
         self._lin(A[f"ex{c.n_enc}"], w[lo:hi], A["mkv"][:, lo:], Me, hi - lo, d, bias=b[lo:hi], ldo=kvld)
 
     @ranged("tt2.decoder")
