@@ -553,16 +553,21 @@ def main():
     ap.add_argument("--no-ragged", action="store_true", help="skip the cfg2 ragged-length variant")
     ap.add_argument("--profile-run", action="store_true", help="the run a rocprofv3 kernel trace is taken of: "
                     "training step only (no ragged / decode / CPU legs, no back-to-back probe replays)")
-    ap.add_argument("--force-dp", action="store_true", help="dev: run the DP path (bucketed RCCL all-reduce, "
-                    "segmented graph) even at world size 1")
+    ap.add_argument("--force-dp", action="store_true", help="dev: run the DP path (bucketed RCCL all-reduce "
+                    "inside the step graph) even at world size 1")
+    ap.add_argument("--dp-standin", action="store_true", help="dev: the DP path at world size 1 with each bucket's "
+                    "all-reduce replaced by a kernel with an N-rank ring all-reduce's CU footprint, HBM bytes and "
+                    "duration (tt2.dist.StandinGradSync; TT2_DP_STANDIN_N / _GBPS / _WG)")
     args = ap.parse_args()
+    if args.dp_standin:
+        args.force_dp = True
     if args.profile_run:
         args.no_ragged = args.no_decode = args.no_longform = args.no_cpu_baseline = True
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))    # before anything touches the GPU
 
     from tt2.config import TTSConfig
-    from tt2.dist import attach, broadcast_params, init_from_env, rccl_env
+    from tt2.dist import StandinGradSync, attach, broadcast_params, init_from_env, rccl_env
     from tt2.model import TransformerTTS
 
     rank, world, local = init_from_env()
@@ -592,7 +597,10 @@ def main():
             os.environ.setdefault("MASTER_PORT", "29533")
             dist.init_process_group("nccl", rank=0, world_size=1)
         broadcast_params(model)
-        sync = attach(model, bucket_bytes=int(float(os.environ.get("TT2_BUCKET_MB", "25")) * (1 << 20)))
+        if args.dp_standin and world > 1:
+            raise SystemExit("bench: --dp-standin rehearses the exchange on ONE rank")
+        sync = attach(model, bucket_bytes=int(float(os.environ.get("TT2_BUCKET_MB", "25")) * (1 << 20)),
+                      sync_cls=StandinGradSync if args.dp_standin else None)
     model.train()
     # pipelined optimizer: each step's Adam runs at the start of the next step beside the encoder
     # forward (identical updates); the last step's Adam is flushed INSIDE the timed region
@@ -648,6 +656,9 @@ def main():
                 else "segmented (torch.distributed between graph segments)",
                 "backend": dist.get_backend(), "bucket_mb": round((sync.buckets[0][1] - sync.buckets[0][0]) * 4 / 2**20, 2),
                 "rccl_env": rccl_env(), "allreduce_alone": sync.bench_allreduce()}
+        if args.dp_standin:
+            comm["sync"] = "stand-in (one rank; per bucket a kernel with an N-rank ring all-reduce's footprint)"
+            comm["standin"] = sync.params()
         log(f"[bench] all-reduce alone: {comm['allreduce_alone']}")
 
     rag = None
@@ -676,7 +687,9 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-            "config": {"workload": ("train step (fwd+loss+bwd+grad all-reduce+Adam), LJSpeech-shape synthetic batch"
+            "config": {"workload": ("train step (fwd+loss+bwd+STAND-IN grad exchange+Adam), LJSpeech-shape synthetic "
+                                    "batch" if args.dp_standin else
+                                    "train step (fwd+loss+bwd+grad all-reduce+Adam), LJSpeech-shape synthetic batch"
                                     if sync is not None else
                                     "train step (fwd+loss+bwd+Adam; one rank: no gradient exchange), "
                                     "LJSpeech-shape synthetic batch"),

@@ -693,6 +693,12 @@ int tt2_allreduce_bucket(void* buf, size_t n, int32_t dtype, void* comm, hipStre
 int tt2_comm_unique_id(void* id_out /* 128 bytes */);
 int tt2_comm_init(void** comm_out, int32_t nranks, const void* id /* 128 bytes */, int32_t rank);
 int tt2_comm_destroy(void* comm);
+/* Measurement stand-in for one bucket's exchange at N ranks (tt2/dist.py StandinGradSync; the
+ * DP schedule rehearsed on one GPU): `wgs` work groups copy `bytes` from src to scratch, then each
+ * holds its CU until `seconds` have passed since it started.  No communicator; src is not modified.
+ * rec (optional, 2 * wgs u64): each work group's {start, end} on the device wall clock. */
+int tt2_comm_standin(const void* src, void* scratch, size_t bytes, double seconds, int32_t wgs, uint64_t* rec,
+                     hipStream_t stream);
 
 /* ------------------------------------------------------------ audio data path
  * Either side of the mel engine: log-mel extraction of the

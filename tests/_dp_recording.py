@@ -32,8 +32,11 @@ def _role_of(sync, stream) -> str:
 
 
 def _exchange(buf: torch.Tensor, issuing: torch.cuda.Stream, comm: torch.cuda.Stream, tick: torch.Tensor,
-              group, world: int):
-    comm.wait_stream(issuing)
+              group, world: int, after=None):
+    if after is not None:
+        comm.wait_event(after)
+    else:
+        comm.wait_stream(issuing)
     with torch.cuda.stream(comm):
         if torch.cuda.is_current_stream_capturing() or world == 1:
             tick.add_(1)
@@ -47,8 +50,8 @@ def _exchange(buf: torch.Tensor, issuing: torch.cuda.Stream, comm: torch.cuda.St
 class RecordingSync(RcclGradSync):
     in_graph = True
 
-    def __init__(self, flat_grads: torch.Tensor, bucket_bytes: int = 25 << 20, group=None):
-        GradSync.__init__(self, flat_grads, bucket_bytes, group)
+    def __init__(self, flat_grads: torch.Tensor, bucket_bytes: int = 25 << 20, group=None, cuts=None):
+        GradSync.__init__(self, flat_grads, bucket_bytes, group, cuts)
         self.comm = C.c_void_p(1)      # truthy, never handed to RCCL
         self.stream = torch.cuda.Stream()
         self.pending = False
@@ -57,13 +60,13 @@ class RecordingSync(RcclGradSync):
         self._tick = torch.zeros(1, device=flat_grads.device)
         self.hold = None               # negative control: a bucket index whose hand-off is held back
 
-    def _launch(self, lo, hi):
+    def _launch(self, lo, hi, after=None):
         cur = torch.cuda.current_stream()
         self.log.append(("bucket", lo, hi, _role_of(self, cur)))
-        _exchange(self.flat[lo:hi], cur, self.stream, self._tick, self.group, self.world)
+        _exchange(self.flat[lo:hi], cur, self.stream, self._tick, self.group, self.world, after)
         self.pending = True
 
-    def ready(self, offset: int):
+    def ready(self, offset: int, after=None):
         idx = self.take_ready(offset)
         if self.hold is not None:
             held = [i for i in idx if i == self.hold]
@@ -74,7 +77,7 @@ class RecordingSync(RcclGradSync):
                 idx = idx + self._held      # the held bucket goes after the next one
                 self._held = None
         for i in idx:
-            self._launch(*self.buckets[i])
+            self._launch(*self.buckets[i], after=after)
 
     def finish(self):
         if getattr(self, "_held", None):

@@ -167,3 +167,30 @@ def test_compare_issue_logs_lengths():
     assert compare_issue_logs([a, a[:1]]) == [(1, 1, ("bn", 4104, "main"), None)]
     assert compare_issue_logs([a, a + [("bn", 1, "main")]]) == [(1, 2, None, ("bn", 1, "main"))]
     assert compare_issue_logs([a, [("bucket", 0, 10, "main"), a[1]]]) == [(1, 0, a[0], ("bucket", 0, 10, "main"))]
+
+
+def test_layer_aligned_buckets():
+    """Buckets cut at the backward's ready offsets (engine.ready_offsets): one bucket per reported
+    range, ranges below per / 4 merged into the next lower one, covering the buffer exactly in
+    reverse layout order; each bucket is complete at the ready call of its own lowest offset."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "transformer-tacotron2_amd"))
+    from tt2.config import TTSConfig
+    from tt2.dist import _buckets
+    from tt2.params import Layout, build_slots
+    cfg = TTSConfig()
+    lay = Layout(build_slots(cfg))
+    names = (["post.conv0.w", "heads.w"] + [f"dec{l}.qkv.w" for l in reversed(range(cfg.n_dec))] + ["dec.fc1.w"] +
+             [f"enc{l}.qkv.w" for l in reversed(range(cfg.n_enc))] + ["enc.embed"])
+    cuts = [lay.offset(n) for n in names]
+    per = (25 << 20) // 4
+    b = _buckets(lay.numel, per, cuts)
+    assert b[0][1] == lay.numel and b[-1][0] == 0
+    assert all(b[i][0] == b[i + 1][1] for i in range(len(b) - 1))
+    assert all(lo in cuts for lo, _ in b)
+    assert len(b) == 1 + cfg.n_dec + 1 + cfg.n_enc + 1          # heads merged into decoder layer 5
+    assert (lay.offset("heads.w"), lay.offset("post.conv0.w")) not in b
+    # fixed slices without cuts
+    f = _buckets(1000, 300)
+    assert f == [(700, 1000), (400, 700), (100, 400), (0, 100)]

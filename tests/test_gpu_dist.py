@@ -85,9 +85,11 @@ class _Snap:
     def _init_snap(self):
         self.snaps, self.bad, self.steps = [], [], 0
 
-    def _launch(self, lo, hi):
+    def _launch(self, lo, hi, after=None):
+        if after is not None:   # the snapshot is taken on the stream the bucket is final on
+            torch.cuda.current_stream().wait_event(after)
         self.snaps.append((lo, hi, self.flat[lo:hi].clone()))
-        super()._launch(lo, hi)
+        super()._launch(lo, hi, after)
 
     def finish(self):
         super().finish()
@@ -242,18 +244,19 @@ class IssueSnap:
         return [(lo, hi) for lo, hi in self.sync.buckets if not torch.equal(self.buf[lo:hi], self.sync.flat[lo:hi])]
 
 
-@pytest.mark.parametrize("overlap", [False, True])
-def test_misplaced_grad_ready_is_caught(nccl_group, overlap):
+@pytest.mark.parametrize("overlap,layers", [(False, False), (True, False), (True, True)])
+def test_misplaced_grad_ready_is_caught(nccl_group, overlap, layers):
     """Negative control for the checks above: the engine's bucket hook shifted so every bucket
-    is handed to RCCL 2M elements (8 MB of gradients) before it is final.  The captured step
-    must then show buckets whose final gradients differ from what the issuing stream copied at
-    the hand-off, with the in-place and with the overlapped (side-stream) weight gradients;
-    the correctly placed hook shows none (IssueSnap agrees with InGraphSnap's positive check)."""
+    is handed to RCCL early -- 2M elements (8 MB of gradients) with fixed 25 MB buckets, 4M (more
+    than a layer) with layer-aligned ones -- before it is final.  The captured step must then show
+    buckets whose final gradients differ from what the issuing stream copied at the hand-off, with
+    the in-place and with the overlapped (side-stream) weight gradients; the correctly placed hook
+    shows none (IssueSnap agrees with InGraphSnap's positive check)."""
     B, Tx, Ty, text, tl, mel, ml = _cfg2_batch()
-    for shift, want_bad in ((2 << 20, True), (0, False)):
+    for shift, want_bad in (((4 if layers else 2) << 20, True), (0, False)):
         m = _model()
         m.engine.wgrad_overlap = overlap
-        sync = attach(m, kind="rccl")
+        sync = attach(m, kind="rccl", layer_buckets=layers)
         ready = sync.ready
         sync.ready = lambda off, r=ready, s=shift: r(max(0, off - s))   # the captured step hooks it too
         snap = IssueSnap(sync)
@@ -300,4 +303,62 @@ def test_syncbn_rccl_exchange_in_graph_one_rank(nccl_group):
     torch.cuda.synchronize()
     assert torch.equal(ref.engine.params, dp.engine.params)
     assert torch.equal(ref.engine.stats, dp.engine.stats)
+    sync.close()
+
+
+def test_comm_standin_kernel():
+    """tt2_comm_standin (the DP stand-in's per-bucket kernel): copies `bytes` from src into the
+    scratch buffer, leaves src unchanged, and every work group holds its CU for the requested time
+    (its {start, end} wall-clock record spans at least that)."""
+    import ctypes as C
+    from tt2._lib import check, lib
+    torch.manual_seed(5)
+    src = torch.randn(1 << 20, device="cuda")
+    keep = src.clone()
+    scratch = torch.zeros(1 << 20, device="cuda")
+    rec = torch.zeros(2 * 32, dtype=torch.int64, device="cuda")
+    nbytes, secs = 3 << 20, 200e-6
+    check(lib().tt2_comm_standin(C.c_void_p(src.data_ptr()), C.c_void_p(scratch.data_ptr()), nbytes, secs, 32,
+                                 C.c_void_p(rec.data_ptr()), C.c_void_p(torch.cuda.current_stream().cuda_stream)),
+          "tt2_comm_standin")
+    torch.cuda.synchronize()
+    assert torch.equal(src, keep)
+    n = nbytes // 4
+    assert torch.equal(scratch[:n], src[:n]) and scratch[n:].abs().sum().item() == 0
+    r = rec.view(32, 2).cpu()
+    assert (r[:, 0] > 0).all()
+    assert ((r[:, 1] - r[:, 0]) >= int(0.95 * secs * 1e8)).all()   # 100 MHz wall clock
+    assert lib().tt2_comm_standin(C.c_void_p(src.data_ptr()), C.c_void_p(scratch.data_ptr()), 16, 2.0, 32,
+                                  None, None) != 0   # > 1 s refused
+
+
+def test_standin_dp_step_matches_single_graph(nccl_group):
+    """The DP schedule with the stand-in transport (bench.py --dp-standin): each bucket handed to
+    the comm stream inside the one captured step runs the stand-in kernel instead of an all-reduce;
+    the gradients are untouched, so the captured DP step reproduces the plain single-graph step bit
+    for bit, and every bucket's stand-in ran in each replay (span records)."""
+    from tt2.dist import StandinGradSync
+    g = torch.Generator().manual_seed(3)
+    B, Tx, Ty = 2, 24, 48
+    text = torch.randint(1, 80, (B, Tx), generator=g).cuda()
+    tl = torch.tensor([24, 17]).cuda()
+    mel = torch.randn(B, Ty, 80, generator=g).cuda()
+    ml = torch.tensor([48, 30]).cuda()
+    ref, dp = _model(), _model()
+    sync = attach(dp, sync_cls=StandinGradSync, bucket_bytes=4 << 20)
+    assert isinstance(sync, StandinGradSync) and sync.in_graph and len(sync.buckets) > 2
+    for _ in range(2):
+        ref.train_step(text, tl, mel, ml)
+        dp.train_step(text, tl, mel, ml, sync_grads=sync.finish)
+    sync.rec = torch.zeros(len(sync.buckets), 2 * sync.wgs, dtype=torch.int64, device="cuda")
+    run_ref = ref.capture_train_step(B, Tx, Ty)
+    run_dp = dp.capture_train_step(B, Tx, Ty, sync_grads=sync.finish)
+    for _ in range(2):
+        sync.rec.zero_()
+        la = run_ref(text, tl, mel, ml).clone()
+        lb = run_dp(text, tl, mel, ml).clone()
+        assert torch.equal(la, lb)
+        torch.cuda.synchronize()
+        assert (sync.rec.view(len(sync.buckets), -1, 2)[:, :, 0] > 0).all()
+    assert torch.equal(ref.engine.params, dp.engine.params)
     sync.close()

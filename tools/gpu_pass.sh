@@ -122,6 +122,47 @@ for s in $STEPS; do
                echo "${pk:-current} $(lastms "$OUT/ab_run.json")" >> "$OUT/pkgab.txt"
              done
            done ;;
+    dpab) for i in 1 2; do   # DP schedule on one GPU: no exchange / 1-rank RCCL in-graph / N-rank stand-in
+            for m in "" "--force-dp" "--dp-standin"; do
+              run "dpab $m" 90 200 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-decode --no-ragged \
+                $m > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
+              echo "${m:-plain} $(lastms "$OUT/ab_run.json")" >> "$OUT/dpab.txt"
+            done
+          done ;;
+    bucketab) for i in 1 2; do   # bucket size under the stand-in (and the 1-rank RCCL path)
+                for mb in ${BUCKETS:-25 12.5 8}; do
+                  for m in ${BUCKET_MODES:---dp-standin}; do
+                    run "bucketab $mb $m" 90 200 env TT2_BUCKET_MB=$mb python -u bench.py --steps 30 --warmup 5 \
+                      --no-cpu-baseline --no-decode --no-ragged $m > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
+                    echo "$mb $m $(lastms "$OUT/ab_run.json")" >> "$OUT/bucketab.txt"
+                  done
+                done
+              done ;;
+    modeab) for i in 1 2; do   # layer-aligned vs fixed-size DP buckets, no-DP step beside them
+              run "modeab plain" 90 200 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-decode \
+                --no-ragged > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
+              echo "plain $(lastms "$OUT/ab_run.json")" >> "$OUT/modeab.txt"
+              for mode in layers fixed; do
+                for m in --dp-standin --force-dp; do
+                  run "modeab $mode $m" 90 200 env TT2_BUCKET_MODE=$mode python -u bench.py --steps 30 --warmup 5 \
+                    --no-cpu-baseline --no-decode --no-ragged $m > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
+                  echo "$mode $m $(lastms "$OUT/ab_run.json")" >> "$OUT/modeab.txt"
+                done
+              done
+            done ;;
+    deferab) for i in 1 2; do   # bucket hand-off right after its side job (0) or after the next one (1)
+               run "deferab plain" 90 200 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-decode \
+                 --no-ragged > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
+               echo "plain $(lastms "$OUT/ab_run.json")" >> "$OUT/deferab.txt"
+               for dfr in 0 1; do
+                 for m in --dp-standin --force-dp; do
+                   run "deferab $dfr $m" 90 200 env TT2_DEFER_FORK=$dfr python -u bench.py --steps 30 --warmup 5 \
+                     --no-cpu-baseline --no-decode --no-ragged $m > "$OUT/ab_run.json" 2> "$OUT/ab_run.err"
+                   echo "defer=$dfr $m $(lastms "$OUT/ab_run.json")" >> "$OUT/deferab.txt"
+                 done
+               done
+             done ;;
+    otls) run otls 90 200 python -u tools/overlap_timeline.py --standin > "$OUT/otl_standin.txt" 2>&1 ;;
     det) run det 60 200 python -u tools/det_check.py > "$OUT/det.txt" 2>&1 ;;
     newt) run newt 120 600 python -u -m pytest ${NEWT:-tests/test_gpu_capture.py tests/test_gpu_dp_order.py} -x -v \
             --timeout 600 --timeout-method thread > "$OUT/new_tests.log" 2>&1 ;;

@@ -845,3 +845,44 @@ extern "C" int tt2_step_bump(int32_t* step, uint32_t* seed, hipStream_t s) {
   hipLaunchKernelGGL(step_bump_kernel, dim3(1), dim3(64), 0, s, step, seed);
   return tt2_check_launch(hipGetLastError(), "tt2_step_bump");
 }
+
+// ------------------------------------------------------------ DP exchange stand-in
+// A kernel with the footprint of one rank's share of an N-rank ring all-reduce of a bucket
+// (measurement of the DP schedule on one GPU, tt2/dist.py StandinGradSync): `wgs` work groups
+// (RCCL's channels) copy `bytes` from the bucket into a scratch buffer (the reduce-scatter /
+// all-gather traffic through HBM), then each holds its CU until `ticks` of the device wall clock
+// have passed since it started (the time the ring waits on its xGMI links).  Every wave exits:
+// the wait is bounded by the clock, not by a flag.
+__global__ __launch_bounds__(256) void comm_standin_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                           int64_t n16, uint64_t ticks, uint64_t* rec) {
+  const uint64_t t0 = wall_clock64();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  if (rec && threadIdx.x == 0) {   // this work group's {start, end} on the wall clock
+    rec[2 * blockIdx.x] = t0;
+    rec[2 * blockIdx.x + 1] = wall_clock64();
+  }
+}
+
+extern "C" int tt2_comm_standin(const void* src, void* scratch, size_t bytes, double seconds, int32_t wgs,
+                                uint64_t* rec, hipStream_t s) {
+  if (!src || !scratch || wgs <= 0 || wgs > 1024 || seconds < 0 || seconds > 1.0 ||
+      (reinterpret_cast<uintptr_t>(src) % 16) || (reinterpret_cast<uintptr_t>(scratch) % 16))
+    return tt2_set_error(TT2_E_INVALID, "tt2_comm_standin: 16-B aligned src / scratch, 0 < wgs <= 1024, "
+                                        "0 <= seconds <= 1");
+  static int khz = 0;
+  if (!khz) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) {
+      khz = 0;
+      return tt2_set_error(TT2_E_HIP, "tt2_comm_standin: no wall clock rate");
+    }
+  }
+  const uint64_t ticks = (uint64_t)(seconds * khz * 1e3);
+  hipLaunchKernelGGL(comm_standin_kernel, dim3(wgs), dim3(256), 0, s, reinterpret_cast<const u32x4*>(src),
+                     reinterpret_cast<u32x4*>(scratch), (int64_t)(bytes / 16), ticks, rec);
+  return tt2_check_launch(hipGetLastError(), "tt2_comm_standin");
+}

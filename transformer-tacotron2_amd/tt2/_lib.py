@@ -356,4 +356,5 @@ SIGNATURES.update({
     "tt2_comm_unique_id": ([vp], C.c_int),
     "tt2_comm_init": ([C.POINTER(vp), i32, vp, i32], C.c_int),
     "tt2_comm_destroy": ([vp], C.c_int),
+    "tt2_comm_standin": ([vp, vp, sz, C.c_double, i32, vp, vp], C.c_int),
 })

@@ -47,10 +47,24 @@ def rccl_env() -> dict:
     return {k: os.environ[k] for k in RCCL_ENV_KEYS if k in os.environ}
 
 
-def _buckets(n: int, per: int) -> list[tuple[int, int]]:
+def _buckets(n: int, per: int, cuts=None) -> list[tuple[int, int]]:
+    """Buckets [lo, hi) from the end of the flat buffer down.  Without cuts: `per` elements each.
+    With cuts (the offsets at which the backward reports gradients final, engine.ready_offsets):
+    layer-aligned buckets, one per reported range, a range smaller than per / 4 merged into the
+    one below it -- a bucket is then complete as soon as its layer is, where fixed-size buckets
+    straddling two layers wait for the lower one."""
+    if not cuts:
+        out, hi = [], n
+        while hi > 0:
+            lo = max(0, hi - per)
+            out.append((lo, hi))
+            hi = lo
+        return out
+    pts = sorted({c for c in cuts if 0 < c < n} | {0}, reverse=True)
     out, hi = [], n
-    while hi > 0:
-        lo = max(0, hi - per)
+    for lo in pts:
+        if hi - lo < per // 4 and lo > 0:
+            continue   # too small: extend down to the next cut
         out.append((lo, hi))
         hi = lo
     return out
@@ -59,10 +73,10 @@ def _buckets(n: int, per: int) -> list[tuple[int, int]]:
 class GradSync:
     in_graph = False
 
-    def __init__(self, flat_grads: torch.Tensor, bucket_bytes: int = 25 << 20, group=None):
+    def __init__(self, flat_grads: torch.Tensor, bucket_bytes: int = 25 << 20, group=None, cuts=None):
         self.flat = flat_grads
         self.group = group
-        self.buckets = _buckets(flat_grads.numel(), max(1, bucket_bytes // flat_grads.element_size()))
+        self.buckets = _buckets(flat_grads.numel(), max(1, bucket_bytes // flat_grads.element_size()), cuts)
         self.reset()
 
     @property
@@ -73,14 +87,19 @@ class GradSync:
         self.next = 0
         self.works = []
 
-    def _launch(self, lo, hi):
+    accepts_after = False   # ready(offset, after=event): see RcclGradSync
+
+    def _launch(self, lo, hi, after=None):
+        if after is not None:
+            torch.cuda.current_stream().wait_event(after)
         w = dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self.works.append(w)
 
-    def ready(self, offset: int):
-        """Every gradient at flat index >= offset is final."""
+    def ready(self, offset: int, after=None):
+        """Every gradient at flat index >= offset is final (on the current stream, or once the
+        event `after` has completed)."""
         for i in self.take_ready(offset):
-            self._launch(*self.buckets[i])
+            self._launch(*self.buckets[i], after=after)
 
     def take_ready(self, offset: int) -> list[int]:
         """Indices of the buckets that became complete at offset (advances the cursor
@@ -138,13 +157,16 @@ class GradSync:
 
 class RcclGradSync(GradSync):
     """Bucketed SUM all-reduce over libtt2's RCCL communicator on a comm stream, ordered
-    after the producing kernels by stream waits only (capturable: ``in_graph``)."""
+    after the producing kernels by stream waits only (capturable: ``in_graph``).
+    ready(offset, after=event): the comm stream waits for that event instead of the current
+    stream (the overlapped backward hands a bucket over after issuing its next side job)."""
     in_graph = True
+    accepts_after = True
 
-    def __init__(self, flat_grads: torch.Tensor, bucket_bytes: int = 25 << 20, group=None):
+    def __init__(self, flat_grads: torch.Tensor, bucket_bytes: int = 25 << 20, group=None, cuts=None):
         from . import _lib
         self._lib = _lib
-        super().__init__(flat_grads, bucket_bytes, group)
+        super().__init__(flat_grads, bucket_bytes, group, cuts)
         os.environ.setdefault("NCCL_MIN_NCHANNELS", str(RCCL_MIN_CHANNELS))
         L = _lib.lib()
         rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -164,11 +186,14 @@ class RcclGradSync(GradSync):
         # bucket's all-reduce is issued (captured with it), e.g. to copy what RCCL produced
         self.snap_hook = None
 
-    def _launch(self, lo, hi):
+    def _launch(self, lo, hi, after=None):
         if not (self.comm and self.comm.value):
             raise RuntimeError("RcclGradSync: the communicator was closed")
         cur = torch.cuda.current_stream()
-        self.stream.wait_stream(cur)          # the bucket's gradients are final on `cur`
+        if after is not None:
+            self.stream.wait_event(after)     # the bucket's gradients are final at `after`
+        else:
+            self.stream.wait_stream(cur)      # the bucket's gradients are final on `cur`
         if self._span is None and not torch.cuda.is_current_stream_capturing():
             # eager step: the exchange's span on the comm stream, from the first bucket's start
             # to finish() (StepMetrics' allreduce_ms; a captured step records no events)
@@ -219,6 +244,54 @@ class RcclGradSync(GradSync):
             torch.cuda.synchronize()
             self._lib.check(self._lib.lib().tt2_comm_destroy(self.comm), "tt2_comm_destroy")
             self.comm = C.c_void_p()
+
+
+class StandinGradSync(RcclGradSync):
+    """RcclGradSync's schedule with a stand-in transport: the DP step of an N-rank job rehearsed on
+    one GPU (bench.py --dp-standin).  Every bucket is handed to the comm stream exactly as in the
+    production N-rank step (from the overlapped backward's side stream, inside the one captured
+    graph), but instead of the 1-rank all-reduce the comm stream runs tt2_comm_standin with the
+    footprint of this rank's share of an N-rank ring all-reduce: `wgs` work groups (RCCL's
+    channels, NCCL_MIN_NCHANNELS), 2 (N-1)/N x bucket bytes of HBM copy traffic (read + write), and
+    those CUs held for 2 (N-1)/N x bucket / busbw seconds (the ring's time on the xGMI links).  The
+    gradients are not changed (at world 1 the sum is the identity), so the step's numerics are the
+    plain ones.  Knobs: TT2_DP_STANDIN_N (8), TT2_DP_STANDIN_GBPS (bus bandwidth, 300),
+    TT2_DP_STANDIN_WG (32)."""
+
+    def __init__(self, flat_grads: torch.Tensor, bucket_bytes: int = 25 << 20, group=None, cuts=None):
+        super().__init__(flat_grads, bucket_bytes, group, cuts)
+        self.ranks = int(os.environ.get("TT2_DP_STANDIN_N", "8"))
+        self.busbw = float(os.environ.get("TT2_DP_STANDIN_GBPS", "300")) * 1e9
+        self.wgs = int(os.environ.get("TT2_DP_STANDIN_WG", str(RCCL_MIN_CHANNELS)))
+        per = max(hi - lo for lo, hi in self.buckets) * flat_grads.element_size()
+        self._scratch = torch.empty(per // 4 + 4, dtype=torch.float32, device=flat_grads.device)
+        # per bucket, each work group's {start, end} (device wall clock) when recording (tools)
+        self.rec = None   # torch.int64 [len(buckets), 2 * wgs] or None
+
+    def params(self) -> dict:
+        return {"ranks_modelled": self.ranks, "busbw_GBps": self.busbw / 1e9, "work_groups": self.wgs}
+
+    def _launch(self, lo, hi, after=None):
+        if not (self.comm and self.comm.value):
+            raise RuntimeError("StandinGradSync: closed")
+        if after is not None:
+            self.stream.wait_event(after)
+        else:
+            self.stream.wait_stream(torch.cuda.current_stream())
+        esz = self.flat.element_size()
+        nbytes = (hi - lo) * esz
+        f = 2.0 * (self.ranks - 1) / self.ranks
+        src = self.flat.data_ptr() + lo * esz
+        pad = (-src) % 16                     # buckets start at any element: copy from the next 16-B boundary
+        copy = max(0, int(f / 2 * nbytes) - pad) // 16 * 16   # read + write = f x bucket bytes
+        rec = None
+        if self.rec is not None:
+            bi = next(i for i, (a, b) in enumerate(self.buckets) if a == lo and b == hi)
+            rec = C.c_void_p(self.rec[bi].data_ptr())
+        self._lib.check(self._lib.lib().tt2_comm_standin(C.c_void_p(src + pad), C.c_void_p(self._scratch.data_ptr()),
+                                                         copy, f * nbytes / self.busbw, self.wgs, rec,
+                                                         C.c_void_p(self.stream.cuda_stream)), "tt2_comm_standin")
+        self.pending = True
 
 
 class BnSync:
@@ -310,18 +383,22 @@ def sync_kind(group=None) -> str:
 
 
 def attach(model, group=None, bucket_bytes: int = 25 << 20, kind: str | None = None,
-           sync_bn: bool = False, sync_cls=None, bn_cls=None) -> GradSync:
+           sync_bn: bool = False, sync_cls=None, bn_cls=None, layer_buckets: bool | None = None) -> GradSync:
     """Wire a TransformerTTS for data parallelism: gradient pre-scaling and the
     bucket hook.  Returns the sync object whose finish() goes between backward and
     the optimizer step (pass it as train_step(..., sync_grads=sync.finish)).
     sync_bn: SyncBatchNorm (the encoder pre-net's and post-net's BatchNorms take their
     training statistics over every rank's rows; BnSync).
     sync_cls / bn_cls: the exchange classes (default RcclGradSync or GradSync by `kind`, and
-    BnSync); a subclass may swap the transport, as the issue-order test's recording syncs do."""
+    BnSync); a subclass may swap the transport, as the issue-order test's recording syncs do.
+    layer_buckets: buckets cut where the backward reports layers final (default: TT2_BUCKET_MODE,
+    "layers" unless it says "fixed"), else fixed bucket_bytes slices from the end."""
     eng = model.engine
     kind = kind or sync_kind(group)
     cls = sync_cls or (RcclGradSync if kind == "rccl" else GradSync)
-    sync = cls(eng.grads, bucket_bytes, group)
+    if layer_buckets is None:
+        layer_buckets = os.environ.get("TT2_BUCKET_MODE", "layers") != "fixed"
+    sync = cls(eng.grads, bucket_bytes, group, cuts=eng.ready_offsets() if layer_buckets else None)
     eng.grad_scale = 1.0 / sync.world
     eng.grad_ready_hook = sync.ready
     sync.engine = eng

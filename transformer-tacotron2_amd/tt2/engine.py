@@ -291,6 +291,11 @@ class TTSEngine:
         self.dropout_enabled = True
         self.grad_scale = 1.0
         self.grad_ready_hook = None   # called as hook(flat_offset) during backward (DP bucketing)
+        self._ready_set = set(self.ready_names())
+        # overlapped backward with DP: hand each bucket to the comm stream after the next side job
+        # is issued, ordered by an event (_fire_deferred); TT2_DEFER_FORK=0: right after its job
+        self.defer_bucket_fork = os.environ.get("TT2_DEFER_FORK", "1") != "0"
+        self._deferred = []
         self.bn_sync = None   # SyncBatchNorm exchange (tt2/dist.py BnSync), None: per-replica statistics
         self.opt = dict(lr=1.0, beta1=0.9, beta2=0.98, eps=1e-9, weight_decay=0.0, clip_norm=1.0, warmup=4000.0,
                         noam=True)
@@ -481,6 +486,7 @@ class TTSEngine:
             self._side_ws = ops.Workspace()
         self._side.wait_stream(torch.cuda.current_stream())
         self._jobs = []
+        self._deferred = []
         self._side_live = False
 
     def _push_job(self, q, fin=None, ready=()):
@@ -494,12 +500,36 @@ class TTSEngine:
         self._side.wait_event(job["ev"])
         with torch.cuda.stream(self._side):
             self._launch_wgrads(job["q"], job["fin"], self._side_ws, side=True)
+            self._fire_deferred()
+            ev = None
+            if job["ready"] and self.grad_ready_hook is not None and self.defer_bucket_fork:
+                ev = torch.cuda.Event()
+                ev.record()
             for name in job["ready"]:
                 off = self.lay.offset(name)
                 if self.grad_ready_hook is not None:
-                    self.grad_ready_hook(off)
+                    if ev is not None:
+                        self._deferred.append((off, ev))
+                    else:
+                        self.grad_ready_hook(off)
                 self._norm_range(off)
         job["done"] = True
+
+    def _fire_deferred(self):
+        """The bucket hand-offs of the previous side job, issued only now that this job's weight
+        gradients are on the side stream, each ordered after an event recorded at the end of its
+        own job (defer_bucket_fork).  Issued right after their job, the comm stream's exchange
+        kernels were created ahead of the side stream's next job in the captured graph, and the
+        graph's executor ran the two branches one after the other (every side job then waited for
+        the previous bucket's exchange)."""
+        h = self.grad_ready_hook
+        after_ok = getattr(getattr(h, "__self__", None), "accepts_after", False)
+        for off, ev in self._deferred:
+            if after_ok:
+                h(off, after=ev)
+            else:   # a hook without the event form: ordered after everything issued on the side stream
+                h(off)
+        self._deferred = []
 
     def _norm_begin(self, side: bool):
         """The clip norm's squared sum is taken over fixed ranges of the flat gradients, one per
@@ -553,6 +583,7 @@ class TTSEngine:
             self._start_side()
         self._pump(len(self._jobs))
         with torch.cuda.stream(self._side):
+            self._fire_deferred()
             self._norm_range(0)
         torch.cuda.current_stream().wait_stream(self._side)
         self._jobs = None
@@ -846,7 +877,21 @@ class TTSEngine:
                      A["g_after"], A.B, A.Ty, c.n_mels, c.stop_pos_weight, self.grad_scale, ws=self.ws)
 
     # ------------------------------------------------------------ backward
+    def ready_names(self) -> list[str]:
+        """The parameters whose flat offsets the backward reports as final (_ready), in the order
+        it reports them: everything at or above each offset is final then.  DP buckets cut at
+        these offsets (dist.attach, layer-aligned buckets) become complete as soon as their layer
+        is done."""
+        c = self.cfg
+        return (["post.conv0.w", "heads.w"] + [f"dec{l}.qkv.w" for l in reversed(range(c.n_dec))] + ["dec.fc1.w"] +
+                [f"enc{l}.qkv.w" for l in reversed(range(c.n_enc))] + ["enc.embed"])
+
+    def ready_offsets(self) -> list[int]:
+        return [self.lay.offset(n) for n in self.ready_names()]
+
     def _ready(self, name):
+        if name not in self._ready_set:
+            raise RuntimeError(f"engine._ready({name!r}): not in ready_names() (DP bucket cuts would miss it)")
         if self._jobs is not None:
             # the bucket is final once the queued weight gradients have run: its hook goes
             # with them, in a job ordered after everything the main stream has issued so far
