@@ -12,11 +12,15 @@ from gemm_ab import graph_of, time_graph, ops  # noqa: E402
 
 SHAPES = [(12800, 2048, 512), (12800, 1536, 512), (12800, 512, 512), (12800, 512, 2048), (2048, 6144, 512),
           (2048, 2048, 512), (2048, 512, 2048), (4096, 4096, 4096), (8192, 8192, 8192)]
+# `enc`: the encoder chain's 2048-row products (forward QKV / o / FFN1 / FFN2 / pre-net conv as a plain
+# K = 2560 GEMM, and the dgrads' M x N x K: o, qkv, FFN1)
+ENC_SHAPES = [(2048, 1536, 512), (2048, 512, 512), (2048, 2048, 512), (2048, 512, 2048), (2048, 512, 2560),
+              (2048, 512, 1536)]
 
 
 def main():
     torch.manual_seed(0)
-    for m, n, k in SHAPES:
+    for m, n, k in (ENC_SHAPES if "enc" in sys.argv[1:] else SHAPES):
         A = torch.randn(m, k, device="cuda").bfloat16()
         B = (torch.randn(n, k, device="cuda") / k ** 0.5).bfloat16()
         C = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)

@@ -216,6 +216,84 @@ __global__ __launch_bounds__(256) void mix_k(const char* src, int tiles, int* si
   if (threadIdx.x == 0 && lds[5] == 123) *sink = 1;
 }
 
+// v7's K loop without its epilogue: 4 loader waves fill the ring by LDS-DMA as dma_k (step t + 2
+// issued at step t), 8 reader waves read the stage of step t as v7's MFMA waves do (16
+// ds_read_b128 per wave per step = 128 KB per step per CU) and, with MF, issue v7's 32
+// v_mfma_f32_16x16x32_bf16 per wave per step on what they read; one barrier per step.  RD = 0:
+// the loaders alone in a 768-thread work group.  Shows how much the fragment reads slow the fill.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+template <bool RD, bool MF, bool FRESH>
+__global__ __launch_bounds__(768, 1) void con_k(const char* src, int tiles, int* sink) {
+  __shared__ __attribute__((aligned(1024))) char lds[STAGES * STEP];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int NI = 12;
+  const int b = blockIdx.x, blk0 = (b % 8) * 8 + (b / 8) / 4;
+  const int total = tiles * NSTEP;
+  if (w >= 8) {   // loaders
+    const int lw = w - 8;
+    auto issue = [&](int step) {
+      const int tile = step / NSTEP;
+      const int blk = FRESH ? (blk0 + 64 * tile) % NBLK : blk0;
+      const char* base = src + (int64_t)blk * ROWS * LD + (step % NSTEP) * 128;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int inst = lw * NI + i, row = inst * 8 + (lane >> 3);
+        __builtin_amdgcn_global_load_lds((gvoid_t*)(base + (int64_t)row * LD + (lane & 7) * 16),
+                                         (lvoid_t*)(lds + (step % STAGES) * STEP + inst * 1024), 16, 0, 0);
+      }
+    };
+    issue(0);
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    BARRIER();
+    for (int t = 0; t < total; ++t) {
+      if (t + 2 < total) { issue(t + 2); asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); }
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      BARRIER();
+    }
+    return;
+  }
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  BARRIER();
+  for (int t = 0; t < total; ++t) {
+    if (RD) {
+      const char* st = lds + (t % STAGES) * STEP;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8_t fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          fa[i] = *(const bf16x8_t*)(st + (((w * 8 + kk * 4 + i) * 1024) % (32 * 1024)) + lane * 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          fb[j] = *(const bf16x8_t*)(st + 32 * 1024 + (((w * 8 + kk * 4 + j) * 1024) % (16 * 1024)) + lane * 16);
+        if (MF) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][0][0] += (float)fa[i][0] + (float)fb[i][1];
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    BARRIER();
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sum += acc[i][j][0];
+  if (sum == 123.f) *sink = 1;
+}
+
 int main() {
   const int WG = 256, TILES = 64;
   const size_t bytes = (size_t)NBLK * ROWS * LD;   // 96 MB
@@ -249,6 +327,25 @@ int main() {
   run("fresh+P4", dma_k<4, true>);
   run("fresh+P6", dma_k<6, true>);
   run("resident+P2", dma_k<2, false>);
+  auto run768 = [&](const char* name, auto kern) {
+    float best = 1e9;
+    for (int rep = 0; rep < 4; ++rep) {
+      CK(hipEventRecord(e0));
+      kern<<<WG, 768>>>(src, TILES, sink);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      if (rep > 0 && ms < best) best = ms;
+    }
+    const double b = (double)WG * TILES * NSTEP * STEP;
+    printf("%-12s %8.1f us  %6.2f TB/s  %5.1f B/clk/CU  %6.0f cyc/step\n", name, best * 1e3,
+           b / (best * 1e-3) / 1e12, b / (best * 1e-3) / WG / 2.4e9, best * 1e-3 * 2.4e9 / (TILES * NSTEP));
+  };
+  run768("v7 loaders", con_k<false, false, true>);
+  run768("+reads", con_k<true, false, true>);
+  run768("+reads+mfma", con_k<true, true, true>);
+  run768("res +r+mfma", con_k<true, true, false>);
   run("mix dma", mix_k<0>);
   run("mix reg", mix_k<1>);
   run("mix hyb", mix_k<2>);

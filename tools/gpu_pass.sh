@@ -162,6 +162,15 @@ for s in $STEPS; do
                  done
                done
              done ;;
+    encblas) run encblas 90 200 python -u tools/blas_cmp.py enc > "$OUT/encblas.txt" 2>&1
+             run encblas_prof 90 300 rocprofv3 --kernel-trace --stats -d "$OUT/blas" -o run --output-format csv -- \
+               python3 tools/blas_cmp.py enc > "$OUT/encblas_prof.txt" 2>&1 ;;
+    libenc) for i in 1 2; do   # encoder shapes (tools/blas_cmp.py enc) against an A/B library
+              for lib in abl/${LIBENC_OLD:-g8r8}.so transformer-tacotron2_amd/tt2/libtt2.so; do
+                echo "== $lib" >> "$OUT/libenc.txt"
+                run "libenc $lib" 60 150 env TT2_LIB=$lib python -u tools/blas_cmp.py enc >> "$OUT/libenc.txt" 2>&1
+              done
+            done ;;
     otls) run otls 90 200 python -u tools/overlap_timeline.py --standin > "$OUT/otl_standin.txt" 2>&1 ;;
     det) run det 60 200 python -u tools/det_check.py > "$OUT/det.txt" 2>&1 ;;
     newt) run newt 120 600 python -u -m pytest ${NEWT:-tests/test_gpu_capture.py tests/test_gpu_dp_order.py} -x -v \

@@ -1826,7 +1826,10 @@ hipError_t launch7(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, 
 // leaves through LDS as whole 128-B rows.
 // =====================================================================================
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-constexpr int G8_NT = 512, G8_STAGES = 4;   // 4 MFMA waves + 4 loader waves
+#ifndef G8_RING   // ring stages (a power of two); the loaders run G8_RING - 1 steps ahead
+#define G8_RING 4
+#endif
+constexpr int G8_NT = 512, G8_STAGES = G8_RING;   // 4 MFMA waves + 4 loader waves
 constexpr int G8_TILE = 64 * 128;          // bytes per operand tile: 64 rows x 64 bf16
 constexpr int G8_STAGE = 2 * G8_TILE;
 
@@ -1976,7 +1979,7 @@ TT2_DEV void g8_stats(const EpiParams& E, char* smem, int m0, int n0, int M, int
 }
 
 template <bool BKC, int SM = 0>
-__global__ __launch_bounds__(G8_NT, 2) void gemm8_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
+__global__ __launch_bounds__(G8_NT, G8_STAGES <= 4 ? 2 : 1) void gemm8_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
                                                          int ntn, int items, unsigned long long* span) {
   __shared__ __attribute__((aligned(1024))) char smem[G8_STAGES * G8_STAGE];
   __shared__ int span_done;
@@ -1996,18 +1999,25 @@ __global__ __launch_bounds__(G8_NT, 2) void gemm8_kernel(OpDesc A, OpDesc B, Epi
       else g8_issue<true>(A, st, m0, 64 * t, lane, lw);
       g8_issue<BKC>(B, st + G8_TILE, n0, 64 * t, lane, lw);
     };
-    // three steps ahead; each step is 4 copies per loader wave
-    for (int t = 0; t < 3 && t < nkt; ++t) issue(t);
-    if (nkt >= 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (nkt == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // G8_STAGES - 1 steps ahead; each step is 4 copies per loader wave
+    constexpr int AH = G8_STAGES - 1;
+    auto wait_ahead = [](int ahead) {   // step t+1 landed, `ahead` later steps may stay in flight
+      switch (ahead) {
+        case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    };
+    for (int t = 0; t < AH && t < nkt; ++t) issue(t);
+    wait_ahead(min(AH, nkt) - 1);   // step 0 landed
     __builtin_amdgcn_s_barrier();
     for (int t = 0; t < nkt; ++t) {
-      if (t + 3 < nkt) issue(t + 3);   // into the stage step t-1 used: free since the last barrier
-      const int ahead = min(2, nkt - 2 - t);   // steps after t+1 that may stay in flight
-      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (t + AH < nkt) issue(t + AH);   // into the stage step t-1 used: free since the last barrier
+      wait_ahead(min(AH - 1, nkt - 2 - t));
       __builtin_amdgcn_s_barrier();    // step t+1 landed
     }
   } else {   // ------------------------------------------------------- MFMA waves
