@@ -54,7 +54,7 @@ def test_state_dict_roundtrip(pair32):
 # Dropout seed: with seed 1234 one kept encoder-layer-3 FFN pre-activation is +1.3e-6 (f64)
 # and the engine's f32 sum lands on the other side of the ReLU kink (the CPU f32 oracle does
 # not), which moves every gradient below that layer by ~1.4e-3; seeds 1-5 give <= 6e-6 on
-# every gradient against a float64 oracle (tools/fp32_grad_err.py, tools/kink_check.py).
+# every gradient against a float64 oracle (tools/fp32_grad_err.py; round 1's tools/kink_check.py is in git history).
 @pytest.mark.parametrize("train,drop_seed", [(False, None), (True, None), (True, 1)])
 def test_forward_backward_fp32(train, drop_seed):
     oracle, model = build(torch.float32)

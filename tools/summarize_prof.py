@@ -1,5 +1,5 @@
-"""Turn a tools/profile_bench.sh run (gpurun_out/prof_<tag>/) into committed
-summaries under profiles/:
+"""Turn a `tools/gpu_pass.sh <tag> prof` run (gpurun_out/<tag>/kt, bench_kt.json; called on the GPU
+box by tools/summarize_pass.sh) into committed summaries under profiles/:
 
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats table (as produced)
   profiles/<tag>_kernel_stats.md    top kernels, per-step times, vs bench.py's live figure
@@ -34,7 +34,7 @@ def per_kernel_counter(path, counter):
 
 def main(tag: str):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
-    if not os.path.isdir(src):  # tools/gpu_round.sh layout
+    if not os.path.isdir(src):  # tools/gpu_pass.sh layout (prof_<tag>: the round-1 layout)
         src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -48,7 +48,7 @@ def main(tag: str):
     total_ns = sum(float(r["TotalDurationNs"]) for r in rows)
     lines = [f"# rocprofv3 kernel stats — {tag}", "",
              f"Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps {bench['steps']} "
-             f"--warmup {bench['warmup']} --no-cpu-baseline --no-decode` (tools/profile_bench.sh).", "",
+             f"--warmup {bench['warmup']} --profile-run` (tools/gpu_pass.sh prof).", "",
              f"bench under the profiler: {bench['ms_per_step']} ms/step, {bench['value']} frames/s.", "",
              f"Total kernel time {total_ns / 1e6:.1f} ms over ~{steps_total} executed steps.", "",
              "| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
