@@ -171,6 +171,12 @@ for s in $STEPS; do
                 run "libenc $lib" 60 150 env TT2_LIB=$lib python -u tools/blas_cmp.py enc >> "$OUT/libenc.txt" 2>&1
               done
             done ;;
+    libab) for i in 1 2; do   # v7 / grouped-v7 shapes (tools/lib_ab.py) against an A/B library, outputs compared
+             run "libab old" 60 150 env TT2_LIB=abl/${LIBAB_OLD:-prio0}.so python -u tools/lib_ab.py run /tmp/libab_old.pt \
+               >> "$OUT/libab_old.txt" 2>&1
+             run "libab new" 60 150 python -u tools/lib_ab.py run /tmp/libab_new.pt >> "$OUT/libab_new.txt" 2>&1
+           done
+           python tools/lib_ab.py compare /tmp/libab_old.pt /tmp/libab_new.pt > "$OUT/libab_cmp.txt" 2>&1 ;;
     otls) run otls 90 200 python -u tools/overlap_timeline.py --standin > "$OUT/otl_standin.txt" 2>&1 ;;
     det) run det 60 200 python -u tools/det_check.py > "$OUT/det.txt" 2>&1 ;;
     newt) run newt 120 600 python -u -m pytest ${NEWT:-tests/test_gpu_capture.py tests/test_gpu_dp_order.py} -x -v \

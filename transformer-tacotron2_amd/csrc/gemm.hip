@@ -1013,6 +1013,9 @@ TT2_DEV void g7_frag(Frag8<bf16>& f, const char* img, int r0, int kk, int lane) 
 #ifndef TT2_G10_AUTO
 #define TT2_G10_AUTO 1
 #endif
+#ifndef G7_PRIO   // MFMA waves 4-7 (the younger of each SIMD's two) at s_setprio 1 for the K loop:
+#define G7_PRIO 0   // bit-identical, within +-2 % per GEMM, the step the same (profiles/r06_g7_prio_ab.txt)
+#endif
 #ifndef G7_REG   // the loader waves stage plain operand steps through VGPRs (1) or by LDS-DMA (0):
 #define G7_REG 0   // bit-identical, 3-17 % slower per GEMM, step 6.58 -> 6.88 ms
 #endif
@@ -1535,6 +1538,12 @@ TT2_DEV void g7_item(const G7Prob& P, int tile, int split, char* smem, unsigned 
   const bool pre_drop = fast >= 4 && fast <= 7;   // its dropout keep bits are hashed in the K loop
   const int gps = (8 + nkt - 1) / nkt;            // keep-bit groups per K step
   uint64_t dbits = 0;
+#if G7_PRIO
+  // waves w and w + 4 share a SIMD and run the same K loop in lockstep: the younger half at
+  // static priority 1 wins the VALU / issue arbitration it otherwise always loses
+  // (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   __builtin_amdgcn_s_barrier();
   int stage = 0;
   for (int t = 0; t < nkt; ++t) {
@@ -2168,6 +2177,9 @@ __global__ __launch_bounds__(G10_NT, 1) void gemm10_kernel(OpDesc A, OpDesc B, E
     const uint32_t seed = DROP ? *E.drop.seed : 0u;
     const int gps = (16 + nkt - 1) / nkt;   // keep-bit groups (16-row block i, column pair pr) per K step
     uint64_t dbits[2] = {0, 0};
+#if G7_PRIO
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);   // as v7: the younger wave of each SIMD's pair
+#endif
     __builtin_amdgcn_s_barrier();
     for (int t = 0; t < nkt; ++t) {
       G7_STAMP(t, 0)
