@@ -2,7 +2,8 @@
 variant, each timed as 10 launches replayed from a hipGraph (no host gaps), interleaved rounds,
 and the forced variant's output checked against the auto plan's.
 
-    python tools/gemm_ab.py [variant=16]  (also the graph_of / time_graph helpers of the other A/B tools)
+    python tools/gemm_ab.py [variant=16] [enc]  (enc: the encoder's 2048-row shapes; also the graph_of /
+    time_graph helpers of the other A/B tools)
 """
 import os
 import sys
@@ -53,10 +54,22 @@ def time_graph(g, n=10, reps=5):
     return e[0].elapsed_time(e[1]) * 1e-3 / (reps * n)
 
 
-def main(variant=16):
+ENC_SHAPES = [  # the encoder's 2048-row products (`enc`)
+    ("enc qkv fwd bias", 2048, 1536, 512, False, "b", None),
+    ("enc ffn1 fwd b+relu+drop", 2048, 2048, 512, False, "brd", None),
+    ("enc ffn2 fwd bias", 2048, 512, 2048, False, "b", None),
+    ("enc o fwd bias", 2048, 512, 512, False, "b", None),
+    ("enc ffn2 dgrad gate", 2048, 2048, 512, True, "gate", None),
+    ("enc ffn1 dgrad res", 2048, 512, 2048, True, "res", None),
+    ("enc qkv dgrad", 2048, 512, 1536, True, "", None),
+    ("enc conv fwd bias", 2048, 512, 2560, False, "b", (128, 512, 2)),
+]
+
+
+def main(variant=16, enc=False):
     torch.manual_seed(0)
     seed = torch.tensor([99], dtype=torch.int32, device="cuda")
-    for name, m, n, k, tb, epi, conv in SHAPES:
+    for name, m, n, k, tb, epi, conv in (ENC_SHAPES if enc else SHAPES):
         lda = k if conv is None else conv[1]
         A = torch.randn(m, lda, device="cuda").bfloat16()
         B = (torch.randn(k, n, device="cuda") if tb else torch.randn(n, k, device="cuda")).bfloat16() / k ** 0.5
@@ -94,4 +107,4 @@ def main(variant=16):
 
 
 if __name__ == "__main__":
-    main(*[int(a) for a in sys.argv[1:]])
+    main(*[int(a) for a in sys.argv[1:] if a != "enc"], enc="enc" in sys.argv[1:])

@@ -177,6 +177,10 @@ for s in $STEPS; do
              run "libab new" 60 150 python -u tools/lib_ab.py run /tmp/libab_new.pt >> "$OUT/libab_new.txt" 2>&1
            done
            python tools/lib_ab.py compare /tmp/libab_old.pt /tmp/libab_new.pt > "$OUT/libab_cmp.txt" 2>&1 ;;
+    encab) for lib in ${ENCAB_LIBS:-abl/g8lw8.so}; do   # forced v8 (15) vs auto on the encoder shapes, per library
+             echo "== $lib" >> "$OUT/encab.txt"
+             run "encab $lib" 60 150 env TT2_LIB=$lib python -u tools/gemm_ab.py 15 enc >> "$OUT/encab.txt" 2>&1
+           done ;;
     otls) run otls 90 200 python -u tools/overlap_timeline.py --standin > "$OUT/otl_standin.txt" 2>&1 ;;
     det) run det 60 200 python -u tools/det_check.py > "$OUT/det.txt" 2>&1 ;;
     newt) run newt 120 600 python -u -m pytest ${NEWT:-tests/test_gpu_capture.py tests/test_gpu_dp_order.py} -x -v \

@@ -1838,7 +1838,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef G8_RING   // ring stages (a power of two); the loaders run G8_RING - 1 steps ahead
 #define G8_RING 4
 #endif
-constexpr int G8_NT = 512, G8_STAGES = G8_RING;   // 4 MFMA waves + 4 loader waves
+#ifndef G8_LOADERS   // loader waves: 4 (2 copies per operand per wave and step) or 8 (1).  8: the
+#define G8_LOADERS 8  // LDS-DMA issue rate, not the bytes in flight, bounded the K step
+#endif
+constexpr int G8_LW = G8_LOADERS, G8_PC = 8 / G8_LW;   // copies per operand tile per loader wave
+constexpr int G8_NT = 64 * (4 + G8_LW), G8_STAGES = G8_RING;   // 4 MFMA waves + the loader waves
+constexpr int G8_EPI = 512;   // threads of the C image store / fused statistics (64 rows x 8 chunks)
 constexpr int G8_TILE = 64 * 128;          // bytes per operand tile: 64 rows x 64 bf16
 constexpr int G8_STAGE = 2 * G8_TILE;
 
@@ -1847,13 +1852,13 @@ TT2_DEV int g8_swz(int r) {
   return ((x & 1) << 2) | (x >> 1);
 }
 
-// this wave's 2 of the 8 LDS-DMA copies of one operand tile (8 rows x 128 B each);
+// this wave's G8_PC of the 8 LDS-DMA copies of one operand tile (8 rows x 128 B each);
 // KC: tile rows are m / n and chunks run along k; MC: tile rows are k, chunks along n
 template <bool KC>
 TT2_DEV void g8_issue(const OpDesc& d, char* img, int r0, int k0, int lane, int wave) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int inst = wave * 2 + i;
+  for (int i = 0; i < G8_PC; ++i) {
+    const int inst = wave * G8_PC + i;
     const int row = inst * 8 + (lane >> 3);
     const int c = (lane & 7) ^ g8_swz(row);
     const void* src = KC ? chunk_src(d, r0 + row, k0 + c * 8) : chunk_src(d, k0 + row, r0 + c * 8);
@@ -1863,11 +1868,11 @@ TT2_DEV void g8_issue(const OpDesc& d, char* img, int r0, int k0, int lane, int 
 
 // K-contiguous conv operand with C % 64 == 0 and K % 64 == 0 (as g7_conv_fast): each copy's
 // row offset and valid-tap mask are set once per tile; a step reads tap k0 / C.
-struct G8Conv { int64_t off[2]; uint32_t vm[2]; };
+struct G8Conv { int64_t off[G8_PC]; uint32_t vm[G8_PC]; };
 TT2_DEV void g8_conv_init(const OpDesc& d, G8Conv& c, int r0, int lane, int wave) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (wave * 2 + i) * 8 + (lane >> 3), outer = r0 + row;
+  for (int i = 0; i < G8_PC; ++i) {
+    const int row = (wave * G8_PC + i) * 8 + (lane >> 3), outer = r0 + row;
     const int t = outer % d.conv_t;
     const int lo = max(0, d.conv_pad - t), hi = min(31, d.conv_t - 1 - t + d.conv_pad);
     c.off[i] = (int64_t)outer * d.ld + ((lane & 7) ^ g8_swz(row)) * 8 - (int64_t)d.conv_pad * d.conv_c;
@@ -1878,9 +1883,9 @@ TT2_DEV void g8_issue_conv(const OpDesc& d, const G8Conv& c, char* img, int k0, 
   const int tap = k0 / d.conv_c;
   const bf16* p = reinterpret_cast<const bf16*>(d.p) + k0;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < G8_PC; ++i) {
     const void* src = (c.vm[i] >> tap) & 1u ? (const void*)(p + c.off[i]) : (const void*)g_zero_page;
-    __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(img + (wave * 2 + i) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(img + (wave * G8_PC + i) * 1024), 16, 0, 0);
   }
 }
 
@@ -1917,8 +1922,8 @@ TT2_DEV bf16x8 g8_frag_mc(const char* img, int col0, int s, int lane) {
 template <int SM>
 TT2_DEV void g8_stats(const EpiParams& E, char* smem, int m0, int n0, int M, int N) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int rr = tid >> 3, c = tid & 7, m = m0 + rr, n = n0 + 8 * c;
-  const bool ok = m < M && n < N;
+  const int rr = (tid >> 3) & 63, c = tid & 7, m = m0 + rr, n = n0 + 8 * c;
+  const bool ok = tid < G8_EPI && m < M && n < N;   // (8 loader waves: threads past 512 add nothing)
   float v[8], s1[8], s2[8];
   bf16x8_unpack(*reinterpret_cast<const u32x4*>(smem + rr * 128 + ((c ^ g8_swz(rr)) << 4)), v);
   if constexpr (SM == 1) {
@@ -1958,7 +1963,7 @@ TT2_DEV void g8_stats(const EpiParams& E, char* smem, int m0, int n0, int M, int
     s2[j] += __shfl_xor(s2[j], 32);
   }
   float* red = reinterpret_cast<float*>(smem + 2 * G8_STAGE);   // [8 waves][64 cols][2], past the image
-  if (lane < 8) {
+  if (lane < 8 && w < G8_EPI / 64) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       red[(w * 64 + 8 * c + j) * 2 + 0] = s1[j];
@@ -1968,7 +1973,7 @@ TT2_DEV void g8_stats(const EpiParams& E, char* smem, int m0, int n0, int M, int
   __syncthreads();
   if (tid < 64 && n0 + tid < N) {
     float S1 = 0.f, S2 = 0.f;
-    for (int q = 0; q < G8_NT / 64; ++q) {
+    for (int q = 0; q < G8_EPI / 64; ++q) {
       S1 += red[(q * 64 + tid) * 2 + 0];
       S2 += red[(q * 64 + tid) * 2 + 1];
     }
@@ -2011,13 +2016,17 @@ __global__ __launch_bounds__(G8_NT, G8_STAGES <= 4 ? 2 : 1) void gemm8_kernel(Op
     // G8_STAGES - 1 steps ahead; each step is 4 copies per loader wave
     constexpr int AH = G8_STAGES - 1;
     auto wait_ahead = [](int ahead) {   // step t+1 landed, `ahead` later steps may stay in flight
-      switch (ahead) {
-        case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-        case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      switch (ahead * 2 * G8_PC) {        // copies per step and wave: 2 G8_PC
+        case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+        case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+        case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+        case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     };
@@ -2072,10 +2081,10 @@ __global__ __launch_bounds__(G8_NT, G8_STAGES <= 4 ? 2 : 1) void gemm8_kernel(Op
       *reinterpret_cast<bf16x8*>(smem + r * 128 + (((cl >> 3) ^ g8_swz(r)) << 4)) = x;
     }
   }
-  __syncthreads();   // the C image is complete: all 8 waves store whole 128-B rows
+  __syncthreads();   // the C image is complete: 512 threads store whole 128-B rows
   bf16* C = reinterpret_cast<bf16*>(E.c);
   const int id = tid, rr = id >> 3, c = id & 7, mm = m0 + rr, nn = n0 + 8 * c;
-  if (mm < M && nn < N)   // nontemporal, as v7's C (g7_store_c)
+  if (tid < G8_EPI && mm < M && nn < N)   // nontemporal, as v7's C (g7_store_c)
     __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(smem + rr * 128 + ((c ^ g8_swz(rr)) << 4)),
                                 reinterpret_cast<u32x4*>(C + (int64_t)mm * E.ldc + nn));
   if constexpr (SM != 0) g8_stats<SM>(E, smem, m0, n0, M, N);
