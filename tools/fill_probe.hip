@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void mix_k(const char* src, int tiles, int* si
 // the loaders alone in a 768-thread work group.  Shows how much the fragment reads slow the fill.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
-template <bool RD, bool MF, bool FRESH>
+template <bool RD, bool MF, bool FRESH, bool BUF = false>
 __global__ __launch_bounds__(768, 1) void con_k(const char* src, int tiles, int* sink) {
   __shared__ __attribute__((aligned(1024))) char lds[STAGES * STEP];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -232,15 +232,23 @@ __global__ __launch_bounds__(768, 1) void con_k(const char* src, int tiles, int*
   const int total = tiles * NSTEP;
   if (w >= 8) {   // loaders
     const int lw = w - 8;
+    // BUF: buffer_load ... lds (SGPR resource + 32-bit lane offset) instead of global_load_lds
+    // (64-bit lane address)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 0x7fffffff, 0x00020000);
     auto issue = [&](int step) {
       const int tile = step / NSTEP;
       const int blk = FRESH ? (blk0 + 64 * tile) % NBLK : blk0;
-      const char* base = src + (int64_t)blk * ROWS * LD + (step % NSTEP) * 128;
+      const int64_t boff = (int64_t)blk * ROWS * LD + (step % NSTEP) * 128;
+      const char* base = src + boff;
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
         const int inst = lw * NI + i, row = inst * 8 + (lane >> 3);
-        __builtin_amdgcn_global_load_lds((gvoid_t*)(base + (int64_t)row * LD + (lane & 7) * 16),
-                                         (lvoid_t*)(lds + (step % STAGES) * STEP + inst * 1024), 16, 0, 0);
+        if (BUF)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lvoid_t*)(lds + (step % STAGES) * STEP + inst * 1024), 16,
+                                                   (unsigned)(boff + row * LD + (lane & 7) * 16), 0, 0, 0);
+        else
+          __builtin_amdgcn_global_load_lds((gvoid_t*)(base + (int64_t)row * LD + (lane & 7) * 16),
+                                           (lvoid_t*)(lds + (step % STAGES) * STEP + inst * 1024), 16, 0, 0);
       }
     };
     issue(0);
@@ -346,6 +354,9 @@ int main() {
   run768("+reads", con_k<true, false, true>);
   run768("+reads+mfma", con_k<true, true, true>);
   run768("res +r+mfma", con_k<true, true, false>);
+  run768("buf loaders", con_k<false, false, true, true>);
+  run768("buf +r+mfma", con_k<true, true, true, true>);
+  run768("buf res+r+mf", con_k<true, true, false, true>);
   run("mix dma", mix_k<0>);
   run("mix reg", mix_k<1>);
   run("mix hyb", mix_k<2>);

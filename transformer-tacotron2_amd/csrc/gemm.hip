@@ -1013,6 +1013,9 @@ TT2_DEV void g7_frag(Frag8<bf16>& f, const char* img, int r0, int kk, int lane) 
 #ifndef TT2_G10_AUTO
 #define TT2_G10_AUTO 1
 #endif
+#ifndef G7_BUF   // plain operands' LDS-DMA copies as buffer_load ... lds (1) or global_load_lds (0)
+#define G7_BUF 1
+#endif
 #ifndef G7_PRIO   // MFMA waves 4-7 (the younger of each SIMD's two) at s_setprio 1 for the K loop:
 #define G7_PRIO 0   // bit-identical, within +-2 % per GEMM, the step the same (profiles/r06_g7_prio_ab.txt)
 #endif
@@ -1084,10 +1087,21 @@ TT2_DEV void g7_issue(const OpDesc& d, G7Lane<NI>& L, char* lds, int k0, int ke,
   const int64_t shift = conv ? (int64_t)d.conv_pad * d.conv_c : 0;
   const char* base = reinterpret_cast<const char*>(d.p) + ((KC ? (int64_t)k0 : (int64_t)k0 * d.ld) - shift) * 2;
   if (!conv && !tl) {
+#if G7_BUF && defined(__HIP_DEVICE_COMPILE__)   // (the host pass has no buffer_load_lds builtin)
+    // buffer_load ... lds: the step's byte offset in an SGPR, the lane's loop-invariant offset in
+    // one VGPR (no 64-bit lane address per copy); operands < 2 GB (the plan's v7 condition)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(d.p), (short)0, 0x7fffffff,
+                                                                        0x00020000);
+    const unsigned soff = (unsigned)((KC ? (int64_t)k0 : (int64_t)k0 * d.ld) * 2);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lvoid_t*)(lds + (lw * NI + i) * 1024), 16, L.off[i], soff, 0, 0);
+#else
 #pragma unroll
     for (int i = 0; i < NI; ++i)
       __builtin_amdgcn_global_load_lds((gvoid_t*)(base + L.off[i]), (lvoid_t*)(lds + (lw * NI + i) * 1024), 16, 0,
                                        0);
+#endif
     return;
   }
   if (KC && cfast) {   // the whole step reads tap k0 / C
