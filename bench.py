@@ -249,6 +249,8 @@ def gemm_kernel_name(plan: int, ta: int, tb: int) -> str:
         return f"gemm8_kernel<{bk}, 0>"
     if plan == 16:
         return "gemm10_kernel"
+    if plan == 17:
+        return "gemm11_kernel"
     if plan == 1:
         return "gemm_kernel"
     return f"gemm plan {plan}"

@@ -72,7 +72,9 @@ typedef struct tt2_gemm_args {
                               when eligible) with its register / LDS-image epilogue (auto: LDS image),
                               15 64x64 (K-contiguous A; auto for <= 64 v7 tiles), 16 256x256 (NT, bf16 C,
                               N % 256 == 0, K % 64 == 0, bias / ReLU / dropout epilogues only; auto when
-                              its rounds of the chip cost less than v7's) */
+                              its rounds of the chip cost less than v7's), 17 256x128 with 8 loader waves
+                              (NT, bf16 C, N % 128 == 0, K % 64 == 0, the same epilogues; auto where v7 would
+                              run) */
   /* optional fused row sums of op(A) over k: a_ksum[m] = a_ksum_beta * a_ksum[m] + sum_k A(m, k)
    * (f32).  With A = dY^T of a weight-gradient GEMM this is the bias gradient, taken from the
    * A tiles already staged in LDS.  Requires bf16, trans_a, no conv on A. */

@@ -1,7 +1,8 @@
 """tt2_gemm_plan's kernel choice (host logic, CPU: the plan reads only sizes, flags and pointer
 alignment): v10 (16) takes the NT products whose 256 x 256 tiles' rounds of the chip cost
-less than v7's (the decoder FFN1 forward, the memory K/V projection), v7 (13) the N = 512 and
-dgrad / residual / split products, v8 (15) the small ones; explicit variants win."""
+less than v7's (the decoder FFN1 forward, the memory K/V projection), v11 (17) the other NT
+forward products up to K = 1024, v7 (13) the long-K, dgrad / residual / split products, v8 (15)
+the small ones; explicit variants win."""
 import ctypes as C
 import os
 import sys
@@ -41,10 +42,18 @@ def test_v10_takes_the_wide_forward_products():
     assert plan(8192, 8192, 8192) == 16
 
 
+def test_v11_takes_the_forward_k512_products():
+    assert plan(12800, 512, 512, bias=_BIAS) == 17                  # 200 v7 tiles; v11 is v7's tile, 8 loaders
+    assert plan(12800, 1536, 512, bias=_BIAS) == 17                 # QKV: 2 v10 rounds cost more than 3 of v7's
+    assert plan(12800, 512, 1024, bias=_BIAS) == 17
+    assert plan(12800, 512, 2048) == 13                             # long K: v7 (two MFMA waves per SIMD)
+    assert plan(12800, 512, 512, trans_b=True) == 13                # activation gradients stay on v7 ...
+    assert plan(12800, 512, 512, trans_b=True, variant=17) == 17    # ... unless forced
+    assert plan(12800, 512, 512, res=_C, ldr=512) == 13             # a forward residual: v7
+
+
 def test_v7_and_v8_keep_the_rest():
-    assert plan(12800, 512, 512, bias=_BIAS) == 13                  # 200 vs 100 tiles: one round either way
     assert plan(12800, 512, 2048) == 13
-    assert plan(12800, 1536, 512, bias=_BIAS) == 13                 # QKV: 2 v10 rounds cost more than 3 of v7
     assert plan(12800, 2048, 512, trans_b=True) == 13               # dgrad (N-contiguous B)
     assert plan(12800, 2048, 512, res=_C, ldr=2048) == 13           # residual epilogue
     assert plan(12800, 2048, 512, act=ACT_TANH) == 13

@@ -1013,6 +1013,12 @@ TT2_DEV void g7_frag(Frag8<bf16>& f, const char* img, int r0, int kk, int lane) 
 #ifndef TT2_G10_AUTO
 #define TT2_G10_AUTO 1
 #endif
+#ifndef TT2_G11_AUTO   // the auto plan takes v11 where it would take v7 and v11 is eligible
+#define TT2_G11_AUTO 1
+#endif
+#ifndef G11_MAX_K       // ... up to this K (one MFMA wave per SIMD loses to v7's two at long K:
+#define G11_MAX_K 1024  // 12800 x 512 x 2048 30.3 -> 30.9 us; K = 512: -7 %)
+#endif
 #ifndef G7_BUF   // plain operands' LDS-DMA copies as buffer_load ... lds (1) or global_load_lds (0)
 #define G7_BUF 1
 #endif
@@ -2327,6 +2333,229 @@ hipError_t launch10(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M,
 
 // v10's epilogue code for this launch, or -1: bf16 C on 16-B rows, no beta / residual / gate /
 // tanh / k-sums (g7_fast_code's forward option sets)
+// =====================================================================================
+// v11: v7's 256 x 128 tile with v10's MFMA-wave layout and twice the loader waves.  The K loop
+// of v7 is bound by its 4 loader waves' LDS-DMA issue rate (12 copies per wave per step:
+// round 2's ablation, loads removed, and round 6's v8, whose K step fell 22 % with 8 loader
+// waves), and v7 cannot add loader waves: 8 MFMA waves at ~146 VGPRs leave room for 12 waves
+// per CU.  Here 4 MFMA waves (2 M x 2 N, 128 x 64 each: v10's 128 accumulators per lane, one
+// wave per SIMD) and 8 loader waves (6 copies each per 48 KB step: A 4, B 2) into v7's 3-stage
+// ring, with v7's images, swizzles and fragment reads.  The MFMA waves read 96 KB of fragments
+// per step instead of v7's 128 KB.  NT, plain bf16 operands, K % 64 == 0, N % 128 == 0, the
+// v10 epilogue codes (bias, ReLU, dropout); the C image goes where v7's does (g7_img_row).
+// =====================================================================================
+constexpr int G11_NT = 768;
+
+// CODE: bit 0 bias, bit 1 ReLU, bit 2 dropout (the forward's options, with BKC: NT); 8: a bf16
+// residual added, 16: a bf16 ReLU gate (the activation gradients, !BKC: B N-contiguous), whose
+// tile the loader waves stage into the C image during the last two K steps (v7's G7_X_AUX copies)
+template <bool BKC, int CODE>
+__global__ __launch_bounds__(G11_NT, 1) void gemm11_kernel(OpDesc A, OpDesc B, EpiParams E, int M, int N, int K,
+                                                           int ntn, int items, unsigned long long* span) {
+  constexpr bool BIAS = CODE & 1, RELU = CODE & 2, DROP = CODE & 4;
+  constexpr int PX = CODE & 8 ? 1 : CODE & 16 ? 2 : 0;   // staged epilogue operand: residual / gate
+  __shared__ __attribute__((aligned(1024))) char smem[G7_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (span && tid == 0) span[TT2_SPAN_W * blockIdx.x] = wall_clock64();
+  const int tile = xcd_item(blockIdx.x, items);
+  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 128;
+  const int nkt = K / 64;
+  if (wave >= 4) {   // ------------------------------------------------ loader waves
+    const int lw = wave - 4;
+    G7Lane<4> la;   // 4 of the A tile's 32 copies, 2 of the B tile's 16
+    G7Lane<2> lb;
+    g7_lane_init<true>(la, A, m0, 0, lane, lw);
+    g7_lane_init<BKC>(lb, B, n0, 0, lane, lw);
+    auto issue = [&](int step, int stage) {
+      char* sa = smem + stage * G7_STAGE;
+      g7_issue<true>(A, la, sa, 64 * step, K, lane, lw, false, false);
+      g7_issue<BKC>(B, lb, sa + G7_A, 64 * step, K, lane, lw, false, false);
+    };
+    // the residual / gate tile (PX), 6 + 2 copies per wave into the image's rows 0..191 (the stage
+    // of step nkt - 3) and 192..255 (step nkt - 2), each once its stage is free
+    G7Prob px_p;
+    px_p.M = M;
+    const void* xs = PX == 1 ? E.res : E.gate;
+    const int64_t ldx = PX == 1 ? E.ldr : E.ldg;
+    issue(0, 0);
+    if (nkt > 1) { issue(1, 1); asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); }
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    int st = 2;
+    for (int t = 0; t < nkt; ++t) {
+      if (t + 2 < nkt) {
+        issue(t + 2, st);
+        st = st == 2 ? 0 : st + 1;
+      } else if (PX) {
+        if (t == nkt - 2 || nkt == 1) g7_issue_x(px_p, xs, ldx, smem, nkt, m0, n0, 0, 6, lane, lw);
+        if (t == nkt - 1) g7_issue_x(px_p, xs, ldx, smem, nkt, m0, n0, 192, 2, lane, lw);
+      }
+      if (t + 2 < nkt || (PX && t == nkt - 2))
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // step t+1 landed; t+2 (or the staged rows) in flight
+      else if (!PX)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    if (PX) {   // the staged tile has landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {   // ------------------------------------------------------- MFMA waves
+    const int wm = wave >> 1, wn = wave & 1, q = lane >> 4;
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint32_t seed = DROP ? *E.drop.seed : 0u;
+    const int gps = (16 + nkt - 1) / nkt;   // keep-bit groups (16-row block i, column pair pr) per K step
+    uint64_t dbits[2] = {0, 0};
+    __builtin_amdgcn_s_barrier();
+    int stage = 0;
+    for (int t = 0; t < nkt; ++t) {
+      const char* sa = smem + stage * G7_STAGE;
+      const char* sb = sa + G7_A;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        Frag8<bf16> fb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g7_frag<BKC>(fb[j], sb, wn * 64 + 16 * j, kk, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          Frag8<bf16> fa;
+          g7_frag<true>(fa, sa, wm * 128 + 16 * i, kk, lane);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) mma16(fb[j], fa, acc[i][j]);   // D[n][m]
+        }
+      }
+      if (DROP) {   // VALU work beside this step's MFMAs
+        const int g1 = min(16, (t + 1) * gps);
+        for (int gi = t * gps; gi < g1; ++gi) {
+          const int m = m0 + wm * 128 + 16 * (gi >> 1) + (lane & 15);
+          const int n = n0 + wn * 64 + 16 * (2 * (gi & 1) + (q & 1)) + 8 * (q >> 1);
+          const uint64_t kb = drop_bits8(seed, E.drop.site, (uint32_t)((int64_t)m * E.n_log + n), E.drop.thr);
+          dbits[gi >> 3] |= kb << (8 * (gi & 7));
+        }
+      }
+      stage = stage == 2 ? 0 : stage + 1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this stage's reads retired (WAR vs the next copy)
+      __builtin_amdgcn_s_barrier();
+    }
+    if (PX) __builtin_amdgcn_s_barrier();   // the loaders' staged residual / gate tile has landed
+    // epilogue: alpha, bias, residual, ReLU, gate, dropout (v7's order) into v7's C image
+    f32x4 pbias[2][2];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int n = n0 + wn * 64 + 16 * (2 * pr + (q & 1)) + 8 * (q >> 1);
+      pbias[pr][0] = pbias[pr][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (BIAS) {
+        pbias[pr][0] = *reinterpret_cast<const f32x4*>(E.bias + n);
+        pbias[pr][1] = *reinterpret_cast<const f32x4*>(E.bias + n + 4);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = wm * 128 + 16 * i + (lane & 15);
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        float v[8];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * pr][rr]),
+                                                           __float_as_uint(acc[i][2 * pr + 1][rr]), false, false);
+          v[rr] = __uint_as_float(sw[0]);
+          v[4 + rr] = __uint_as_float(sw[1]);
+        }
+        const int cl = wn * 64 + 16 * (2 * pr + (q & 1)) + 8 * (q >> 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = BIAS ? v[j] * E.alpha + pbias[pr][0][j] : v[j] * E.alpha;
+          v[4 + j] = BIAS ? v[4 + j] * E.alpha + pbias[pr][1][j] : v[4 + j] * E.alpha;
+        }
+        char* cp = smem + g7_img_row(nkt, r) + (((cl >> 3) ^ (r & 15)) << 4);   // C overwrites the staged chunk
+        if (PX) {
+          float tx[8];
+          unpack_lds8(cp, tx);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            if (PX == 1) v[j] += tx[j];
+            else v[j] = tx[j] != 0.f ? v[j] * E.gate_scale : 0.f;
+          }
+        }
+        if (RELU) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+        }
+        if (DROP) {
+          const int gi = 2 * i + pr;
+          const uint32_t kb = (uint32_t)(dbits[gi >> 3] >> (8 * (gi & 7)));
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (kb >> j) & 1u ? v[j] * E.drop.scale : 0.f;
+        }
+        bf16x8 x;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = (bf16)v[j];
+        *reinterpret_cast<bf16x8*>(cp) = x;
+      }
+    }
+  }
+  __syncthreads();   // the C image is complete: all 12 waves store whole 256-B row segments
+  bf16* C = reinterpret_cast<bf16*>(E.c);
+  for (int id = tid; id < 256 * 16; id += G11_NT) {
+    const int r = id >> 4, c = id & 15;
+    const int mm = m0 + r, nn = n0 + 8 * c;
+    if (mm < M)   // nontemporal, as v7's C
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(smem + g7_img_row(nkt, r) + ((c ^ (r & 15)) << 4)),
+                                  reinterpret_cast<u32x4*>(C + (int64_t)mm * E.ldc + nn));
+  }
+  if (span) {   // every wave's stores completed, then one end stamp
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) span[TT2_SPAN_W * blockIdx.x + 1] = wall_clock64();
+  }
+}
+
+hipError_t launch11(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, bool bkc, int code,
+                    hipStream_t s) {
+  const int ntn = N / 128, items = ((M + 255) / 256) * ntn;
+  ProbeScope ps(s, items);
+#define TT2_G11(BK_, C_)                                                                                          \
+  case C_:                                                                                                        \
+    if (ps.ext())                                                                                                 \
+      hipExtLaunchKernelGGL((gemm11_kernel<BK_, C_>), dim3(items), dim3(G11_NT), 0, s, ps.e0, ps.e1, 0, A, B, E, M, \
+                            N, K, ntn, items, ps.span);                                                           \
+    else                                                                                                          \
+      hipLaunchKernelGGL((gemm11_kernel<BK_, C_>), dim3(items), dim3(G11_NT), 0, s, A, B, E, M, N, K, ntn, items,  \
+                         ps.span);                                                                                \
+    break;
+  if (bkc) {
+    switch (code) {
+      TT2_G11(true, 0) TT2_G11(true, 1) TT2_G11(true, 2) TT2_G11(true, 3) TT2_G11(true, 4) TT2_G11(true, 5)
+      TT2_G11(true, 6) TT2_G11(true, 7)
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (code) {
+      TT2_G11(false, 0) TT2_G11(false, 8) TT2_G11(false, 16)
+      default: return hipErrorInvalidValue;
+    }
+  }
+#undef TT2_G11
+  return hipGetLastError();
+}
+
+// v11's epilogue code for a request (-1: an option set v11 does not fuse): NT forward requests
+// take bias / ReLU / dropout; activation-gradient (trans_b) requests a bf16 residual or gate alone
+int g11_code(const EpiParams& E, bool bkc) {
+  if (E.c_dt != TT2_BF16 || !E.vec || E.beta != 0.f || E.act == ACT_TANH || E.ksum || (E.res && E.gate)) return -1;
+  const int fwd = (E.bias ? 1 : 0) | (E.act == ACT_RELU ? 2 : 0) | (E.drop.thr ? 4 : 0);
+  if (bkc) return (E.res || E.gate) ? -1 : fwd;
+  if (fwd) return -1;
+  if (E.res) return E.res_dt == TT2_BF16 ? 8 : -1;
+  if (E.gate) return E.gate_dt == TT2_BF16 ? 16 : -1;
+  return 0;
+}
+
 int g10_code(const EpiParams& E) {
   if (E.c_dt != TT2_BF16 || !E.vec || E.beta != 0.f || E.act == ACT_TANH || E.res || E.gate || E.ksum) return -1;
   return (E.bias ? 1 : 0) | (E.act == ACT_RELU ? 2 : 0) | (E.drop.thr ? 4 : 0);
@@ -2428,6 +2657,18 @@ static int gemm_plan(const tt2_gemm_args* a) {
   const int64_t cus = tt2_cu_count();
   const int64_t rounds7 = (tiles7 + cus - 1) / cus, rounds10 = ((a->m + 255) / 256 * (a->n / 256) + cus - 1) / cus;
   if (v10ok && (var == 16 || (var == 0 && TT2_G10_AUTO && 17 * rounds10 < 10 * rounds7))) return 16;
+  // v11 (v7's tile, 4 MFMA + 8 loader waves; NT, bf16 C, K % 64 == 0, N % 128 == 0, bias / ReLU /
+  // dropout epilogues only, checked at launch): forced by variant 17; auto where v7 would run
+  const bool v11ok = v7ok && !a->trans_a && a->a_conv_t == 0 && a->b_conv_t == 0 && !a->a_ksum &&
+                     a->dtype_out == TT2_BF16 && a->splits <= 1 && a->n % 128 == 0 && a->k % 64 == 0 &&
+                     a->beta == 0.f && a->act != ACT_TANH && !a->col_stats && !a->bn_bwd &&
+                     (a->trans_b ? !a->bias && !a->act && !a->drop_thr && !(a->res && a->gate)
+                                 : !a->res && !a->gate) &&
+                     reinterpret_cast<uintptr_t>(a->c) % 16 == 0 && a->ldc % 8 == 0 &&
+                     reinterpret_cast<uintptr_t>(a->bias) % 16 == 0;
+  // (auto: the forward's NT products only; on the activation gradients, with the residual / gate
+  // tile staged, v11 measured 3-5 % slower than v7 and the step 1 % slower: profiles/r06_v11_ab.txt)
+  if (v11ok && (var == 17 || (var == 0 && TT2_G11_AUTO && a->k <= G11_MAX_K && !a->trans_b))) return 17;
   if ((var == 13 || var == 14 || var == 0) && v7ok) return 13;
   return 2;
 }
@@ -2602,6 +2843,14 @@ extern "C" int tt2_gemm(const tt2_gemm_args* a, hipStream_t stream) {
     const int code = g10_code(ep);
     if (code >= 0) return tt2_check_launch(launch10(A, B, ep, a->m, a->n, a->k, code, stream), "tt2_gemm(v10)");
     tt2_gemm_args b = *a;   // an epilogue v10 does not fuse (unaligned rows, ...): v7
+    b.kernel_variant = 13;
+    plan = gemm_plan(&b);
+  }
+  if (plan == 17) {
+    const int code = g11_code(ep, !a->trans_b);
+    if (code >= 0)
+      return tt2_check_launch(launch11(A, B, ep, a->m, a->n, a->k, !a->trans_b, code, stream), "tt2_gemm(v11)");
+    tt2_gemm_args b = *a;   // an epilogue v11 does not fuse: v7
     b.kernel_variant = 13;
     plan = gemm_plan(&b);
   }
