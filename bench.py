@@ -218,7 +218,7 @@ def decode_bench(model, reps: int = 3):
                                  f"{DECODE_LAUNCHES} dependent kernels per step)"}}
 
 
-DECODE_LAUNCHES = 46   # kernels per decode step (csrc/decoder.cpp tt2_decode_step; profiles/r04_decode_traffic.json counts them)
+DECODE_LAUNCHES = 46   # kernels per decode step (csrc/decoder.cpp step_launches: 7 per layer + 4)
 
 
 def decode_traffic(kind: str):

@@ -271,6 +271,36 @@ int tt2_kv_append(const void* src, int64_t src_ld, void* cache, int64_t c_bstrid
 int tt2_decode_emit(const float* heads, int64_t heads_ld, int batch, int n_mels, int t_max, float* mel_seq,
                     float* stop_seq, void* prev, int prev_dtype, int32_t* t_ptr, uint32_t* seed,
                     const float* stop_bias, int32_t* stop_len, float stop_thr, hipStream_t stream);
+/* The decode step's whole FFN sublayer in ONE launch (the decoder layer's
+ * FFN + third post-LN, modeling_speecht5.py's SpeechT5FeedForward + final_layer_norm):
+ *   hidden = relu(x W1^T + b1)            (m x d_ffn, stored in `hidden`, dtype)
+ *   slab[s] = hidden[:, 256 s ..] W2[:, 256 s ..]^T   (s < 8, raw f32 partial sums)
+ *   y = LN(x + b2 + sum_s slab[s]) * gamma + beta
+ * with the arithmetic of the three launches it replaces (tt2_gemm act = relu, tt2_gemm splits = 8
+ * main_only, tt2_ln_combine splits = 8): bit-identical results, but slower than those three
+ * launches on MI355X (its two in-kernel hand-offs between work groups cost more than two launch
+ * boundaries), so the decode step uses it only under schedule 4.  256 work groups that order the
+ * three phases among themselves through the counters at `sync` (TT2_FFN_SYNC_INTS int32, zero
+ * before the first call; every call leaves them zero again; sync[TT2_FFN_SYNC_ERR] != 0 afterwards
+ * means a phase timed out and the outputs are invalid).  m <= 64, d_model 512, d_ffn 2048, dtype TT2_DT_BF16 or TT2_DT_F16,
+ * 16-B aligned rows; anything else is TT2_E_INVALID.  Replayable from a captured graph. */
+typedef struct tt2_ffn_decode_args {
+  const void* x;                      /* [m][512] FFN input and residual */
+  const void* w1; const float* b1;    /* [2048][512], [2048] */
+  const void* w2; const float* b2;    /* [512][2048], [512] */
+  const float* gamma; const float* beta;
+  void* hidden;                       /* [m][2048] scratch */
+  float* slab;                        /* [8][m][512] scratch */
+  int32_t* sync;                      /* [TT2_FFN_SYNC_INTS] */
+  void* y;                            /* [m][512] */
+  int32_t m, d_model, d_ffn, dtype;
+  float eps;
+} tt2_ffn_decode_args;
+#define TT2_FFN_SYNC_INTS 2048
+#define TT2_FFN_SYNC_ERR 1088
+int tt2_ffn_decode(const tt2_ffn_decode_args* a, hipStream_t stream);
+/* measurement hook: also 8 device wall-clock stamps per work group into stamps[256][8] */
+int tt2_ffn_decode_stamps(const tt2_ffn_decode_args* a, uint64_t* stamps, hipStream_t stream);
 
 /* ------------------------------------------------------------ decode step / graph
  * The whole autoregressive decode step (the loop body of
@@ -307,7 +337,9 @@ typedef struct tt2_decode_desc {
   int32_t batch, text_len, t_max, n_layers, d_model, n_heads, d_ffn, n_mels, prenet_dim;
   int32_t dtype;        /* step storage type: TT2_DT_BF16, TT2_DT_F16 (batch <= 64) or TT2_DT_F32 */
   int32_t schedule;     /* 0 auto, 1 plain (one launch per op), 2 split-K (16-bit, batch <= 64; output
-                         * projections fused into the attention launches), 3 split-K without that fusion */
+                         * projections fused into the attention launches), 3 split-K without that
+                         * fusion, 4 split-K with it and each FFN sublayer as one tt2_ffn_decode
+                         * launch (bit-identical to 2, measured slower: opt-in) */
   float ln_eps;
   float prenet_dropout; /* 0 = off (Tacotron2 keeps it on at inference) */
   float stop_logit;     /* logit(stop_threshold); +inf never stops */

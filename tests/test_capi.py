@@ -53,7 +53,7 @@ def test_struct_sizes_match_c_layout(lib):
                "tt2_bn_args": lib.BnArgs, "tt2_pe_args": lib.PeArgs, "tt2_loss_args": lib.LossArgs,
                "tt2_adam_args": lib.AdamArgs, "tt2_reduce_args": lib.ReduceArgs,
                "tt2_attn_decode_args": lib.AttnDecodeArgs, "tt2_decode_desc": lib.DecodeDesc, "tt2_desc": lib.Desc,
-               "tt2_wflip_job": lib.WflipJob}
+               "tt2_wflip_job": lib.WflipJob, "tt2_ffn_decode_args": lib.FfnDecodeArgs}
     prog = "#include <stdio.h>\n#include <stddef.h>\n#include \"tt2_capi.h\"\nint main(){\n"
     for name, cls in structs.items():
         last = cls._fields_[-1][0]

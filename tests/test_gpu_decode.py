@@ -7,7 +7,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 from tt2.config import TTSConfig  # noqa: E402
-from tt2.infer import SCHEDULE_PLAIN, SCHEDULE_SPLIT, Decoder  # noqa: E402
+from tt2.infer import SCHEDULE_AUTO, SCHEDULE_PLAIN, SCHEDULE_SPLIT, SCHEDULE_SPLIT_FFN1, Decoder  # noqa: E402
 from tt2.model import TransformerTTS  # noqa: E402
 from tt2 import ops  # noqa: E402
 from tt2_oracle import OracleConfig, TransformerTTSOracle, init_deterministic  # noqa: E402
@@ -66,6 +66,27 @@ def test_decode_schedules_match():
     b, _ = out.run(text.cuda(), tl.cuda(), T, stop_threshold=None)
     assert rel(b, a) < 2e-2
     assert out.t.item() == T and ref.t.item() == T
+
+
+@pytest.mark.parametrize("cd", [torch.bfloat16, torch.float16])
+def test_one_launch_ffn_schedule_bitwise(cd):
+    """The split schedule with each layer's FFN sublayer in one tt2_ffn_decode launch
+    (SCHEDULE_SPLIT_FFN1) decodes the same frames, stop logits, stop positions and device
+    counters bit for bit as the default (the FFN as three launches), with prenet dropout and a
+    stop threshold, through the captured graph; bf16 and the fp16 step."""
+    _, model, text, tl = setup(torch.bfloat16)
+    T = 19
+    outs = []
+    for sched in (SCHEDULE_AUTO, SCHEDULE_SPLIT_FFN1):
+        dec = Decoder(model.engine, 3, 17, T, seed=7, dtype=cd, schedule=sched)
+        after, out_len = dec.run(text.cuda(), tl.cuda(), T, stop_threshold=0.5)
+        torch.cuda.synchronize()
+        outs.append((after.clone(), out_len.clone(), dec.mel_seq.clone(), dec.stop_seq.clone(), dec.t.item(),
+                     dec.seed.item()))
+    (a0, l0, m0, s0, t0, e0), (a1, l1, m1, s1, t1, e1) = outs
+    assert torch.equal(m0, m1) and torch.equal(s0, s1)
+    assert torch.equal(a0, a1) and torch.equal(l0, l1)
+    assert (t0, e0) == (t1, e1)
 
 
 def test_stop_token_early_exit():

@@ -288,3 +288,64 @@ def test_fp16_kv_scatter_attention_ln_combine():
     ops.ln_combine(x, slab, 4, bias, gam, bet, y, B)
     s = x.double() + bias.double() + slab.view(4, B, d).double().sum(0)
     assert rel(y, F.layer_norm(s, (d,), gam.double(), bet.double(), 1e-5)) < 2e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("m", [1, 17, 32, 40, 64])
+def test_ffn_decode_one_launch_equals_three(dtype, m):
+    """tt2_ffn_decode (the FFN sublayer in one launch of 256 work groups ordered by device
+    counters) writes bit for bit what the three launches it replaces write: the skinny FFN1
+    with relu (hidden), the skinny FFN2 split-K slabs (8, raw f32) and tt2_ln_combine (y).
+    Three calls in a row on NEW inputs into the same hidden / slab buffers (a reader that hit a
+    stale cache line of the previous call would differ); the counters are re-armed after every
+    call, no phase timed out, and y is LN(x + b2 + relu(x W1^T + b1) W2^T) against float64."""
+    g = torch.Generator().manual_seed(100 + m)
+    d, f = 512, 2048
+    mk = (lambda sh, sc=1.0: _bf(sh, g, sc)) if dtype == torch.bfloat16 else (lambda sh, sc=1.0: _h(sh, g, sc))
+    w1, w2 = mk((f, d), 1 / math.sqrt(d)), mk((d, f), 1 / math.sqrt(f))
+    b1, b2, gam, bet = (torch.randn(n, generator=g).cuda() * 0.1 for n in (f, d, d, d))
+    sync = torch.zeros(2048, dtype=torch.int32, device="cuda")
+    hid = torch.full((m, f), float("nan"), device="cuda").to(dtype)
+    slab = torch.full((8 * m * d,), float("nan"), device="cuda")
+    for _ in range(3):
+        x = mk((m, d))
+        # reference: the three launches of the split schedule
+        h_ref = torch.empty(m, f, dtype=dtype, device="cuda")
+        ops.gemm(x, w1, h_ref, m, f, d, d, d, f, bias=b1, act=1, variant=3)
+        slab_ref = torch.full((8 * m * d,), float("nan"), device="cuda")
+
+        class WS:
+            def get(self, nbytes):
+                assert nbytes <= slab_ref.numel() * 4
+                return slab_ref
+
+        dummy = torch.empty(m, d, dtype=dtype, device="cuda")
+        ops.gemm(h_ref, w2, dummy, m, d, f, f, f, d, splits=8, main_only=True, ws=WS(), variant=3)
+        y_ref = torch.empty(m, d, dtype=dtype, device="cuda")
+        ops.ln_combine(x, slab_ref, 8, b2, gam, bet, y_ref, m)
+        y = torch.full((m, d), float("nan"), device="cuda").to(dtype)
+        ops.ffn_decode(x, w1, b1, w2, b2, gam, bet, hid, slab, sync, y, m)
+        torch.cuda.synchronize()
+        assert int(sync.abs().sum()) == 0, sync.tolist()
+        assert torch.equal(hid.view(torch.int16), h_ref.view(torch.int16))
+        assert torch.equal(slab, slab_ref)
+        assert torch.equal(y.view(torch.int16), y_ref.view(torch.int16))
+    hd = torch.relu(x.double() @ w1.double().t() + b1.double())
+    ref = F.layer_norm(x.double() + b2.double() + hd @ w2.double().t(), (d,), gam.double(), bet.double(), 1e-5)
+    assert rel(y, ref) < 2e-2
+
+
+def test_ffn_decode_rejects_unsupported_shapes():
+    """m > 64, d_ffn != 2048 or f32: TT2_E_INVALID before any launch (the decoder then keeps the
+    three-launch FFN)."""
+    g = torch.Generator().manual_seed(5)
+    d = 512
+    for m, f, dtype in ((65, 2048, torch.bfloat16), (8, 1024, torch.bfloat16), (8, 2048, torch.float32)):
+        x = torch.randn(m, d, generator=g).cuda().to(dtype)
+        w1, w2 = torch.zeros(f, d, device="cuda", dtype=dtype), torch.zeros(d, f, device="cuda", dtype=dtype)
+        v = torch.zeros(f, device="cuda")
+        hid = torch.zeros(m, f, device="cuda", dtype=dtype)
+        slab = torch.zeros(8 * m * d, device="cuda")
+        sync = torch.zeros(2048, dtype=torch.int32, device="cuda")
+        with pytest.raises(RuntimeError, match="tt2_ffn_decode"):
+            ops.ffn_decode(x, w1, v, w2, v[:d], v[:d], v[:d], hid, slab, sync, x.clone(), m)

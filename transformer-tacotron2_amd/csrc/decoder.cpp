@@ -11,6 +11,10 @@
 //    into raw f32 slabs; tt2_ln_combine folds each sublayer's slabs with bias + residual
 //    into its LayerNorm, except the first post-LN of a layer, which rides in the cross-attention
 //    launch's prologue (it feeds that launch's query projection).  7 launches per layer + 4.
+//    Schedule 4: the same with each FFN sublayer (FFN1, FFN2 slabs, post-LN) as ONE launch
+//    (tt2_ffn_decode, 5 per layer): bit-identical, but measured slower -- its two in-kernel
+//    hand-offs between work groups cost more than the two launch boundaries they replace
+//    (DESIGN.md section 0.5 item 4).  Schedule 3: split-K without the attention fusions.
 //  * plain (f32 parity mode, or batch > 64): one launch per op (GEMM, KV append,
 //    LayerNorm, PE, emit), no slabs.
 // The step reads the frame index from the device counter d->step and bumps it in the
@@ -42,6 +46,7 @@ struct Bufs {
   float* slab;
   size_t slab_bytes;
   int32_t* emit_done;
+  int32_t* ffn_sync;   // tt2_ffn_decode's counters (zeroed by tt2_decode_reset, re-armed by each launch)
   char* cache;
   size_t cache_layer;   // bytes per layer of the KV cache
   size_t total;
@@ -70,6 +75,7 @@ Bufs carve(const tt2_decode_desc* d, char* base) {
   b.slab_bytes = (size_t)16 * (B > 32 ? B : 32) * D * sizeof(float);
   b.slab = reinterpret_cast<float*>(take(b.slab_bytes));
   b.emit_done = reinterpret_cast<int32_t*>(take(sizeof(int32_t)));
+  b.ffn_sync = reinterpret_cast<int32_t*>(take(TT2_FFN_SYNC_INTS * sizeof(int32_t)));
   b.cache_layer = B * (size_t)d->t_max * 2 * D * e;
   b.cache = take(b.cache_layer * d->n_layers);
   b.total = off;
@@ -79,7 +85,7 @@ Bufs carve(const tt2_decode_desc* d, char* base) {
 bool split_schedule(const tt2_decode_desc* d) {
   const bool half = d->dtype == TT2_DT_BF16 || d->dtype == TT2_DT_F16;
   if (d->schedule == 1) return false;
-  if (d->schedule == 2 || d->schedule == 3) return true;
+  if (d->schedule >= 2 && d->schedule <= 4) return true;
   return half && d->batch <= 64;
 }
 
@@ -137,6 +143,8 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
   const size_t e = esz_of(dt);
   const bool split = split_schedule(d);
   const bool fuse_o = split && d->schedule != 3;   // output projections inside the attention launches
+  // schedule 4: the FFN sublayer in one launch (tt2_ffn_decode's shapes; batch <= 64 already)
+  const bool fuse_ffn = fuse_o && d->schedule == 4 && D == 512 && F == 2048;
   const float scale = 1.f / std::sqrt((float)(D / H));
   const int64_t kvld = (int64_t)d->n_layers * 2 * D;
 
@@ -265,6 +273,16 @@ int step_launches(const tt2_decode_desc* d, hipStream_t s) {
       TT2_TRY(layernorm(b.h1, b.co, L.ln2_g, L.ln2_b, b.h2));
     }
     // FFN
+    if (fuse_ffn) {
+      tt2_ffn_decode_args fa;
+      std::memset(&fa, 0, sizeof(fa));
+      fa.x = b.h2; fa.w1 = L.ffn1_w; fa.b1 = L.ffn1_b; fa.w2 = L.ffn2_w; fa.b2 = L.ffn2_b;
+      fa.gamma = L.ln3_g; fa.beta = L.ln3_b; fa.hidden = b.f1; fa.slab = b.slab; fa.sync = b.ffn_sync; fa.y = xn;
+      fa.m = B; fa.d_model = D; fa.d_ffn = F; fa.dtype = dt; fa.eps = d->ln_eps;
+      TT2_TRY(tt2_ffn_decode(&fa, s));
+      x = xn;
+      continue;
+    }
     {
       tt2_gemm_args g = lin(b.h2, L.ffn1_w, b.f1, B, F, D, L.ffn1_b, dt, dt);
       g.act = 1;
@@ -349,6 +367,7 @@ extern "C" int tt2_decode_reset(const tt2_decode_desc* d, uint32_t seed0, hipStr
   if (e == hipSuccess) e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d->stop_len), INT_MAX, d->batch, s);
   if (e == hipSuccess) e = hipMemsetAsync(b.prev, 0, (size_t)d->batch * d->n_mels * esz_of(d->dtype), s);
   if (e == hipSuccess) e = hipMemsetAsync(b.emit_done, 0, sizeof(int32_t), s);
+  if (e == hipSuccess) e = hipMemsetAsync(b.ffn_sync, 0, TT2_FFN_SYNC_INTS * sizeof(int32_t), s);
   return tt2_check_launch(e, "tt2_decode_reset");
 }
 

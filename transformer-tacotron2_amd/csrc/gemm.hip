@@ -945,6 +945,268 @@ __global__ __launch_bounds__(NT) void gemm_skinny_kernel(const TE* X, int64_t ld
   }
 }
 
+// =====================================================================================
+// The decode step's FFN sublayer in one launch (tt2_ffn_decode): y = LN3(x + b2 + relu(x W1^T
+// + b1) W2^T) for m <= 64 rows, d = 512, F = 2048, with the arithmetic of the three launches
+// it replaces (skinny FFN1 with relu, skinny FFN2 split-K into 8 f32 slabs, tt2_ln_combine):
+// bit-identical.  One grid of 256 work groups; work group w takes split s = w / 32 (hidden
+// units 256 s .. + 255) and output column block c = w % 32 (columns 16 c .. + 15):
+//  (0) every lane issues its W2 chunks first (they do not depend on phase 1);
+//  (1) c < 16: hidden columns 256 s + 16 c .. + 15 -- the skinny FFN1 body (4 waves split
+//      K = 512, NCH 4) -- relu(. + b1) stored to `hidden`, then count[s] += 1;
+//  (2) every work group waits for count[s] == 16 (the producers of its K slice), then runs the
+//      skinny split-K body (NCH 2) on hidden[:, 256 s ..] and stores its slab columns,
+//      done[s] += 1;
+//  (3) work groups 0 .. m/4 - 1 wait for done[0..7] == 32 and combine one row per wave
+//      (ln_combine_vals<8>, as tt2_ln_combine).
+// A work group only ever waits for work groups of lower index (and the phase-3 ones, at most
+// 16, for all), so in-order dispatch makes progress even when the grid is not resident at once.
+// Cross-XCD visibility without cache maintenance: the hidden row and the slabs are stored
+// with agent-coherent (sc1, L2 write-through) stores, every wave waits for its stores'
+// acknowledgements before the work group's barrier and counter increment, and the readers
+// load them with sc1 buffer loads, which do not hit a stale L2 / L1 line.  (Agent-scope fences
+// instead -- an L2 write-back per producer and an L2 invalidate per waiter, 32 of each per XCD
+// per phase -- made the launch 2x slower than the three launches it replaces.)  The last
+// work group to leave re-arms the counters for the next launch.  A spin gives up after
+// FFN_SPIN_TICKS of the 100 MHz wall clock and raises sync[FFN_ERR].
+// Measured (tools/ffn_decode_ab.py, per-work-group stamps): each hand-off -- the producers'
+// stores acknowledged, the counter increment, the waiter's poll seeing it -- costs 1.3-2.3 us,
+// about what a launch boundary inside a graph costs, so the launch is 0.6-1.2 us SLOWER than
+// the three it replaces (10.9-11.3 vs 10.3 us per layer at m = 32).  Opt-in (decode schedule 4).
+// =====================================================================================
+constexpr int FFN_D = 512, FFN_F = 2048, FFN_WG = 256;
+constexpr uint64_t FFN_SPIN_TICKS = 2000000;   // 20 ms
+// counter i at sync[64 i] (256 B apart): count[s] (16 producers each), done[s] (the 32 slab
+// writers of split s: one counter per split, since 256 increments of one word serialise at its
+// atomic unit for ~3.5 us), exit, err
+enum { FFN_LINE = 64, FFN_DONE = 8, FFN_EXIT = 16, FFN_ERR = 17, FFN_NCTR = 18 };
+static_assert(FFN_NCTR * FFN_LINE <= TT2_FFN_SYNC_INTS && FFN_ERR * FFN_LINE == TT2_FFN_SYNC_ERR, "sync words");
+// how a phase's data reaches the next phase's readers (measurement builds): 0 sc1 stores and
+// sc1 loads; 1 plain stores, an agent-scope release (L2 write-back) per producer, sc1 loads;
+// 2 plain stores and loads, no cache maintenance (WRONG results across XCDs: timing floor only)
+#ifndef FFN_SYNC
+#define FFN_SYNC 0
+#endif
+#ifndef FFN_SLEEP
+#define FFN_SLEEP 1
+#endif
+
+template <typename TE> struct FfnArgs {
+  const TE* x; const TE* w1; const float* b1; const TE* w2; const float* b2;
+  const float* gamma; const float* beta;
+  TE* hid; float* slab; int32_t* sync; TE* y;
+  int M;
+  float eps;
+  uint64_t* stamps;   // optional [256][8] wall-clock stamps per work group (tt2_ffn_decode_stamps)
+};
+#define FFN_STAMP(k) \
+  if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (k)] = wall_clock64()
+
+// every wave: its sc1 stores acknowledged, then the work group's barrier; thread 0 counts
+TT2_DEV void ffn_arrive(int32_t* ctr) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // keeps the stores above (compiler)
+  __builtin_amdgcn_s_waitcnt(0);                            // vmcnt(0): this wave's stores done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#if FFN_SYNC == 1
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+    __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+template <typename T> TT2_DEV void ffn_st(T* p, T v) {
+#if FFN_SYNC == 0
+  typedef __attribute__((ext_vector_type(1))) unsigned short u16v;
+  if constexpr (sizeof(T) == 2)
+    __hip_atomic_store(reinterpret_cast<uint16_t*>(p), __builtin_bit_cast(uint16_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  else
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
+// 16-B agent-coherent load (sc1) of p (16-B aligned, within 2 GB of base)
+TT2_DEV uint4 ld_sc1(__amdgpu_buffer_rsrc_t rs, const void* base, const void* p) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+      rs, (int)(reinterpret_cast<const char*>(p) - reinterpret_cast<const char*>(base)), 0, FFN_SYNC == 2 ? 0 : 16);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+TT2_DEV __amdgpu_buffer_rsrc_t ffn_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+// thread 0; the work group's barrier follows.  Waits until ctr[i * FFN_LINE] >= target for
+// i < n; the clock and the error word are checked every 16th poll only (a poll is one
+// agent-coherent load round trip)
+TT2_DEV void ffn_wait(int32_t* ctr, int n, int target, int32_t* err) {
+  const uint64_t t0 = wall_clock64();
+  for (int it = 1;; ++it) {
+    int lo = target;   // every counter's load in flight at once
+    for (int i = 0; i < n; ++i)
+      lo = min(lo, __hip_atomic_load(ctr + i * FFN_LINE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (lo >= target) break;
+    if ((it & 15) == 0) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+      if (wall_clock64() - t0 > FFN_SPIN_TICKS) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_s_sleep(FFN_SLEEP);
+  }
+}
+
+template <typename TE, int MR>
+__global__ __launch_bounds__(NT) void ffn_decode_kernel(FfnArgs<TE> a) {
+  typedef typename SkT<TE>::V V8;
+  union U { uint4 u; V8 v; };
+  __shared__ float red[4][16 * MR][SK_COLS + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  const int s = blockIdx.x >> 5, c = blockIdx.x & 31;
+  const int ecol = threadIdx.x & 15, erow = threadIdx.x >> 4;
+  const int M = a.M;
+  FFN_STAMP(0);
+  const TE* xr[MR];
+  const TE* hr[MR];
+  bool rok[MR];
+#pragma unroll
+  for (int q = 0; q < MR; ++q) {
+    rok[q] = 16 * q + r < M;
+    xr[q] = a.x + (int64_t)(rok[q] ? 16 * q + r : 0) * FFN_D;
+    hr[q] = a.hid + (int64_t)(rok[q] ? 16 * q + r : 0) * FFN_F;
+  }
+  // (0) phase 2's W2 slice: output column 16 c + r, k = 256 s + 64 wave + 32 cc + 8 g
+  const int k2 = s * 256 + wave * 64 + 8 * g;
+  U w2[2];
+  {
+    const TE* wrow = a.w2 + (int64_t)(c * SK_COLS + r) * FFN_F + k2;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) w2[cc].u = *reinterpret_cast<const uint4*>(wrow + 32 * cc);
+  }
+  if (c < 16) {
+    // (1) hidden column 256 s + 16 c + r, k = 128 wave + 32 cc + 8 g
+    const int n1 = s * 256 + c * SK_COLS;
+    const int k1 = wave * 128 + 8 * g;
+    U w1[4], a1[MR][4];
+    const TE* wrow = a.w1 + (int64_t)(n1 + r) * FFN_D + k1;
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) w1[cc].u = *reinterpret_cast<const uint4*>(wrow + 32 * cc);
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+      for (int q = 0; q < MR; ++q)
+        a1[q][cc].u = *reinterpret_cast<const uint4*>(rok[q] ? (const void*)(xr[q] + k1 + 32 * cc)
+                                                              : (const void*)g_zero_page);
+    const float e_bias = a.b1[n1 + ecol];
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc[MR];
+#pragma unroll
+    for (int q = 0; q < MR; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+      for (int q = 0; q < MR; ++q) acc[q] = SkT<TE>::mma(a1[q][cc].v, w1[cc].v, acc[q]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < MR; ++q) red[wave][16 * q + 4 * g + i][r] = acc[q][i];
+    __syncthreads();
+#pragma unroll
+    for (int hrow = 0; hrow < MR; ++hrow) {
+      const int m = erow + 16 * hrow;
+      if (m < M) {
+        // the skinny epilogue's expression: relu(alpha v + bias + residual 0) + pe 0, alpha 1
+        const float v = (red[0][m][ecol] + red[1][m][ecol]) + (red[2][m][ecol] + red[3][m][ecol]);
+        float y = 1.f * v + e_bias + 0.f;
+        y = fmaxf(y * 1.f, 0.f);
+        y += 0.f;
+        ffn_st(a.hid + (int64_t)m * FFN_F + n1 + ecol, (TE)y);
+      }
+    }
+    FFN_STAMP(1);
+    ffn_arrive(a.sync + FFN_LINE * s);
+    FFN_STAMP(2);
+  }
+  // (2) the K slice 256 s .. + 255 of hidden once its 16 producers are done
+  if (threadIdx.x == 0) ffn_wait(a.sync + FFN_LINE * s, 1, 16, a.sync + FFN_LINE * FFN_ERR);
+  __syncthreads();
+  FFN_STAMP(3);
+  {
+    const __amdgpu_buffer_rsrc_t hrs = ffn_rsrc(a.hid);
+    U a2[MR][2];
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int q = 0; q < MR; ++q)   // rows past m read row 0 and are not stored
+        a2[q][cc].u = ld_sc1(hrs, a.hid, hr[q] + k2 + 32 * cc);
+    f32x4 acc[MR];
+#pragma unroll
+    for (int q = 0; q < MR; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int q = 0; q < MR; ++q) acc[q] = SkT<TE>::mma(a2[q][cc].v, w2[cc].v, acc[q]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < MR; ++q) red[wave][16 * q + 4 * g + i][r] = acc[q][i];
+    __syncthreads();
+#pragma unroll
+    for (int hrow = 0; hrow < MR; ++hrow) {
+      const int m = erow + 16 * hrow;
+      if (m < M)
+        ffn_st(a.slab + ((int64_t)s * M + m) * FFN_D + c * SK_COLS + ecol,
+               (red[0][m][ecol] + red[1][m][ecol]) + (red[2][m][ecol] + red[3][m][ecol]));
+    }
+    FFN_STAMP(4);
+    ffn_arrive(a.sync + FFN_LINE * (FFN_DONE + s));
+    FFN_STAMP(5);
+  }
+  // (3) one row per wave once every slab is written
+  if ((int)blockIdx.x < (M + 3) / 4) {
+    if (threadIdx.x == 0) ffn_wait(a.sync + FFN_LINE * FFN_DONE, 8, 32, a.sync + FFN_LINE * FFN_ERR);
+    __syncthreads();
+    FFN_STAMP(6);
+    const int row = blockIdx.x * 4 + wave;
+    if (row < M) {
+      // ln_combine_row<8> with the slabs read agent-coherently
+      const __amdgpu_buffer_rsrc_t srs = ffn_rsrc(a.slab);
+      const int c0 = lane * 8;
+      float v[8], p[8][8], bb[8], gm[8], be[8], o[8];
+      ld8f(a.x + (int64_t)row * FFN_D + c0, v);
+#pragma unroll
+      for (int sl = 0; sl < 8; ++sl) {
+        const float* ps = a.slab + ((int64_t)sl * M + row) * FFN_D + c0;
+        const uint4 u0 = ld_sc1(srs, a.slab, ps), u1 = ld_sc1(srs, a.slab, ps + 4);
+        p[sl][0] = __uint_as_float(u0.x); p[sl][1] = __uint_as_float(u0.y);
+        p[sl][2] = __uint_as_float(u0.z); p[sl][3] = __uint_as_float(u0.w);
+        p[sl][4] = __uint_as_float(u1.x); p[sl][5] = __uint_as_float(u1.y);
+        p[sl][6] = __uint_as_float(u1.z); p[sl][7] = __uint_as_float(u1.w);
+      }
+      ld8f(a.b2 + c0, bb);
+      ld8f(a.gamma + c0, gm);
+      ld8f(a.beta + c0, be);
+      ln_combine_vals<8>(v, p, bb, gm, be, a.eps, o);
+      typedef TE t8 __attribute__((ext_vector_type(8)));
+      t8 yv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) yv[j] = (TE)o[j];
+      *reinterpret_cast<t8*>(a.y + (int64_t)row * FFN_D + lane * 8) = yv;
+    }
+  }
+  // every wait of this work group is behind it: the last one out re-arms the counters
+  FFN_STAMP(7);
+  if (threadIdx.x == 0) {
+    const int prev =
+        __hip_atomic_fetch_add(a.sync + FFN_LINE * FFN_EXIT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == FFN_WG - 1) {
+#pragma unroll
+      for (int i = 0; i < FFN_ERR; ++i)
+        __hip_atomic_store(a.sync + FFN_LINE * i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 template <bool AK, bool BKC>
 hipError_t launch2(const OpDesc& A, const OpDesc& B, const EpiParams& E, int M, int N, int K, int splits, float* ws,
                    hipStream_t s) {
@@ -3065,4 +3327,45 @@ extern "C" void tt2_probe_reset(void) {
   }
   g_probe.clear();
   g_probe_armed = -1;
+}
+
+// The decode step's FFN sublayer in one launch (ffn_decode_kernel above).
+static int ffn_decode(const tt2_ffn_decode_args* a, uint64_t* stamps, hipStream_t s) {
+  if (!a) return tt2_set_error(TT2_E_INVALID, "tt2_ffn_decode: null arguments");
+  if (a->m <= 0) return TT2_OK;
+  if (a->m > 64 || a->d_model != FFN_D || a->d_ffn != FFN_F)
+    return tt2_set_error(TT2_E_INVALID, "tt2_ffn_decode: m <= 64, d_model 512 and d_ffn 2048");
+  if (a->dtype != TT2_DT_BF16 && a->dtype != TT2_DT_F16)
+    return tt2_set_error(TT2_E_INVALID, "tt2_ffn_decode: dtype bf16 or f16");
+  if (!a->x || !a->w1 || !a->b1 || !a->w2 || !a->b2 || !a->gamma || !a->beta || !a->hidden || !a->slab ||
+      !a->sync || !a->y)
+    return tt2_set_error(TT2_E_INVALID, "tt2_ffn_decode: null buffer");
+  const void* vec[] = {a->x, a->w1, a->w2, a->hidden, a->y, a->slab, a->gamma, a->beta, a->b1, a->b2};
+  for (const void* p : vec)
+    if (reinterpret_cast<uintptr_t>(p) % 16)
+      return tt2_set_error(TT2_E_INVALID, "tt2_ffn_decode: buffers must be 16-B aligned");
+  if (reinterpret_cast<uintptr_t>(a->sync) % 4) return tt2_set_error(TT2_E_INVALID, "tt2_ffn_decode: sync alignment");
+#define TT2_FFN(TE, MR)                                                                                             \
+  {                                                                                                                 \
+    FfnArgs<TE> f{reinterpret_cast<const TE*>(a->x), reinterpret_cast<const TE*>(a->w1), a->b1,                  \
+                  reinterpret_cast<const TE*>(a->w2), a->b2, a->gamma, a->beta, reinterpret_cast<TE*>(a->hidden), \
+                  a->slab, a->sync, reinterpret_cast<TE*>(a->y), a->m, a->eps, stamps};                          \
+    hipLaunchKernelGGL((ffn_decode_kernel<TE, MR>), dim3(FFN_WG), dim3(NT), 0, s, f);                           \
+  }
+  if (a->dtype == TT2_DT_F16) {
+    if (a->m <= 32) TT2_FFN(f16, 2) else TT2_FFN(f16, 4)
+  } else {
+    if (a->m <= 32) TT2_FFN(bf16, 2) else TT2_FFN(bf16, 4)
+  }
+#undef TT2_FFN
+  return tt2_check_launch(hipGetLastError(), "tt2_ffn_decode");
+}
+
+extern "C" int tt2_ffn_decode(const tt2_ffn_decode_args* a, hipStream_t s) { return ffn_decode(a, nullptr, s); }
+
+// Measurement hook: tt2_ffn_decode that also writes 8 wall-clock stamps per work group to
+// stamps[256][8] (entry, hidden stored, hidden counted, K slice ready, slab stored, slab
+// counted, rows ready, exit).
+extern "C" int tt2_ffn_decode_stamps(const tt2_ffn_decode_args* a, uint64_t* stamps, hipStream_t s) {
+  return ffn_decode(a, stamps, s);
 }

@@ -177,19 +177,14 @@ template <typename T> TT2_DEV void ld8f(const T* p, float (&v)[8]) {
 // The decode step's residual combine + LayerNorm of one 512-wide row by one wave (lane =
 // 8-column chunk c0 = 8 lane): y = LN(x + (bias + sum_s part[s])) with the slab sum in fixed
 // order.  tt2_ln_combine and the cross-attention launch's fused prologue both call it, so
-// the two round identically.  part: this row's slab 0 (slabs part_stride floats apart).
-template <int S, typename T>
-TT2_DEV void ln_combine_row(const T* x, const float* part, int64_t part_stride, const float* bias,
-                            const float* gamma, const float* beta, float eps, int lane, float (&o)[8]) {
+// the two round identically (and tt2_ffn_decode, through ln_combine_vals: the same arithmetic
+// on values it loads itself).  part: this row's slab 0 (slabs part_stride floats apart).
+// ln_combine_vals: v = this lane's 8 x (overwritten), p its 8 columns of each slab, bb / g / be
+// bias, gamma, beta.
+template <int S>
+TT2_DEV void ln_combine_vals(float (&v)[8], const float (&p)[S][8], const float (&bb)[8], const float (&g)[8],
+                             const float (&be)[8], float eps, float (&o)[8]) {
   constexpr int C = 512;
-  const int c0 = lane * 8;
-  float v[8], p[S][8], bb[8], g[8], be[8];
-  ld8f(x + c0, v);
-#pragma unroll
-  for (int s = 0; s < S; ++s) ld8f(part + s * part_stride + c0, p[s]);
-  ld8f(bias + c0, bb);
-  ld8f(gamma + c0, g);
-  ld8f(beta + c0, be);
   float sum = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -206,6 +201,19 @@ TT2_DEV void ln_combine_row(const T* x, const float* part, int64_t part_stride, 
   const float rstd = rsqrtf(wave_sum(sq) / C + eps);
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = (v[j] - mean) * rstd * g[j] + be[j];
+}
+template <int S, typename T>
+TT2_DEV void ln_combine_row(const T* x, const float* part, int64_t part_stride, const float* bias,
+                            const float* gamma, const float* beta, float eps, int lane, float (&o)[8]) {
+  const int c0 = lane * 8;
+  float v[8], p[S][8], bb[8], g[8], be[8];
+  ld8f(x + c0, v);
+#pragma unroll
+  for (int s = 0; s < S; ++s) ld8f(part + s * part_stride + c0, p[s]);
+  ld8f(bias + c0, bb);
+  ld8f(gamma + c0, g);
+  ld8f(beta + c0, be);
+  ln_combine_vals<S>(v, p, bb, g, be, eps, o);
 }
 
 TT2_DEV float wave_max(float v) {

@@ -299,8 +299,18 @@ class DecodeDesc(C.Structure):
     ]
 
 
+class FfnDecodeArgs(C.Structure):
+    _fields_ = [
+        ("x", vp), ("w1", vp), ("b1", vp), ("w2", vp), ("b2", vp), ("gamma", vp), ("beta", vp),
+        ("hidden", vp), ("slab", vp), ("sync", vp), ("y", vp),
+        ("m", i32), ("d_model", i32), ("d_ffn", i32), ("dtype", i32), ("eps", f32),
+    ]
+
+
 SIGNATURES.update({
     "tt2_attn_decode": ([C.POINTER(AttnDecodeArgs), vp], C.c_int),
+    "tt2_ffn_decode": ([C.POINTER(FfnDecodeArgs), vp], C.c_int),
+    "tt2_ffn_decode_stamps": ([C.POINTER(FfnDecodeArgs), vp, vp], C.c_int),
     "tt2_kv_append": ([vp, i64, vp, i64, i64, C.c_int, C.c_int, vp, C.c_int, vp], C.c_int),
     "tt2_decode_emit": ([vp, i64, C.c_int, C.c_int, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp, vp, f32, vp], C.c_int),
     "tt2_decode_workspace_size": ([C.POINTER(DecodeDesc)], sz),

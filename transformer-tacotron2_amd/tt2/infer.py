@@ -31,6 +31,8 @@ from ._lib import check, dt, lib, stream_ptr
 from .engine import TTSEngine
 
 SCHEDULE_AUTO, SCHEDULE_PLAIN, SCHEDULE_SPLIT = 0, 1, 2
+SCHEDULE_SPLIT_UNFUSED = 3   # split-K, the attention launches without the fused projections
+SCHEDULE_SPLIT_FFN1 = 4      # split-K, each FFN sublayer in one tt2_ffn_decode launch (opt-in: slower)
 STOP_FORCE = 1e4   # |injected stop logit|: dominates any logit the heads produce
 
 
@@ -70,6 +72,9 @@ class Decoder:
         self.dd = cd
         if cd == torch.float16 and (e.cd != torch.bfloat16 or batch > 64):
             raise ValueError("f16 decode needs a bf16 engine and batch <= 64 (the skinny decode kernels)")
+        # TT2_DEC_SCHEDULE (dev knob, A/B runs): overrides the default schedule
+        if schedule == SCHEDULE_AUTO and os.environ.get("TT2_DEC_SCHEDULE"):
+            schedule = int(os.environ["TT2_DEC_SCHEDULE"])
         self.schedule = schedule
         # steps per decode graph launch (tt2_decode_graph_create_n; TT2_DEC_GRAPH_STEPS): one
         # graph boundary per 8 frames, +0.6-1.2 % frames/s over one per frame

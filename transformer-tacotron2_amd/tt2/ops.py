@@ -371,6 +371,22 @@ def ln_combine(x, part, splits, bias, gamma, beta, y, m, eps=1e-5):
           "tt2_ln_combine")
 
 
+def ffn_decode(x, w1, b1, w2, b2, gamma, beta, hidden, slab, sync, y, m, eps=1e-5, stamps=None):
+    """The decode step's FFN sublayer in one launch (tt2_ffn_decode): y = LN(x + b2 + relu(x W1^T +
+    b1) W2^T), hidden = relu(x W1^T + b1), slab = the 8 raw FFN2 partial slabs; sync: int32 [2048],
+    zero before the first call (each call leaves it zero; sync[1088] != 0 flags a timed-out phase).
+    stamps (int64 [256, 8], optional): per-work-group wall-clock stamps (tt2_ffn_decode_stamps)."""
+    a = _lib.FfnDecodeArgs()
+    a.x, a.w1, a.b1, a.w2, a.b2 = x.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr()
+    a.gamma, a.beta, a.hidden, a.slab = gamma.data_ptr(), beta.data_ptr(), hidden.data_ptr(), slab.data_ptr()
+    a.sync, a.y = sync.data_ptr(), y.data_ptr()
+    a.m, a.d_model, a.d_ffn, a.dtype, a.eps = m, x.shape[-1], w1.shape[0], dt(x), eps
+    if stamps is None:
+        check(lib().tt2_ffn_decode(C.byref(a), stream_ptr()), "tt2_ffn_decode")
+    else:
+        check(lib().tt2_ffn_decode_stamps(C.byref(a), stamps.data_ptr(), stream_ptr()), "tt2_ffn_decode")
+
+
 def layernorm_bwd(dy, x, branch, gamma, mean, rstd, dx, dbranch, dgamma, dbeta, m, drop: Drop = NO_DROP,
                   ws: Workspace | None = None, dbias=None, part=None, defer=False, prev=None):
     """dx = d(LN)/ds, dbranch = drop-masked dx, gamma/beta grads, and optionally
