@@ -2123,6 +2123,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef G8_LOADERS   // loader waves: 4 (2 copies per operand per wave and step) or 8 (1).  8: the
 #define G8_LOADERS 8  // LDS-DMA issue rate, not the bytes in flight, bounded the K step
 #endif
+#ifndef G8_SPB   // K steps per barrier (64 deep each): 2 or 4 make the barrier cadence 128 / 256 deep
+#define G8_SPB 1
+#endif
+static_assert(G8_RING > G8_SPB && G8_RING % G8_SPB == 0, "v8 ring: whole barrier groups, one ahead at least");
 constexpr int G8_LW = G8_LOADERS, G8_PC = 8 / G8_LW;   // copies per operand tile per loader wave
 constexpr int G8_NT = 64 * (4 + G8_LW), G8_STAGES = G8_RING;   // 4 MFMA waves + the loader waves
 constexpr int G8_EPI = 512;   // threads of the C image store / fused statistics (64 rows x 8 chunks)
@@ -2295,8 +2299,8 @@ __global__ __launch_bounds__(G8_NT, G8_STAGES <= 4 ? 2 : 1) void gemm8_kernel(Op
       else g8_issue<true>(A, st, m0, 64 * t, lane, lw);
       g8_issue<BKC>(B, st + G8_TILE, n0, 64 * t, lane, lw);
     };
-    // G8_STAGES - 1 steps ahead; each step is 4 copies per loader wave
-    constexpr int AH = G8_STAGES - 1;
+    // G8_STAGES - G8_SPB steps ahead; each step is 2 G8_PC copies per loader wave
+    constexpr int AH = G8_STAGES - G8_SPB;
     auto wait_ahead = [](int ahead) {   // step t+1 landed, `ahead` later steps may stay in flight
       switch (ahead * 2 * G8_PC) {        // copies per step and wave: 2 G8_PC
         case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
@@ -2313,12 +2317,14 @@ __global__ __launch_bounds__(G8_NT, G8_STAGES <= 4 ? 2 : 1) void gemm8_kernel(Op
       }
     };
     for (int t = 0; t < AH && t < nkt; ++t) issue(t);
-    wait_ahead(min(AH, nkt) - 1);   // step 0 landed
+    wait_ahead(min(AH, nkt) - G8_SPB);   // steps 0 .. G8_SPB - 1 landed
     __builtin_amdgcn_s_barrier();
-    for (int t = 0; t < nkt; ++t) {
-      if (t + AH < nkt) issue(t + AH);   // into the stage step t-1 used: free since the last barrier
-      wait_ahead(min(AH - 1, nkt - 2 - t));
-      __builtin_amdgcn_s_barrier();    // step t+1 landed
+    for (int t = 0; t < nkt; t += G8_SPB) {
+#pragma unroll
+      for (int j = 0; j < G8_SPB; ++j)   // into the stages steps t - G8_SPB .. t - 1 used: free since the last barrier
+        if (t + AH + j < nkt) issue(t + AH + j);
+      wait_ahead(min(AH - G8_SPB, nkt - 2 * G8_SPB - t));
+      __builtin_amdgcn_s_barrier();    // steps t + G8_SPB .. t + 2 G8_SPB - 1 landed
     }
   } else {   // ------------------------------------------------------- MFMA waves
     const int wm = wave >> 1, wn = wave & 1;
@@ -2326,16 +2332,21 @@ __global__ __launch_bounds__(G8_NT, G8_STAGES <= 4 ? 2 : 1) void gemm8_kernel(Op
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     __builtin_amdgcn_s_barrier();
-    for (int t = 0; t < nkt; ++t) {
-      const char* sa = smem + (t & (G8_STAGES - 1)) * G8_STAGE;
-      const char* sb = sa + G8_TILE;
+    for (int t0 = 0; t0 < nkt; t0 += G8_SPB) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 fa = g8_frag_kc(sa, wm * 32 + (lane & 31), s, hi);
-        const bf16x8 fb = BKC ? g8_frag_kc(sb, wn * 32 + (lane & 31), s, hi) : g8_frag_mc(sb, wn * 32, s, lane);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb, fa, acc, 0, 0, 0);   // D[n][m]
+      for (int j = 0; j < G8_SPB; ++j) {
+        const int t = t0 + j;
+        if (G8_SPB > 1 && t >= nkt) break;
+        const char* sa = smem + (t & (G8_STAGES - 1)) * G8_STAGE;
+        const char* sb = sa + G8_TILE;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 fa = g8_frag_kc(sa, wm * 32 + (lane & 31), s, hi);
+          const bf16x8 fb = BKC ? g8_frag_kc(sb, wn * 32 + (lane & 31), s, hi) : g8_frag_mc(sb, wn * 32, s, lane);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb, fa, acc, 0, 0, 0);   // D[n][m]
+        }
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this stage's reads retired before it is re-filled
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // these stages' reads retired before they are re-filled
       __builtin_amdgcn_s_barrier();
     }
     // lane holds C[m0 + 32 wm + (lane & 31)][n0 + 32 wn + (r & 3) + 8 (r >> 2) + 4 hi]; the
