@@ -376,6 +376,11 @@ def ffn_decode(x, w1, b1, w2, b2, gamma, beta, hidden, slab, sync, y, m, eps=1e-
     b1) W2^T), hidden = relu(x W1^T + b1), slab = the 8 raw FFN2 partial slabs; sync: int32 [2048],
     zero before the first call (each call leaves it zero; sync[1088] != 0 flags a timed-out phase).
     stamps (int64 [256, 8], optional): per-work-group wall-clock stamps (tt2_ffn_decode_stamps)."""
+    if sync.dtype != torch.int32 or sync.numel() < 2048:
+        raise ValueError("ffn_decode: sync must be an int32 tensor of at least TT2_FFN_SYNC_INTS (2048) words")
+    for t in (x, w1, w2, hidden, y, slab):
+        if not t.is_contiguous():
+            raise ValueError("ffn_decode: x, w1, w2, hidden, slab and y must be contiguous (packed rows)")
     a = _lib.FfnDecodeArgs()
     a.x, a.w1, a.b1, a.w2, a.b2 = x.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr()
     a.gamma, a.beta, a.hidden, a.slab = gamma.data_ptr(), beta.data_ptr(), hidden.data_ptr(), slab.data_ptr()
