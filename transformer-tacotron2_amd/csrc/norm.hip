@@ -155,13 +155,16 @@ __global__ __launch_bounds__(NT) void ln_fwd_kernel(LnArgs a) {
 // 512 columns of a row, where part holds the raw partial sums of a skinny split-K
 // projection ([S][M][512] f32).  One wave per row, every load (x, the S slabs, bias,
 // gamma, beta) issued before the first reduction: one memory round trip.
+#ifndef LNC_ROWS
+#define LNC_ROWS 1   // rows (waves) per work group: one row per CU reads its 8 slabs faster than 4 (r06zp)
+#endif
 template <int S, typename T>
-__global__ __launch_bounds__(NT) void ln_combine_kernel(const T* x, const float* part, const float* bias,
-                                                        const float* gamma, const float* beta, T* y, int M,
-                                                        float eps) {
+__global__ __launch_bounds__(64 * LNC_ROWS) void ln_combine_kernel(const T* x, const float* part, const float* bias,
+                                                                   const float* gamma, const float* beta, T* y, int M,
+                                                                   float eps) {
   constexpr int C = 512;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = blockIdx.x * LNC_ROWS + (threadIdx.x >> 6);
   if (row >= M) return;
   float o[8];
   ln_combine_row<S, T>(x + (int64_t)row * C, part + (int64_t)row * C, (int64_t)M * C, bias, gamma, beta, eps, lane,
@@ -862,13 +865,13 @@ extern "C" int tt2_ln_combine(const void* x, const float* part, int32_t splits, 
   if (!x || !part || !bias || !gamma || !beta || !y) return tt2_set_error(TT2_E_INVALID, "tt2_ln_combine: null");
   if (dtype != TT2_DT_BF16 && dtype != TT2_DT_F16) return tt2_set_error(TT2_E_INVALID, "tt2_ln_combine: bf16 / f16");
   if (m <= 0) return TT2_OK;
-  const dim3 g((m + 3) / 4);
+  const dim3 g((m + LNC_ROWS - 1) / LNC_ROWS), b(64 * LNC_ROWS);
 #define TT2_LNC(S)                                                                                             \
   if (dtype == TT2_DT_F16)                                                                                     \
-    hipLaunchKernelGGL((ln_combine_kernel<S, f16>), g, dim3(NT), 0, s, (const f16*)x, part, bias, gamma, beta,  \
+    hipLaunchKernelGGL((ln_combine_kernel<S, f16>), g, b, 0, s, (const f16*)x, part, bias, gamma, beta,        \
                        (f16*)y, m, eps);                                                                       \
   else                                                                                                         \
-    hipLaunchKernelGGL((ln_combine_kernel<S, bf16>), g, dim3(NT), 0, s, (const bf16*)x, part, bias, gamma, beta, \
+    hipLaunchKernelGGL((ln_combine_kernel<S, bf16>), g, b, 0, s, (const bf16*)x, part, bias, gamma, beta,      \
                        (bf16*)y, m, eps);
   switch (splits) {
     case 1: TT2_LNC(1) break;
